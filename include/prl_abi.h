@@ -1,0 +1,172 @@
+/*
+ * prl_abi.h — C-ABI of libprl_hip.so, the MI355X (gfx950) hot path of the PPO rollout + update
+ * engine that drops in under Raven4567/Parallel-Reinforcement-Learning's Python API.
+ *
+ * The reference has no FFI: its boundary is the duck-typed Python API of `AsyncTools.AsyncPPO`
+ * and `PPO.PPO`.  Every entry point below replaces one piece of that Python code
+ * and cites the reference lines (paths relative to the reference repository root).  The Python
+ * packages `PPO/` and `AsyncTools/` in this repository bind these symbols with ctypes
+ * (see INTEGRATION.md for the stub a maintainer of the reference would add).
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a caller-owned DEVICE pointer unless the comment says "host";
+ *   - nothing allocates: scratch comes in through `workspace` (size from prl_workspace_bytes);
+ *   - every call is asynchronous on `stream` (a hipStream_t passed as void*; NULL = null stream)
+ *     and contains no host synchronisation, so callers may capture it into a hipGraph;
+ *   - return 0 on success, a negative prl_status on failure; prl_last_error() then holds a
+ *     thread-local message.  Python wrappers raise RuntimeError with that message.
+ *   - not re-entrant per env batch; one host thread per GPU.
+ */
+#ifndef PRL_ABI_H
+#define PRL_ABI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PRL_ABI_VERSION 1
+
+enum prl_status {
+  PRL_OK = 0,
+  PRL_ERR_ARG = -1,     /* bad argument (shape, alignment, null pointer) */
+  PRL_ERR_HIP = -2,     /* a HIP runtime call failed */
+  PRL_ERR_TIMEOUT = -3  /* an in-kernel bounded spin gave up (never expected) */
+};
+
+enum prl_env_kind {
+  PRL_ENV_CARTPOLE = 0,        /* gymnasium CartPole-v1 + TimeLimit(500), discrete(2), obs 4  */
+  PRL_ENV_PENDULUM = 1,        /* gymnasium Pendulum-v1 + TimeLimit(200), continuous(1), obs 3 */
+  PRL_ENV_SYNTH_HUMANOID = 2   /* synthetic Humanoid-v5-shaped env: obs 348, act 17, cont.    */
+};
+
+enum prl_op {
+  PRL_OP_GAE = 0,        /* n = transitions                 */
+  PRL_OP_SURROGATE = 1,  /* n = minibatch size              */
+  PRL_OP_SCAN = 2,       /* n = elements (scan/compaction)  */
+  PRL_OP_STATS = 3       /* n = elements (prl_adv_stats)    */
+};
+
+/* ---- housekeeping ------------------------------------------------------------------------- */
+int prl_abi_version(void);
+const char* prl_last_error(void);
+/* Bytes of device workspace an op needs for n elements (host call, no GPU work). */
+int64_t prl_workspace_bytes(int op, int64_t n);
+/* Host call: static geometry of an env kind (AsyncPPO.py:45-46 action_space/observation_space). */
+int prl_env_dims(int kind, int* obs_dim, int* act_dim, int* phys_dim, int* max_episode_steps,
+                 int* is_discrete);
+
+/* ---- environments (replace EnvVectorizer + gymnasium envs) --------------------------------- */
+/* Seed per-env PCG64 generators exactly as numpy's SeedSequence(seed_e) -> PCG64 does, i.e. as
+ * gymnasium's `env.reset(seed=seed_e)` seeds `env.np_random` (gymnasium.utils.seeding.np_random).
+ * rng[E][4] u64 = {state_hi, state_lo, inc_hi, inc_lo}.  Replaces the per-env RNG that each
+ * deep-copied env carries (AsyncTools/AsyncPPO.py:39). */
+int prl_pcg64_seed(const uint64_t* seeds, int64_t E, uint64_t* rng, void* stream);
+
+/* EnvVectorizer.reset (AsyncTools/AsyncPPO.py:48-62): reset every env (or those with
+ * reset_mask[e] != 0 when reset_mask is non-NULL), clear envs_active (terminal[e] = 0),
+ * t_elapsed[e] = 0, write obs[e*obs_stride .. +D) f32.  phys[E][phys_dim] f64. */
+int prl_env_reset(int kind, int64_t E, double* phys, uint64_t* rng, int32_t* t_elapsed,
+                  uint8_t* terminal, const uint8_t* reset_mask, float* obs, int64_t obs_stride,
+                  void* stream);
+
+/* EnvVectorizer.step, compat form (AsyncTools/AsyncPPO.py:64-102): the i-th of the n active envs
+ * (env index active_idx[i], ascending) takes actions[i] (discrete: int64[n]; continuous: f32[n][A])
+ * and writes its results COMPACTED to row i: obs_out[n][D] f32, reward_out[n] f64,
+ * terminated_out[n] u8, truncated_out[n] u8 (TimeLimit).  Does not touch `terminal`. */
+int prl_env_step_compact(int kind, int64_t E, double* phys, int32_t* t_elapsed,
+                         const int64_t* active_idx, int64_t n, const void* actions,
+                         float* obs_out, double* reward_out, uint8_t* terminated_out,
+                         uint8_t* truncated_out, void* stream);
+
+/* One vector step of the device-resident AsyncPPO.worker (AsyncTools/AsyncPPO.py:120-141):
+ * fuses PPO.get_action's sampling (PPO/PPO.py:85-91), EnvVectorizer.step (:64-102),
+ * utils.buffer_append + VecMemory.push (utils.py:17-36, AsyncPPO.py:20-24),
+ * utils.update_active_environments_list (utils.py:38-43) and the score counters (:137-138).
+ * For every env e with terminal[e] == 0, with t = t_elapsed[e]:
+ *   dist row e (stride dist_stride floats): discrete -> probs[A]; continuous -> mu[A], std[A];
+ *   action sampled with Philox4x32-10 keyed by (sample_seed, e, t); continuous actions are
+ *   tanh(sample) * action_scaling;
+ *   traj_obs[t+1][e] = next obs, traj_act[t][e] = action (f32), traj_rew[t][e] = reward (f32),
+ *   traj_done[t][e] = terminated|truncated, terminal[e] = that, t_elapsed[e] = ep_len[e] = t+1.
+ * traj_obs row t must already hold the pre-step observation (reset writes row 0).
+ * active_after[step] += number of envs still non-terminal after this step; reward_sum[0] += sum
+ * of rewards (f64) — both must be zeroed by the caller before the rollout. */
+int prl_rollout_step(int kind, int64_t E, int32_t step, double* phys, int32_t* t_elapsed,
+                     uint8_t* terminal, const float* dist, int64_t dist_stride,
+                     float action_scaling, uint64_t sample_seed, int32_t t_max, float* traj_obs,
+                     float* traj_act, float* traj_rew, uint8_t* traj_done, int32_t* ep_len,
+                     int32_t* active_after, double* reward_sum, void* stream);
+
+/* ---- mask / compaction / flatten (replace AsyncTools/utils.py) ----------------------------- */
+/* utils.indexes_of_active_environments + number_of_active_environments (utils.py:3-7):
+ * idx_out[0..count) = ascending e with terminal[e] == 0; count_out[0] = count (int64). */
+int prl_active_indices(const uint8_t* terminal, int64_t E, int64_t* idx_out, int64_t* count_out,
+                       void* workspace, void* stream);
+/* utils.update_active_environments_list (utils.py:38-43): terminal[active[i]] = dones[i] for the
+ * n envs active before the call (ascending order), i.e. mask[where(~mask)] = dones. */
+int prl_mask_update(uint8_t* terminal, int64_t E, const uint8_t* dones, int64_t n,
+                    void* workspace, void* stream);
+/* utils.inactive_states_dropout (utils.py:14-15): dst = src[~drop] (row_bytes per row, order
+ * kept); count_out[0] = rows kept. */
+int prl_compact_rows(const void* src, int64_t rows, int64_t row_bytes, const uint8_t* drop,
+                     void* dst, int64_t* count_out, void* workspace, void* stream);
+/* Exclusive scan of episode lengths: offsets[0..E] (offsets[E] = N), int64. */
+int prl_exclusive_scan_i32(const int32_t* in, int64_t n, int64_t* offsets, void* workspace,
+                           void* stream);
+/* utils.buffer_to_target_buffer_transfer (utils.py:45-51): env-major concatenation of the
+ * time-major trajectory buffers: row offsets[e] + t of S/A/R/Dn <- traj[t][e] for t < len_e.
+ * traj_obs is [T+1][E][D], traj_act [T][E][Adim], traj_rew/traj_done [T][E]. */
+int prl_flatten_env_major(int64_t E, int32_t t_max, int32_t D, int32_t Adim,
+                          const int64_t* offsets, int64_t N, const float* traj_obs,
+                          const float* traj_act, const float* traj_rew,
+                          const uint8_t* traj_done, float* S, float* A, float* R, float* Dn,
+                          void* stream);
+
+/* ---- PPO.learn hot path -------------------------------------------------------------------- */
+/* PPO.compute_gae (PPO/PPO.py:107-120) + `advantages = returns - V` (:198), float32, evaluated in
+ * the reference's exact operation order (bit-exact for finite inputs).  next_value: device
+ * scalar, NULL -> V[n-1] (PPO.py:188).  adv may be NULL.  sums_out[2] (f64) receives
+ * {sum(adv), sum(adv^2)} when adv != NULL (for prl_adv_normalize / a cross-GPU all-reduce). */
+int prl_gae(const float* r, const float* d, const float* V, const float* next_value, int64_t n,
+            double gamma, double lam, float* ret, float* adv, double* sums_out,
+            void* workspace, int64_t workspace_bytes, void* stream);
+/* {sum, sum of squares} (f64) of x[n] (PPO.py:199 statistics). */
+int prl_adv_stats(const float* x, int64_t n, double* sums_out, void* workspace,
+                  int64_t workspace_bytes, void* stream);
+/* PPO.py:199: out = (x - mean) / (std_unbiased + eps), mean/std from sums[2] over `count`
+ * elements (count may exceed n when sums were all-reduced across GPUs). out may alias x. */
+int prl_adv_normalize(const float* x, int64_t n, const double* sums, double count, float eps,
+                      float* out, void* stream);
+
+/* PPO.learn's surrogate (PPO/PPO.py:225-249):
+ *   ratio = exp(clamp(logp - old_logp, -20, 20)); s1 = ratio*adv; s2 = clamp(ratio,1-clip,1+clip)*adv
+ *   loss  = mean(-min(s1, s2)) + vf_coef * SmoothL1(V, ret) - ent_coef * entropy   (scalar)
+ * and the gradient of `loss` w.r.t. logp and V (torch semantics: min tie splits 1/2-1/2, clamp
+ * passes gradient at inclusive bounds) into dlogp/dV (NULL = skip).  entropy: device scalar. */
+int prl_ppo_surrogate_fwd(const float* logp, const float* old_logp, const float* adv,
+                          const float* V, const float* ret, const float* entropy, int64_t mb,
+                          float clip, float vf_coef, float ent_coef, float* loss_out,
+                          float* dlogp, float* dV, void* workspace, int64_t workspace_bytes,
+                          void* stream);
+/* Backward of the above for an upstream gradient grad_out (device scalar):
+ * dlogp = grad_out * dlogp_unit, dV = grad_out * dV_unit. */
+int prl_ppo_surrogate_bwd(const float* grad_out, const float* dlogp_unit, const float* dV_unit,
+                          int64_t mb, float* dlogp, float* dV, void* stream);
+
+/* RND.compute_intrinsic_reward (PPO/RND.py:71-94): out[i] = beta * || pred(x_i) - target(x_i) ||_2
+ * with each net Linear(D,64)+b -> GroupNorm(8, 64, eps 1e-5) -> SiLU -> Linear(64,D)+b
+ * (RND.py:25-38).  Weights in torch layout: W1[64][D], b1[64], g[64], beta_gn[64], W2[D][64], b2[D].
+ * fp32 MFMA (v_mfma_f32_32x32x2_f32).  x[n][D] f32 row-major. */
+int prl_rnd_forward(const float* x, int64_t n, int32_t D,
+                    const float* t_w1, const float* t_b1, const float* t_gw, const float* t_gb,
+                    const float* t_w2, const float* t_b2,
+                    const float* p_w1, const float* p_b1, const float* p_gw, const float* p_gb,
+                    const float* p_w2, const float* p_b2, float beta, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PRL_ABI_H */

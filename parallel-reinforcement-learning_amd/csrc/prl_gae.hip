@@ -1,0 +1,437 @@
+// prl_gae.hip — GAE(lambda) reverse scan, advantage statistics and normalisation.
+//
+// Replaces PPO.compute_gae (PPO/PPO.py:107-120) and `advantages = returns - V;
+// (adv - mean) / (std + 1e-8)` (PPO.py:198-199).
+//
+// Bit-exactness.  The reference runs, over float32 numpy values (NumPy 2 / NEP 50: Python floats
+// are weak, so every step stays float32):
+//     delta = r[t] + gamma * nv * (1 - d[t]) - V[t]          ((r + ((gamma*nv)*(1-d))) - V)
+//     gae   = delta + gamma * lambda * (1 - d[t]) * gae      (gamma*lambda formed in float64)
+//     ret[t] = gae + V[t];  nv = V[t]
+// with gae = 0 and nv = V[-1] initially (PPO.py:110, :188).  A float32 affine recurrence is not
+// associative, so a parallel prefix over (c_t, delta_t) pairs would change the rounding.  Instead
+// the scan is parallel across SEGMENTS: wherever c_t = gamma*lambda*(1-d_t) == 0 (an episode end)
+// the recurrence restarts and everything to its left is independent of everything to its right.
+// Within a segment the recurrence is evaluated sequentially in the reference's order, so every
+// output is bit-identical for finite inputs (a non-finite carry would leak through 0*inf = NaN in
+// the reference; here the chain restarts at d = 1).
+//
+// Work decomposition (single pass, one launch):
+//   * a tile = 256 threads x 8 consecutive elements = 2048 elements, loaded with 16-B vector
+//     loads; delta_t and c_t are formed elementwise and staged in LDS;
+//   * each thread first finishes everything at or left of the LAST break in its own chunk, then
+//     resolves its tail from the nearest chunk to the right that has a break (LDS), re-evaluating
+//     break-free chunks in between sequentially;
+//   * tiles are claimed in REVERSE order from an atomic ticket, and a tile publishes its carry-out
+//     g[first element] as one 8-byte {tag, value} granule with a single agent-scope store (the
+//     data is the flag, MI355X guide Guideline 16 R2) as soon as it is known — before it waits.
+//     A tile whose tail runs into the next tile polls that tile's granule (relaxed agent-scope
+//     loads, bounded spin).  Tickets guarantee the waited-on tile has been dispatched, so the
+//     look-back chain always drains; with episodes shorter than a tile it is one hop long.
+//   * when adv is requested, each tile writes {sum adv, sum adv^2} (f64) and the last tile to
+//     arrive reduces all tiles IN TILE ORDER (deterministic) into sums_out (release fence ->
+//     counter -> acquire fence, Guideline 16 counter form).
+#include "prl_common.h"
+
+namespace prl {
+
+constexpr int GAE_THREADS = 256;
+constexpr int GAE_EPT = 8;
+constexpr int GAE_TILE = GAE_THREADS * GAE_EPT;
+constexpr unsigned GAE_SPIN_LIMIT = 1u << 26;
+
+struct GaeWs {
+  unsigned* ctrs;               // [0] ticket, [1] arrivals, [2] timeout flag, [3] pad
+  unsigned long long* gran;     // [ntiles] {tag << 32 | float bits}
+  double2* tile_sums;           // [ntiles]
+};
+
+__host__ __device__ inline int64_t gae_ntiles(int64_t n) { return (n + GAE_TILE - 1) / GAE_TILE; }
+inline int64_t gae_memset_bytes(int64_t ntiles) { return ((16 + 8 * ntiles) + 15) / 16 * 16; }
+inline int64_t gae_ws_bytes(int64_t n) {
+  const int64_t nt = gae_ntiles(n);
+  return gae_memset_bytes(nt) + 16 * nt + 16;
+}
+inline GaeWs gae_ws_carve(void* ws, int64_t ntiles) {
+  char* p = static_cast<char*>(ws);
+  GaeWs w;
+  w.ctrs = reinterpret_cast<unsigned*>(p);
+  w.gran = reinterpret_cast<unsigned long long*>(p + 16);
+  w.tile_sums = reinterpret_cast<double2*>(p + gae_memset_bytes(ntiles));
+  return w;
+}
+
+__device__ inline float chunk_chain(const float* s_delta, const float* s_c, int chunk, float carry) {
+  const float* dl = s_delta + chunk * GAE_EPT;
+  const float* cc = s_c + chunk * GAE_EPT;
+#pragma unroll
+  for (int k = GAE_EPT - 1; k >= 0; --k) carry = dl[k] + cc[k] * carry;
+  return carry;
+}
+
+__device__ inline void publish_granule(unsigned long long* g, float v) {
+  const unsigned long long word = (1ull << 32) | (unsigned long long)__float_as_uint(v);
+  __hip_atomic_store(g, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Last-arriver reduction of per-tile {sum, sumsq} into out[2], in tile order.
+__device__ inline void finalize_tile_sums(const double2* tile_sums, int64_t ntiles, unsigned* arrivals,
+                                          unsigned* flags, double* out, double2 mine, int64_t tile) {
+  __shared__ int s_last;
+  __shared__ double s_part[2][GAE_THREADS / 64];
+  if (threadIdx.x == 0) {
+    double2* ts = const_cast<double2*>(tile_sums);
+    ts[tile] = mine;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (old == (unsigned)(ntiles - 1)) ? 1 : 0;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // fixed partition: thread j sums tiles j, j+256, ... in order; then a fixed-order tree.
+  double a = 0.0, b = 0.0;
+  for (int64_t t = threadIdx.x; t < ntiles; t += GAE_THREADS) {
+    const double2 v = tile_sums[t];
+    a += v.x;
+    b += v.y;
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { s_part[0][wid] = a; s_part[1][wid] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sa = 0.0, sb = 0.0;
+    for (int w = 0; w < GAE_THREADS / 64; ++w) { sa += s_part[0][w]; sb += s_part[1][w]; }
+    out[0] = sa;
+    out[1] = sb;
+    (void)flags;
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
+    const float* __restrict__ r, const float* __restrict__ d, const float* __restrict__ V,
+    const float* __restrict__ next_value, int64_t n, float gf, float glf, float* __restrict__ ret,
+    float* __restrict__ adv, GaeWs ws, int64_t ntiles, double* __restrict__ sums_out) {
+  __shared__ __attribute__((aligned(16))) float s_delta[GAE_TILE];
+  __shared__ __attribute__((aligned(16))) float s_c[GAE_TILE];
+  __shared__ float s_out[GAE_THREADS];
+  __shared__ unsigned char s_hb[GAE_THREADS];
+  __shared__ unsigned s_ticket;
+  __shared__ int s_need;
+  __shared__ float s_carry;
+
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    s_ticket = __hip_atomic_fetch_add(&ws.ctrs[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_need = 0;
+  }
+  __syncthreads();
+  const int64_t tile = ntiles - 1 - (int64_t)s_ticket;
+  const int64_t i0 = tile * GAE_TILE + (int64_t)tid * GAE_EPT;
+
+  float rr[GAE_EPT], dd[GAE_EPT], vv[GAE_EPT];
+  const bool full = (i0 + GAE_EPT <= n);
+  if (VEC && full) {
+    const float4* r4 = reinterpret_cast<const float4*>(r + i0);
+    const float4* d4 = reinterpret_cast<const float4*>(d + i0);
+    const float4* v4 = reinterpret_cast<const float4*>(V + i0);
+    const float4 ra = r4[0], rb = r4[1], da = d4[0], db = d4[1], va = v4[0], vb = v4[1];
+    rr[0] = ra.x; rr[1] = ra.y; rr[2] = ra.z; rr[3] = ra.w; rr[4] = rb.x; rr[5] = rb.y; rr[6] = rb.z; rr[7] = rb.w;
+    dd[0] = da.x; dd[1] = da.y; dd[2] = da.z; dd[3] = da.w; dd[4] = db.x; dd[5] = db.y; dd[6] = db.z; dd[7] = db.w;
+    vv[0] = va.x; vv[1] = va.y; vv[2] = va.z; vv[3] = va.w; vv[4] = vb.x; vv[5] = vb.y; vv[6] = vb.z; vv[7] = vb.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < GAE_EPT; ++k) {
+      const int64_t i = i0 + k;
+      const bool in = i < n;
+      rr[k] = in ? r[i] : 0.f;
+      dd[k] = in ? d[i] : 1.f;  // padding: c = 0, delta = 0
+      vv[k] = in ? V[i] : 0.f;
+    }
+  }
+  // nv for the final element (PPO.py:188: next_value = V[-1]) and for this chunk's last element
+  const float nv_end = next_value ? *next_value : V[n - 1];
+  const int64_t inext = i0 + GAE_EPT;
+  const float vnext = (inext < n) ? V[inext] : nv_end;
+
+  float dl[GAE_EPT], cc[GAE_EPT];
+#pragma unroll
+  for (int k = 0; k < GAE_EPT; ++k) {
+    const int64_t i = i0 + k;
+    float nv = (k + 1 < GAE_EPT) ? vv[k + 1] : vnext;
+    if (i + 1 == n) nv = nv_end;
+    const float omd = 1.0f - dd[k];
+    float a = gf * nv;
+    a = a * omd;
+    const float s = rr[k] + a;
+    dl[k] = s - vv[k];
+    cc[k] = glf * omd;
+  }
+  {
+    float4* sd4 = reinterpret_cast<float4*>(s_delta + tid * GAE_EPT);
+    float4* sc4 = reinterpret_cast<float4*>(s_c + tid * GAE_EPT);
+    sd4[0] = float4{dl[0], dl[1], dl[2], dl[3]};
+    sd4[1] = float4{dl[4], dl[5], dl[6], dl[7]};
+    sc4[0] = float4{cc[0], cc[1], cc[2], cc[3]};
+    sc4[1] = float4{cc[4], cc[5], cc[6], cc[7]};
+  }
+  // local phase: everything at or left of the last break of this chunk
+  int pb = -1;
+#pragma unroll
+  for (int k = 0; k < GAE_EPT; ++k)
+    if (cc[k] == 0.0f) pb = k;
+  float g[GAE_EPT];
+  {
+    float gg = 0.0f;
+#pragma unroll
+    for (int k = GAE_EPT - 1; k >= 0; --k) {
+      if (k <= pb) {
+        gg = dl[k] + cc[k] * gg;
+        g[k] = gg;
+      }
+    }
+  }
+  s_hb[tid] = (pb >= 0) ? 1 : 0;
+  s_out[tid] = (pb >= 0) ? g[0] : 0.0f;
+  __syncthreads();
+
+  // tail: resolve from the nearest chunk to the right that has a break
+  bool resolved = (pb == GAE_EPT - 1);
+  bool need_tile = false;
+  if (!resolved) {
+    int kk = tid + 1;
+    while (kk < GAE_THREADS && !s_hb[kk]) ++kk;
+    if (kk < GAE_THREADS) {
+      float carry = s_out[kk];
+      for (int m = kk - 1; m > tid; --m) carry = chunk_chain(s_delta, s_c, m, carry);
+#pragma unroll
+      for (int k = GAE_EPT - 1; k >= 0; --k) {
+        if (k > pb) {
+          carry = dl[k] + cc[k] * carry;
+          g[k] = carry;
+        }
+      }
+      resolved = true;
+    } else {
+      need_tile = true;
+      s_need = 1;
+    }
+  }
+  if (tid == 0 && resolved) publish_granule(&ws.gran[tile], g[0]);
+  __syncthreads();
+
+  if (s_need) {
+    if (tid == 0) {
+      float cin = 0.0f;  // beyond the last element: gae = 0 (PPO.py:110)
+      if (tile + 1 < ntiles) {
+        unsigned spins = 0;
+        unsigned long long w;
+        for (;;) {
+          w = __hip_atomic_load(&ws.gran[tile + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((w >> 32) == 1ull) break;
+          if (++spins >= GAE_SPIN_LIMIT) {
+            __hip_atomic_fetch_or(&ws.ctrs[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            w = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        cin = __uint_as_float((unsigned)(w & 0xffffffffull));
+      }
+      s_carry = cin;
+    }
+    __syncthreads();
+    if (need_tile) {
+      float carry = s_carry;
+      for (int m = GAE_THREADS - 1; m > tid; --m) carry = chunk_chain(s_delta, s_c, m, carry);
+#pragma unroll
+      for (int k = GAE_EPT - 1; k >= 0; --k) {
+        if (k > pb) {
+          carry = dl[k] + cc[k] * carry;
+          g[k] = carry;
+        }
+      }
+      if (tid == 0) publish_granule(&ws.gran[tile], g[0]);
+    }
+  }
+
+  // outputs: ret = gae + V (PPO.py:116), adv = ret - V (PPO.py:198)
+  float rt[GAE_EPT], av[GAE_EPT];
+#pragma unroll
+  for (int k = 0; k < GAE_EPT; ++k) {
+    rt[k] = g[k] + vv[k];
+    av[k] = rt[k] - vv[k];
+  }
+  if (VEC && full) {
+    float4* o4 = reinterpret_cast<float4*>(ret + i0);
+    o4[0] = float4{rt[0], rt[1], rt[2], rt[3]};
+    o4[1] = float4{rt[4], rt[5], rt[6], rt[7]};
+    if (adv) {
+      float4* a4 = reinterpret_cast<float4*>(adv + i0);
+      a4[0] = float4{av[0], av[1], av[2], av[3]};
+      a4[1] = float4{av[4], av[5], av[6], av[7]};
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < GAE_EPT; ++k) {
+      if (i0 + k < n) {
+        ret[i0 + k] = rt[k];
+        if (adv) adv[i0 + k] = av[k];
+      }
+    }
+  }
+  if (adv) {
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < GAE_EPT; ++k) {
+      if (i0 + k < n) {
+        const double x = (double)av[k];
+        s1 += x;
+        s2 += x * x;
+      }
+    }
+    __shared__ double s_red[2][GAE_THREADS / 64];
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    const int lane = tid & 63, wid = tid >> 6;
+    if (lane == 0) { s_red[0][wid] = s1; s_red[1][wid] = s2; }
+    __syncthreads();
+    double2 mine{0.0, 0.0};
+    if (tid == 0)
+      for (int w = 0; w < GAE_THREADS / 64; ++w) { mine.x += s_red[0][w]; mine.y += s_red[1][w]; }
+    finalize_tile_sums(ws.tile_sums, ntiles, &ws.ctrs[1], &ws.ctrs[2], sums_out, mine, tile);
+  }
+}
+
+// Plain statistics pass (prl_adv_stats): per-tile sums + last-arriver ordered reduction.
+__global__ __launch_bounds__(GAE_THREADS) void stats_kernel(const float* __restrict__ x, int64_t n,
+                                                            GaeWs ws, int64_t ntiles,
+                                                            double* __restrict__ sums_out) {
+  const int64_t tile = blockIdx.x;
+  const int64_t i0 = tile * GAE_TILE + (int64_t)threadIdx.x * GAE_EPT;
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < GAE_EPT; ++k) {
+    const int64_t i = i0 + k;
+    if (i < n) {
+      const double v = (double)x[i];
+      s1 += v;
+      s2 += v * v;
+    }
+  }
+  __shared__ double s_red[2][GAE_THREADS / 64];
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { s_red[0][wid] = s1; s_red[1][wid] = s2; }
+  __syncthreads();
+  double2 mine{0.0, 0.0};
+  if (threadIdx.x == 0)
+    for (int w = 0; w < GAE_THREADS / 64; ++w) { mine.x += s_red[0][w]; mine.y += s_red[1][w]; }
+  finalize_tile_sums(ws.tile_sums, ntiles, &ws.ctrs[1], &ws.ctrs[2], sums_out, mine, tile);
+}
+
+// (x - mean) / (std_unbiased + eps) in float32, statistics from f64 sums (PPO.py:199).
+__global__ __launch_bounds__(256) void normalize_kernel(const float* __restrict__ x, int64_t n,
+                                                        const double* __restrict__ sums, double count,
+                                                        float eps, float* __restrict__ out) {
+  const double mean = sums[0] / count;
+  double var = (count > 1.0) ? (sums[1] - sums[0] * mean) / (count - 1.0) : __builtin_nan("");
+  if (var < 0.0) var = 0.0;
+  const float mean_f = (float)mean;
+  const float den = (float)sqrt(var) + eps;
+  const int64_t n4 = n >> 2;
+  const bool vec = aligned16(x) && aligned16(out);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (vec) {
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    float4* o4 = reinterpret_cast<float4*>(out);
+    for (int64_t j = i; j < n4; j += stride) {
+      const float4 v = x4[j];
+      o4[j] = float4{(v.x - mean_f) / den, (v.y - mean_f) / den, (v.z - mean_f) / den,
+                     (v.w - mean_f) / den};
+    }
+    for (int64_t j = n4 * 4 + i; j < n; j += stride) out[j] = (x[j] - mean_f) / den;
+  } else {
+    for (int64_t j = i; j < n; j += stride) out[j] = (x[j] - mean_f) / den;
+  }
+}
+
+}  // namespace prl
+
+using namespace prl;
+
+int64_t prl_gae_workspace_bytes(int64_t n) { return gae_ws_bytes(n); }
+
+extern "C" int prl_gae(const float* r, const float* d, const float* V, const float* next_value,
+                       int64_t n, double gamma, double lam, float* ret, float* adv,
+                       double* sums_out, void* workspace, int64_t workspace_bytes, void* stream) {
+  PRL_REQUIRE(n >= 0, "prl_gae: n < 0");
+  if (n == 0) return PRL_OK;
+  PRL_REQUIRE(r && d && V && ret, "prl_gae: null pointer");
+  PRL_REQUIRE(!adv || sums_out, "prl_gae: adv requested without sums_out");
+  PRL_REQUIRE(n < ((int64_t)1 << 40), "prl_gae: n too large");
+  const int64_t nt = gae_ntiles(n);
+  PRL_REQUIRE(nt < (int64_t)0x7fffffff, "prl_gae: too many tiles");
+  PRL_REQUIRE(workspace && workspace_bytes >= gae_ws_bytes(n),
+              "prl_gae: workspace too small (%lld < %lld)", (long long)workspace_bytes,
+              (long long)gae_ws_bytes(n));
+  hipStream_t s = as_stream(stream);
+  GaeWs ws = gae_ws_carve(workspace, nt);
+  PRL_HIP_TRY(hipMemsetAsync(workspace, 0, gae_memset_bytes(nt), s));
+  // gamma * nv * (1 - d): gamma is a weak Python float -> float32; gamma * lambda is a Python
+  // float product (float64), rounded to float32 when it meets the float32 (1 - d).
+  const float gf = (float)gamma;
+  const float glf = (float)(gamma * lam);
+  const bool vec = aligned16(r) && aligned16(d) && aligned16(V) && aligned16(ret) &&
+                   (!adv || aligned16(adv));
+  if (vec)
+    hipLaunchKernelGGL(gae_kernel<true>, dim3((unsigned)nt), dim3(GAE_THREADS), 0, s, r, d, V,
+                       next_value, n, gf, glf, ret, adv, ws, nt, sums_out);
+  else
+    hipLaunchKernelGGL(gae_kernel<false>, dim3((unsigned)nt), dim3(GAE_THREADS), 0, s, r, d, V,
+                       next_value, n, gf, glf, ret, adv, ws, nt, sums_out);
+  PRL_LAUNCH_CHECK("gae");
+  return PRL_OK;
+}
+
+extern "C" int prl_adv_stats(const float* x, int64_t n, double* sums_out, void* workspace,
+                             int64_t workspace_bytes, void* stream) {
+  PRL_REQUIRE(n >= 0, "prl_adv_stats: n < 0");
+  PRL_REQUIRE(sums_out, "prl_adv_stats: null sums_out");
+  hipStream_t s = as_stream(stream);
+  if (n == 0) {
+    PRL_HIP_TRY(hipMemsetAsync(sums_out, 0, 2 * sizeof(double), s));
+    return PRL_OK;
+  }
+  PRL_REQUIRE(x, "prl_adv_stats: null x");
+  const int64_t nt = gae_ntiles(n);
+  PRL_REQUIRE(workspace && workspace_bytes >= gae_ws_bytes(n), "prl_adv_stats: workspace too small");
+  GaeWs ws = gae_ws_carve(workspace, nt);
+  PRL_HIP_TRY(hipMemsetAsync(workspace, 0, gae_memset_bytes(nt), s));
+  hipLaunchKernelGGL(stats_kernel, dim3((unsigned)nt), dim3(GAE_THREADS), 0, s, x, n, ws, nt, sums_out);
+  PRL_LAUNCH_CHECK("adv_stats");
+  return PRL_OK;
+}
+
+extern "C" int prl_adv_normalize(const float* x, int64_t n, const double* sums, double count,
+                                 float eps, float* out, void* stream) {
+  PRL_REQUIRE(n >= 0, "prl_adv_normalize: n < 0");
+  if (n == 0) return PRL_OK;
+  PRL_REQUIRE(x && sums && out, "prl_adv_normalize: null pointer");
+  PRL_REQUIRE(count >= (double)n, "prl_adv_normalize: count < n");
+  const int64_t work = aligned16(x) && aligned16(out) ? cdiv(n, 4) : n;
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(work, 256), 2048);
+  hipLaunchKernelGGL(normalize_kernel, dim3(grid), dim3(256), 0, as_stream(stream), x, n, sums,
+                     count, eps, out);
+  PRL_LAUNCH_CHECK("adv_normalize");
+  return PRL_OK;
+}
