@@ -1,0 +1,272 @@
+"""AsyncPPO / EnvVectorizer / VecMemory — drop-in for the reference's AsyncTools/AsyncPPO.py.
+
+Reference semantics kept (AsyncPPO.py:11-165):
+  * EnvVectorizer holds num_envs envs; `envs_active[e]` is True when env e is TERMINAL; reset()
+    resets every env and clears the mask; step(actions) steps only the non-terminal envs in
+    ascending index order, the i-th action going to the i-th active env, and returns
+    obs / rewards / dones / truncates / infos compacted to the active envs.
+  * AsyncPPO.worker() runs ONE episode per env until every env is terminal, records
+    (pre-step state, action, reward, done|truncated) per env and appends the rollout to
+    ppo.memory env-major; run() alternates worker() and ppo.learn() until `steps` transitions.
+
+MI355X design: the envs are one structure-of-arrays batch in HBM stepped by HIP kernels
+(libprl_hip.so).  With a PPO from this package, worker() is DEVICE-RESIDENT: per vector step,
+the policy MLP (PyTorch) reads the contiguous time-major slice traj_obs[t], and one fused kernel
+(prl_rollout_step) samples the actions, steps the physics, writes the transition, updates the
+mask and the score counters.  No per-step host<->device copy: the host only polls a pinned
+"envs still active" counter a few steps behind, and ends the loop when it reaches zero.  The
+finished rollout is flattened env-major on the device (prl_exclusive_scan_i32 +
+prl_flatten_env_major) and handed to ppo.memory as device tensors.  Any other duck-typed `ppo`
+(get_action/memory/learn) runs through the compat path (numpy API, same HIP env kernels).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+import torch.distributed as tdist
+from tqdm import tqdm
+
+import AsyncTools.utils as utils
+import prl_native
+from AsyncTools.envs import resolve
+
+
+class VecMemory:  # AsyncPPO.py:11-33
+    def __init__(self, num_envs: int):
+        self.states = [[] for _ in range(num_envs)]
+        self.actions = [[] for _ in range(num_envs)]
+        self.rewards = [[] for _ in range(num_envs)]
+        self.dones = [[] for _ in range(num_envs)]
+
+    def push(self, idx: int, state, action, reward, done):
+        self.states[idx].append(np.asarray(state).astype(np.float32))
+        self.actions[idx].append(np.asarray(action).astype(np.float32))
+        self.rewards[idx].append(np.asarray(reward).astype(np.float32))
+        self.dones[idx].append(np.asarray(done).astype(np.float32))
+
+    def clear(self):
+        for i in range(len(self.states)):
+            del self.states[i][:]
+            del self.actions[i][:]
+            del self.rewards[i][:]
+            del self.dones[i][:]
+
+
+def _rank_world():
+    if tdist.is_available() and tdist.is_initialized():
+        return tdist.get_rank(), tdist.get_world_size()
+    return 0, 1
+
+
+class EnvVectorizer:  # AsyncPPO.py:35-102
+    """num_envs copies of one env as a device batch.  seed: int -> env i is seeded with
+    seed + i (+ rank * num_envs under torch.distributed), like gymnasium's reset(seed=...);
+    None -> fresh OS entropy, like an unseeded gymnasium env."""
+
+    def __init__(self, env, num_envs: int = 1, seed=None, device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("EnvVectorizer runs on the GPU through libprl_hip.so; no GPU visible")
+        self.spec = resolve(env)
+        self.num_envs = num_envs
+        self.action_space = self.spec.action_space
+        self.observation_space = self.spec.observation_space
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        E, dev = num_envs, self.device
+        self.phys = torch.zeros(E, self.spec.phys_dim, dtype=torch.float64, device=dev)
+        self.rng = torch.zeros(E, 4, dtype=torch.int64, device=dev)
+        self.t_elapsed = torch.zeros(E, dtype=torch.int32, device=dev)
+        self.terminal = torch.zeros(E, dtype=torch.uint8, device=dev)
+        self.obs = torch.zeros(E, self.spec.obs_dim, dtype=torch.float32, device=dev)
+        self._idx = torch.zeros(E, dtype=torch.int64, device=dev)
+        self._cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.seed(seed)
+
+    # the reference exposes the deep-copied env list (AsyncPPO.py:39)
+    @property
+    def envs(self):
+        return [self.spec] * self.num_envs
+
+    def seed(self, seed=None):
+        rank, _ = _rank_world()
+        if seed is None:
+            seeds = np.frombuffer(os.urandom(8 * self.num_envs), dtype=np.uint64) >> np.uint64(1)
+        else:
+            seeds = np.arange(self.num_envs, dtype=np.uint64) + np.uint64(seed) + np.uint64(
+                rank * self.num_envs)
+        s = torch.from_numpy(seeds.astype(np.int64)).to(self.device)
+        prl_native.pcg64_seed(s, self.rng)
+
+    @property
+    def envs_active(self):
+        return self.terminal.cpu().numpy().astype(bool)
+
+    @envs_active.setter
+    def envs_active(self, mask):
+        m = torch.as_tensor(np.asarray(mask, dtype=np.uint8)).to(self.device)
+        self.terminal.copy_(m)
+
+    def reset_device(self, obs_out=None):
+        """Reset every env on the device; obs written to obs_out ([E, D] view) or self.obs."""
+        out = self.obs if obs_out is None else obs_out
+        prl_native.env_reset(self.spec.kind, self.phys, self.rng, self.t_elapsed, self.terminal,
+                             out, out.stride(0))
+        return out
+
+    def reset(self, seed=None):
+        if seed is not None:
+            self.seed(seed)
+        obs = self.reset_device()
+        return obs.cpu().numpy(), [{} for _ in range(self.num_envs)]
+
+    def step(self, actions):
+        prl_native.active_indices(self.terminal, self._idx, self._cnt)
+        n = int(self._cnt.item())
+        if self.spec.discrete:
+            act = torch.as_tensor(np.asarray(actions)).to(self.device, torch.int64).reshape(-1)
+        else:
+            act = torch.as_tensor(np.asarray(actions, dtype=np.float32)).to(self.device)
+            act = act.reshape(-1, self.spec.act_dim)
+        act = act.contiguous()
+        if act.shape[0] < n:
+            raise IndexError(f"{act.shape[0]} actions for {n} active environments")
+        obs = torch.empty(n, self.spec.obs_dim, dtype=torch.float32, device=self.device)
+        rew = torch.empty(n, dtype=torch.float64, device=self.device)
+        term = torch.empty(n, dtype=torch.uint8, device=self.device)
+        trunc = torch.empty(n, dtype=torch.uint8, device=self.device)
+        prl_native.env_step_compact(self.spec.kind, self.phys, self.t_elapsed, self._idx, n, act,
+                                    obs, rew, term, trunc)
+        infos = np.array([{} for _ in range(n)], dtype=object)
+        return (obs.cpu().numpy(), rew.cpu().numpy(), term.cpu().numpy().astype(bool),
+                trunc.cpu().numpy().astype(bool), infos)
+
+    def close(self):
+        pass
+
+
+class DeviceTrajectory:
+    """Time-major rollout buffers in HBM (one row of E envs per vector step)."""
+
+    def __init__(self, E, spec, device):
+        T, D = spec.max_episode_steps, spec.obs_dim
+        adim = 1 if spec.discrete else spec.act_dim
+        self.T, self.E, self.adim = T, E, adim
+        self.obs = torch.empty(T + 1, E, D, dtype=torch.float32, device=device)
+        self.act = torch.empty(T, E, adim, dtype=torch.float32, device=device)
+        self.rew = torch.empty(T, E, dtype=torch.float32, device=device)
+        self.done = torch.empty(T, E, dtype=torch.uint8, device=device)
+        self.ep_len = torch.zeros(E, dtype=torch.int32, device=device)
+        self.active_after = torch.zeros(T, dtype=torch.int32, device=device)
+        self.reward_sum = torch.zeros(1, dtype=torch.float64, device=device)
+        self.offsets = torch.zeros(E + 1, dtype=torch.int64, device=device)
+        self.pinned = torch.zeros(T, dtype=torch.int32, pin_memory=True)
+
+
+class AsyncPPO:  # AsyncPPO.py:104-165
+    def __init__(self, env, ppo: object, num_envs: int = 32, steps: int = 100000, seed=None,
+                 poll_lag: int = 4):
+        self.env = EnvVectorizer(env, num_envs, seed=seed)
+        self.num_envs = num_envs
+        self.steps = steps
+        self.ppo = ppo
+        self.step_score = np.array(0, dtype=np.int32)
+        self.reward_score = np.array(0.0, dtype=np.float32)
+        self.buffer = VecMemory(num_envs)
+        self.poll_lag = poll_lag
+        self.sample_seed = int.from_bytes(os.urandom(8), "little") if seed is None else (
+            int(seed) * 0x9E3779B97F4A7C15 + 0x1234567) & (2**64 - 1)
+        self._rollouts = 0
+        self._traj = None
+        self.last_vector_steps = 0
+
+    # ------------------------------------------------------------------ worker
+    def worker(self):
+        if hasattr(self.ppo, "dist_params"):
+            return self._device_worker()
+        return self._compat_worker()
+
+    def _compat_worker(self):
+        """The reference's worker loop verbatim over the numpy API (AsyncPPO.py:117-146)."""
+        states = self.env.reset()[0]
+        while True:
+            actions = self.ppo.get_action(torch.from_numpy(states))
+            next_states, rewards, dones, truncates, _ = self.env.step(actions)
+            utils.buffer_append(self.buffer, states, actions, rewards, dones | truncates,
+                                self.env.envs_active, self.num_envs)
+            self.reward_score += np.sum(rewards)
+            self.step_score += np.sum(~self.env.envs_active)
+            states = utils.inactive_states_dropout(next_states, dones | truncates)
+            self.env.envs_active = utils.update_active_environments_list(self.env.envs_active,
+                                                                         dones | truncates)
+            if np.all(self.env.envs_active):
+                utils.buffer_to_target_buffer_transfer(self.buffer, self.ppo.memory)
+                break
+
+    def _device_worker(self):
+        env, spec = self.env, self.env.spec
+        E = self.num_envs
+        if self._traj is None:
+            self._traj = DeviceTrajectory(E, spec, env.device)
+        tr = self._traj
+        seed = (self.sample_seed + self._rollouts * 0xD1B54A32D192ED03) & (2**64 - 1)
+        self._rollouts += 1
+        scaling = float(getattr(self.ppo, "action_scaling", None) or 1.0)
+        env.reset_device(tr.obs[0])
+        tr.active_after.zero_()
+        tr.reward_sum.zero_()
+        stream = torch.cuda.current_stream()
+        events = []
+        checked = -1           # last step whose counter has been read
+        finished = False
+        k = 0
+        for k in range(tr.T):
+            dist = self.ppo.dist_params(tr.obs[k])
+            if dist.dtype != torch.float32 or not dist.is_contiguous():
+                dist = dist.float().contiguous()
+            prl_native.rollout_step(spec.kind, k, env.phys, env.t_elapsed, env.terminal, dist,
+                                    scaling, seed, tr.T, tr.obs, tr.act, tr.rew, tr.done,
+                                    tr.ep_len, tr.active_after, tr.reward_sum)
+            tr.pinned[k:k + 1].copy_(tr.active_after[k:k + 1], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            events.append(ev)
+            # poll completed steps without blocking; block only when too far ahead
+            while checked < k and (k - checked > self.poll_lag or events[checked + 1].query()):
+                events[checked + 1].synchronize()
+                checked += 1
+                if int(tr.pinned[checked]) == 0:
+                    finished = True
+                    break
+            if finished:
+                break
+        self.last_vector_steps = k + 1
+        # env-major flatten straight into learn()'s input tensors
+        prl_native.exclusive_scan_i32(tr.ep_len, tr.offsets)
+        N = int(tr.offsets[E].item())
+        D = spec.obs_dim
+        S = torch.empty(N, D, dtype=torch.float32, device=env.device)
+        A = torch.empty(N, tr.adim, dtype=torch.float32, device=env.device)
+        R = torch.empty(N, dtype=torch.float32, device=env.device)
+        Dn = torch.empty(N, dtype=torch.float32, device=env.device)
+        prl_native.flatten_env_major(tr.offsets, N, tr.obs, tr.act, tr.rew, tr.done, S, A, R, Dn)
+        self.ppo.memory.push_device(S, A[:, 0] if spec.discrete else A, R, Dn)
+        self.step_score = self.step_score + N
+        self.reward_score = self.reward_score + float(tr.reward_sum.item())
+        return N
+
+    # ------------------------------------------------------------------ run
+    def run(self):  # AsyncPPO.py:148-165
+        rank, _ = _rank_world()
+        pbar = tqdm(total=self.steps, unit="step", disable=rank != 0)
+        while pbar.n < self.steps:
+            self.step_score = 0
+            self.reward_score = 0
+            self.worker()
+            mean_reward = self.reward_score / self.num_envs
+            pbar.update(min(pbar.total - pbar.n, int(self.step_score)))
+            pbar.set_description(f"Mean reward {float(mean_reward): .1f}")
+            self.ppo.learn()
+        pbar.close()
+        self.env.close()

@@ -1,0 +1,277 @@
+"""PPO — drop-in for the reference's PPO/PPO.py:13-283 on MI355X.
+
+Same constructor (14 kwargs, same defaults), attributes and methods.  What changes is where the
+work runs in learn() (PPO.py:122-260):
+  * the rollout memory is already env-major on the device (no per-transition numpy stacking);
+  * policy_old's log-probs / values are evaluated in large chunks (per-row MLP: same values);
+  * RND intrinsic reward: fused HIP kernel (prl_rnd_forward);
+  * GAE(lambda) + advantages: one single-pass HIP segmented scan (prl_gae), bit-exact with the
+    reference's float32 loop, which is O(N^2) there (list.insert(0), PPO.py:116);
+  * advantage normalisation: f64 statistics from the GAE pass + HIP normalise (prl_adv_normalize);
+  * the clipped surrogate + value loss forward/backward: HIP (prl_ppo_surrogate_fwd/bwd) behind
+    a torch.autograd.Function; the MLP backward, clip_grad_norm_(2.0) and AdamW stay PyTorch;
+  * minibatches are zero-copy slices of the device tensors, sequential and unshuffled, last
+    partial batch kept (the reference's DataLoader semantics, PPO.py:98-105).
+Data parallel (torch.distributed, one process per GPU, RCCL): every rank learns on its own
+rollout; advantage statistics and the flat gradient of every optimizer step are all-reduced,
+and global minibatch j is the union of the ranks' j-th slices (multi-GPU).
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import torch
+import torch.distributed as tdist
+from torch import nn, optim
+from tqdm import tqdm
+
+import prl_native
+
+from .ActorCritic import ActorCritic
+from .Memory import Memory
+from .RND import RND
+
+device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+
+
+def _require_gpu(what):
+    if not torch.cuda.is_available():
+        raise RuntimeError(f"{what} runs on the GPU through libprl_hip.so; no GPU is visible")
+
+
+class SurrogateLoss(torch.autograd.Function):
+    """PPO.py:225-249 as one HIP forward (loss + per-sample gradient) and one HIP scale in
+    backward.  Returns the minibatch mean loss (what the reference back-propagates)."""
+
+    @staticmethod
+    def forward(ctx, logp, old_logp, adv, V, ret, entropy, clip, vf_coef, ent_coef, ops):
+        logp = logp.contiguous()
+        V = V.contiguous()
+        loss = torch.empty((), dtype=torch.float32, device=logp.device)
+        dl = torch.empty_like(logp)
+        dv = torch.empty_like(V)
+        ops.surrogate_fwd(logp, old_logp.contiguous(), adv.contiguous(), V, ret.contiguous(),
+                          entropy.reshape(()).contiguous(), clip, vf_coef, ent_coef, loss, dl, dv)
+        ctx.save_for_backward(dl, dv)
+        ctx.ops = ops
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        dl, dv = ctx.saved_tensors
+        gl = torch.empty_like(dl)
+        gv = torch.empty_like(dv)
+        ctx.ops.surrogate_bwd(grad_out.reshape(()).contiguous(), dl, dv, gl, gv)
+        return gl, None, None, gv, None, None, None, None, None, None
+
+
+class PPO:
+    def __init__(self, is_continuous: bool, observ_dim: int, action_dim: int,
+                 action_scaling: float = None, lr: float = 0.001, k_epochs: int = 7,
+                 policy_clip: float = 0.2, GAE_lambda: float = 0.95, gamma: float = 0.995,
+                 batch_size: int = 1024, mini_batch_size: int = 64, use_RND: bool = False,
+                 beta: float = 0.001):
+        self.device = device
+        self.policy = ActorCritic(is_continuous, observ_dim, action_dim, device=self.device)
+        self.policy_old = ActorCritic(is_continuous, observ_dim, action_dim, device=self.device)
+        if use_RND:
+            self.rnd = RND(in_features=observ_dim, out_features=observ_dim, beta=beta,
+                           device=self.device)
+        self.memory = Memory()
+        self.policy_old.load_state_dict(self.policy.state_dict())
+        self.policy.train()
+        self.policy_old.eval()
+        if use_RND:
+            self.rnd.eval()
+        self.loss_fn = nn.SmoothL1Loss()
+        self.optimizer = optim.AdamW(params=self.policy.parameters(), lr=lr)
+
+        self.is_continuous = is_continuous
+        self.action_scaling = action_scaling
+        self.use_RND = use_RND
+        self.beta = beta
+        self.lr = lr
+        self.policy_clip = policy_clip
+        self.k_epochs = k_epochs
+        self.GAE_lambda = GAE_lambda
+        self.gamma = gamma
+        self.batch_size = batch_size
+        self.mini_batch_size = mini_batch_size
+        self.observ_dim = observ_dim
+        self.action_dim = action_dim
+
+        # engine knobs (not in the reference API)
+        self.eval_chunk = 1 << 18          # rows per policy_old evaluation chunk
+        self.value_coef, self.entropy_coef = 0.5, 0.01  # PPO.py:245
+        self.show_progress = True
+        self.last_loss = None
+        self._ops = prl_native              # HIP entry points (tests may substitute a fake)
+        self._flat_grad = None
+        self._sync_initial_weights()
+
+    # ---------------------------------------------------------------- data parallel helpers
+    @staticmethod
+    def _world():
+        return tdist.get_world_size() if tdist.is_available() and tdist.is_initialized() else 1
+
+    def _sync_initial_weights(self):
+        if self._world() > 1:
+            for m in (self.policy, self.policy_old) + ((self.rnd,) if self.use_RND else ()):
+                for t in list(m.parameters()) + list(m.buffers()):
+                    tdist.broadcast(t.data, src=0)
+
+    def _ensure_flat_grads(self):
+        """Make every policy gradient a view of one flat buffer: one all-reduce per step."""
+        params = [p for p in self.policy.parameters() if p.requires_grad]
+        total = sum(p.numel() for p in params)
+        if self._flat_grad is None or self._flat_grad.numel() != total:
+            self._flat_grad = torch.zeros(total, dtype=torch.float32, device=params[0].device)
+            off = 0
+            for p in params:
+                p.grad = self._flat_grad[off:off + p.numel()].view_as(p)
+                off += p.numel()
+        return self._flat_grad
+
+    # ---------------------------------------------------------------- reference API
+    @torch.no_grad()
+    def get_action(self, state: torch.Tensor) -> np.ndarray:  # PPO.py:81-96
+        state = state.to(dtype=torch.float32, device=self.device)
+        dist = self.policy_old.get_dist(state)
+        action = dist.sample()
+        if self.is_continuous:
+            action = torch.tanh(action).mul(self.action_scaling)
+        return action.cpu().numpy()
+
+    @torch.no_grad()
+    def dist_params(self, obs: torch.Tensor) -> torch.Tensor:
+        """Distribution rows for the fused device worker step (probs, or [mu | std])."""
+        return self.policy_old.dist_params(obs)
+
+    def batch_packer(self, values, batch_size: int):  # PPO.py:98-105 (DataLoader, no shuffle)
+        def split(v):
+            if not isinstance(v, torch.Tensor):
+                v = torch.as_tensor(np.asarray(v))
+            return list(v.split(batch_size))
+        if isinstance(values, torch.Tensor):
+            return split(values)
+        if isinstance(values, list):
+            return [split(v) for v in values]
+        return split(values)
+
+    def compute_gae(self, rewards, dones, state_values, next_value):  # PPO.py:107-120
+        """Same float32 results as the reference loop, from one HIP scan.  numpy inputs ->
+        list of np.float32 (the reference's return type); device tensors -> tensor."""
+        _require_gpu("PPO.compute_gae")
+        as_list = not isinstance(state_values, torch.Tensor)
+        dev = self.device
+
+        def t(x):
+            return torch.as_tensor(np.asarray(x, dtype=np.float32) if as_list else x,
+                                   dtype=torch.float32).to(dev).contiguous()
+        r, d, V = t(rewards), t(dones), t(state_values)
+        nv = t(np.asarray([next_value], np.float32) if as_list else
+               torch.as_tensor(next_value, dtype=torch.float32).reshape(1))
+        ret = torch.empty_like(V)
+        self._ops.gae(r, d, V, nv, self.gamma, self.GAE_lambda, ret)
+        if as_list:
+            return list(ret.cpu().numpy())
+        return ret
+
+    @torch.no_grad()
+    def _evaluate_old(self, S, A):
+        lps, vs = [], []
+        for lo in range(0, S.shape[0], self.eval_chunk):
+            lp, v, _ = self.policy_old.get_evaluate(S[lo:lo + self.eval_chunk],
+                                                    A[lo:lo + self.eval_chunk])
+            lps.append(lp)
+            vs.append(v)
+        cat = (lambda x: x[0]) if len(lps) == 1 else torch.cat
+        return cat(lps).float().contiguous(), cat(vs).float().contiguous()
+
+    def learn(self):  # PPO.py:122-260
+        world = self._world()
+        n_local = len(self.memory)
+        if world > 1:
+            ns = torch.tensor([n_local], dtype=torch.int64, device=self.device)
+            gathered = [torch.zeros_like(ns) for _ in range(world)]
+            tdist.all_gather(gathered, ns)
+            n_ranks = [int(x.item()) for x in gathered]
+        else:
+            n_ranks = [n_local]
+        if sum(n_ranks) < self.batch_size:
+            return
+        _require_gpu("PPO.learn") if self._ops is prl_native else None
+        S, A, R, Dn = self.memory.device_tensors(self.device)
+        N = S.shape[0]
+        old_logp, old_V = self._evaluate_old(S, A)
+
+        if self.use_RND:
+            r_int = self.rnd.compute_intrinsic_reward(S)
+            R = R + r_int                                   # PPO.py:171 (float32 add)
+            self.rnd.update_pred(self.batch_packer(S, self.mini_batch_size))
+        self.memory.clear()
+
+        returns = torch.empty_like(old_V)
+        adv = torch.empty_like(old_V)
+        sums = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self._ops.gae(R, Dn, old_V, old_V[-1:], self.gamma, self.GAE_lambda, returns, adv, sums)
+        if world > 1:
+            tdist.all_reduce(sums)
+        self._ops.adv_normalize(adv, sums, float(sum(n_ranks)), 1e-8, adv)
+
+        self._update(S, A, old_logp, adv, returns, n_ranks)
+        self.policy_old.load_state_dict(self.policy.state_dict())
+
+    def _update(self, S, A, old_logp, adv, returns, n_ranks):
+        """k_epochs x sequential minibatches (PPO.py:219-255)."""
+        mb = self.mini_batch_size
+        world = len(n_ranks)
+        N = S.shape[0]
+        nb = max(-(-n // mb) for n in n_ranks)
+        counts = [sum(min(mb, max(0, n - j * mb)) for n in n_ranks) for j in range(nb)]
+        params = [p for p in self.policy.parameters() if p.requires_grad]
+        flat = self._ensure_flat_grads() if world > 1 else None
+        pbar = tqdm(total=sum(n_ranks) * self.k_epochs, leave=False,
+                    disable=not self.show_progress or (world > 1 and tdist.get_rank() != 0))
+        loss = None
+        for _ in range(self.k_epochs):
+            for j in range(nb):
+                lo, hi = j * mb, min((j + 1) * mb, N)
+                if flat is not None:
+                    flat.zero_()
+                else:
+                    self.optimizer.zero_grad()
+                if lo < hi:
+                    logp, V, H = self.policy.get_evaluate(S[lo:hi], A[lo:hi])
+                    loss = SurrogateLoss.apply(logp, old_logp[lo:hi], adv[lo:hi], V,
+                                               returns[lo:hi], H, self.policy_clip,
+                                               self.value_coef, self.entropy_coef, self._ops)
+                    scaled = loss * ((hi - lo) / counts[j]) if world > 1 else loss
+                    scaled.backward()
+                if flat is not None:
+                    tdist.all_reduce(flat)
+                nn.utils.clip_grad_norm_(params, 2.0)
+                self.optimizer.step()
+                pbar.update(counts[j])
+        self.last_loss = loss.detach() if loss is not None else None
+        if loss is not None and self.show_progress:
+            pbar.set_description(f"Loss: {float(self.last_loss): .6f}")
+        pbar.close()
+
+    def load_weights(self, path: str):  # PPO.py:262-277
+        try:
+            self.policy.load_state_dict(torch.load(os.path.join(path, "Policy_weights.pth"),
+                                                   weights_only=True, map_location=self.device))
+            self.policy_old.load_state_dict(self.policy.state_dict())
+            if self.use_RND:
+                self.rnd.load_state_dict(torch.load(os.path.join(path, "RND_weights.pth"),
+                                                    weights_only=True, map_location=self.device))
+        except FileNotFoundError:
+            pass
+
+    def save_weights(self, path: str):  # PPO.py:279-283
+        torch.save(self.policy.state_dict(), os.path.join(path, "Policy_weights.pth"))
+        if self.use_RND:
+            torch.save(self.rnd.state_dict(), os.path.join(path, "RND_weights.pth"))

@@ -1,0 +1,83 @@
+"""Random Network Distillation — drop-in for the reference's PPO/RND.py:8-115.
+
+Same modules, parameter names, initialisation and optimiser as the reference (target_net and
+pred_net are independent re-initialisations of Linear(D,64) -> GroupNorm(8,64) -> SiLU ->
+Linear(64,D); target frozen; AdamW lr 1e-3 + MSE for the predictor).  The intrinsic-reward
+forward (the hot part: every learn() call runs it over all N transitions) is one fused HIP
+kernel on fp32 MFMA (prl_rnd_forward); the predictor update stays in PyTorch (north star).
+"""
+from __future__ import annotations
+
+from copy import deepcopy
+
+import torch
+from torch import nn, optim
+
+import prl_native
+
+
+class RND(nn.Module):
+    def __init__(self, in_features: int, out_features: int, beta: float = 0.001, device=None):
+        super().__init__()
+        model = nn.Sequential(nn.Linear(in_features, 64), nn.GroupNorm(64 // 8, 64),
+                              nn.SiLU(inplace=True), nn.Linear(64, out_features))
+        self.target_net = deepcopy(model)
+        self.pred_net = deepcopy(model)
+        del model
+        self.init_weights()
+        for p in self.target_net.parameters():
+            p.requires_grad = False
+        self.beta = beta
+        self.loss_fn = nn.MSELoss()
+        self.optimizer = optim.AdamW(params=self.pred_net.parameters(), lr=0.001)
+        self.eval()
+        if device is None:
+            device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+        self.to(device)
+
+    def init_weights(self):  # RND.py:43-57
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.xavier_uniform_(m.weight)
+                if m.bias is not None:
+                    nn.init.normal_(m.bias, mean=0, std=0.01)
+            elif isinstance(m, nn.GroupNorm):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    @staticmethod
+    def _params(net):
+        return (net[0].weight, net[0].bias, net[1].weight, net[1].bias, net[3].weight, net[3].bias)
+
+    @staticmethod
+    def _concat(values):
+        if isinstance(values, torch.Tensor):
+            return values
+        values = list(values)
+        return values[0] if len(values) == 1 else torch.cat(values, dim=0)
+
+    @torch.no_grad()
+    def compute_intrinsic_reward(self, values) -> torch.Tensor:
+        """RND.py:71-94: beta * ||pred(x) - target(x)||_2 per row.  `values` is the reference's
+        list of minibatches (PPO.batch_packer) or one [N, D] tensor; rows keep their order."""
+        x = self._concat(values)
+        dev = self.target_net[0].weight.device
+        x = x.to(device=dev, dtype=torch.float32).contiguous()
+        out = torch.empty(x.shape[0], dtype=torch.float32, device=dev)
+        tp = [p.detach().contiguous() for p in self._params(self.target_net)]
+        pp = [p.detach().contiguous() for p in self._params(self.pred_net)]
+        prl_native.rnd_forward(x, tp, pp, float(self.beta), out)
+        return out
+
+    def update_pred(self, values) -> None:
+        """RND.py:96-115: one MSE/AdamW pass of the predictor over the minibatches (PyTorch)."""
+        self.pred_net.train()
+        for i in values:
+            with torch.no_grad():
+                targets = self.target_net(i)
+            preds = self.pred_net(i)
+            loss = self.loss_fn(preds, targets)
+            self.optimizer.zero_grad()
+            loss.backward()
+            self.optimizer.step()
+        self.pred_net.eval()

@@ -1,0 +1,292 @@
+"""ctypes binding of libprl_hip.so (include/prl_abi.h) for torch device tensors.
+
+This is the only way the Python drop-in packages (`PPO`, `AsyncTools`) reach the GPU hot path.
+There is no fallback: if the library is missing or no GPU is visible, calls raise.  Tensors are
+passed as raw device pointers (`tensor.data_ptr()`) on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PRL_HIP_LIB", os.path.join(_HERE, "libprl_hip.so"))
+
+ENV_KINDS = {"CartPole-v1": 0, "Pendulum-v1": 1, "SyntheticHumanoid-v0": 2}
+OP_GAE, OP_SURROGATE, OP_SCAN, OP_STATS = 0, 1, 2, 3
+
+_P = ctypes.c_void_p
+_I64, _I32, _U64, _F32, _F64, _INT = (ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64,
+                                      ctypes.c_float, ctypes.c_double, ctypes.c_int)
+# symbol -> argtypes (restype int unless listed in _RESTYPES)
+SIGNATURES = {
+    "prl_abi_version": [],
+    "prl_last_error": [],
+    "prl_workspace_bytes": [_INT, _I64],
+    "prl_env_dims": [_INT, _P, _P, _P, _P, _P],
+    "prl_pcg64_seed": [_P, _I64, _P, _P],
+    "prl_env_reset": [_INT, _I64, _P, _P, _P, _P, _P, _P, _I64, _P],
+    "prl_env_step_compact": [_INT, _I64, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P],
+    "prl_rollout_step": [_INT, _I64, _I32, _P, _P, _P, _P, _I64, _F32, _U64, _I32, _P, _P, _P,
+                         _P, _P, _P, _P, _P],
+    "prl_active_indices": [_P, _I64, _P, _P, _P, _P],
+    "prl_mask_update": [_P, _I64, _P, _I64, _P, _P],
+    "prl_compact_rows": [_P, _I64, _I64, _P, _P, _P, _P, _P],
+    "prl_exclusive_scan_i32": [_P, _I64, _P, _P, _P],
+    "prl_flatten_env_major": [_I64, _I32, _I32, _I32, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
+                              _P],
+    "prl_gae": [_P, _P, _P, _P, _I64, _F64, _F64, _P, _P, _P, _P, _I64, _P],
+    "prl_adv_stats": [_P, _I64, _P, _P, _I64, _P],
+    "prl_adv_normalize": [_P, _I64, _P, _F64, _F32, _P, _P],
+    "prl_ppo_surrogate_fwd": [_P, _P, _P, _P, _P, _P, _I64, _F32, _F32, _F32, _P, _P, _P, _P,
+                              _I64, _P],
+    "prl_ppo_surrogate_bwd": [_P, _P, _P, _I64, _P, _P, _P],
+    "prl_rnd_forward": [_P, _I64, _I32] + [_P] * 12 + [_F32, _P, _P],
+}
+_RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load libprl_hip.so once.  Raises RuntimeError if it is missing (build it with
+    `python -c "import __graft_entry__ as g; g.build()"` or csrc/build.py)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise RuntimeError(f"libprl_hip.so not found at {LIB_PATH}: build it with "
+                                       "parallel-reinforcement-learning_amd/csrc/build.py")
+                L = ctypes.CDLL(LIB_PATH)
+                for name, args in SIGNATURES.items():
+                    fn = getattr(L, name)
+                    fn.argtypes = args
+                    fn.restype = _RESTYPES.get(name, ctypes.c_int)
+                if L.prl_abi_version() != 1:
+                    raise RuntimeError("libprl_hip.so ABI version mismatch")
+                _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().prl_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def _dev(t: torch.Tensor | None, dtype=None, name="tensor"):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor (got {t.device})")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype} (got {t.dtype})")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+# ------------------------------------------------------------------------- workspace
+class _Workspace:
+    """Per-device scratch (grown, never shrunk).  Callers that capture graphs reserve first."""
+
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        dev = torch.device(device)
+        key = (dev.type, dev.index)
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+            self.buf[key] = b
+        return b
+
+
+_ws = _Workspace()
+
+
+def workspace_bytes(op: int, n: int) -> int:
+    return int(lib().prl_workspace_bytes(op, int(n)))
+
+
+def workspace(op: int, n: int, device) -> torch.Tensor:
+    return _ws.get(workspace_bytes(op, n), device)
+
+
+def reserve_workspace(n: int, device):
+    """Pre-grow the shared scratch so later calls (e.g. under graph capture) do not allocate."""
+    need = max(workspace_bytes(op, n) for op in (OP_GAE, OP_SURROGATE, OP_SCAN, OP_STATS))
+    return _ws.get(need, device)
+
+
+# ------------------------------------------------------------------------- envs
+def env_dims(kind: int):
+    o = [ctypes.c_int() for _ in range(5)]
+    _check(lib().prl_env_dims(kind, *[ctypes.byref(x) for x in o]), "prl_env_dims")
+    D, A, P, T, disc = (x.value for x in o)
+    return dict(obs_dim=D, act_dim=A, phys_dim=P, max_episode_steps=T, discrete=bool(disc))
+
+
+def pcg64_seed(seeds: torch.Tensor, rng: torch.Tensor):
+    E = seeds.numel()
+    _check(lib().prl_pcg64_seed(_dev(seeds, torch.int64, "seeds"), E,
+                                _dev(rng, torch.int64, "rng"), _stream()), "prl_pcg64_seed")
+
+
+def env_reset(kind, phys, rng, t_elapsed, terminal, obs, obs_stride, reset_mask=None):
+    E = t_elapsed.numel()
+    _check(lib().prl_env_reset(kind, E, _dev(phys, torch.float64, "phys"),
+                               _dev(rng, torch.int64, "rng"), _dev(t_elapsed, torch.int32, "t"),
+                               _dev(terminal, torch.uint8, "terminal"),
+                               _dev(reset_mask, torch.uint8, "reset_mask"),
+                               _dev(obs, torch.float32, "obs"), int(obs_stride), _stream()),
+           "prl_env_reset")
+
+
+def env_step_compact(kind, phys, t_elapsed, active_idx, n, actions, obs_out, reward_out,
+                     terminated_out, truncated_out):
+    E = t_elapsed.numel()
+    _check(lib().prl_env_step_compact(kind, E, _dev(phys, torch.float64, "phys"),
+                                      _dev(t_elapsed, torch.int32, "t"),
+                                      _dev(active_idx, torch.int64, "active_idx"), int(n),
+                                      _dev(actions, None, "actions"),
+                                      _dev(obs_out, torch.float32, "obs_out"),
+                                      _dev(reward_out, torch.float64, "reward_out"),
+                                      _dev(terminated_out, torch.uint8, "terminated_out"),
+                                      _dev(truncated_out, torch.uint8, "truncated_out"),
+                                      _stream()), "prl_env_step_compact")
+
+
+def rollout_step(kind, step, phys, t_elapsed, terminal, dist, action_scaling, seed, t_max,
+                 traj_obs, traj_act, traj_rew, traj_done, ep_len, active_after, reward_sum):
+    E = t_elapsed.numel()
+    _check(lib().prl_rollout_step(kind, E, int(step), _dev(phys, torch.float64, "phys"),
+                                  _dev(t_elapsed, torch.int32, "t"),
+                                  _dev(terminal, torch.uint8, "terminal"),
+                                  _dev(dist, torch.float32, "dist"), int(dist.stride(0)),
+                                  float(action_scaling), int(seed) & (2**64 - 1), int(t_max),
+                                  _dev(traj_obs, torch.float32, "traj_obs"),
+                                  _dev(traj_act, torch.float32, "traj_act"),
+                                  _dev(traj_rew, torch.float32, "traj_rew"),
+                                  _dev(traj_done, torch.uint8, "traj_done"),
+                                  _dev(ep_len, torch.int32, "ep_len"),
+                                  _dev(active_after, torch.int32, "active_after"),
+                                  _dev(reward_sum, torch.float64, "reward_sum"), _stream()),
+           "prl_rollout_step")
+
+
+# ------------------------------------------------------------------------- masks / buffers
+def active_indices(terminal: torch.Tensor, idx_out: torch.Tensor, count_out: torch.Tensor):
+    E = terminal.numel()
+    ws = workspace(OP_SCAN, E, terminal.device)
+    _check(lib().prl_active_indices(_dev(terminal, torch.uint8, "terminal"), E,
+                                    _dev(idx_out, torch.int64, "idx_out"),
+                                    _dev(count_out, torch.int64, "count_out"), _dev(ws),
+                                    _stream()), "prl_active_indices")
+
+
+def mask_update(terminal: torch.Tensor, dones: torch.Tensor):
+    E = terminal.numel()
+    ws = workspace(OP_SCAN, E, terminal.device)
+    _check(lib().prl_mask_update(_dev(terminal, torch.uint8, "terminal"), E,
+                                 _dev(dones, torch.uint8, "dones"), dones.numel(), _dev(ws),
+                                 _stream()), "prl_mask_update")
+
+
+def compact_rows(src: torch.Tensor, drop: torch.Tensor, dst: torch.Tensor, count_out: torch.Tensor):
+    rows = src.shape[0]
+    row_bytes = src[0].numel() * src.element_size() if rows else 0
+    ws = workspace(OP_SCAN, rows, src.device)
+    _check(lib().prl_compact_rows(_dev(src), rows, row_bytes, _dev(drop, torch.uint8, "drop"),
+                                  _dev(dst), _dev(count_out, torch.int64, "count_out"), _dev(ws),
+                                  _stream()), "prl_compact_rows")
+
+
+def exclusive_scan_i32(x: torch.Tensor, offsets: torch.Tensor):
+    n = x.numel()
+    ws = workspace(OP_SCAN, n, x.device)
+    _check(lib().prl_exclusive_scan_i32(_dev(x, torch.int32, "x"), n,
+                                        _dev(offsets, torch.int64, "offsets"), _dev(ws),
+                                        _stream()), "prl_exclusive_scan_i32")
+
+
+def flatten_env_major(offsets, N, traj_obs, traj_act, traj_rew, traj_done, S, A, R, Dn):
+    T1, E, D = traj_obs.shape
+    Adim = traj_act.shape[2] if traj_act.dim() == 3 else 1
+    _check(lib().prl_flatten_env_major(E, traj_rew.shape[0], D, Adim,
+                                       _dev(offsets, torch.int64, "offsets"), int(N),
+                                       _dev(traj_obs, torch.float32, "traj_obs"),
+                                       _dev(traj_act, torch.float32, "traj_act"),
+                                       _dev(traj_rew, torch.float32, "traj_rew"),
+                                       _dev(traj_done, torch.uint8, "traj_done"),
+                                       _dev(S, torch.float32, "S"), _dev(A, torch.float32, "A"),
+                                       _dev(R, torch.float32, "R"),
+                                       _dev(Dn, torch.float32, "Dn"), _stream()),
+           "prl_flatten_env_major")
+
+
+# ------------------------------------------------------------------------- learn()
+def gae(r, d, V, next_value, gamma, lam, ret, adv=None, sums=None):
+    n = V.numel()
+    ws = workspace(OP_GAE, n, V.device)
+    _check(lib().prl_gae(_dev(r, torch.float32, "r"), _dev(d, torch.float32, "d"),
+                         _dev(V, torch.float32, "V"),
+                         _dev(next_value, torch.float32, "next_value"), n, float(gamma),
+                         float(lam), _dev(ret, torch.float32, "ret"),
+                         _dev(adv, torch.float32, "adv"), _dev(sums, torch.float64, "sums"),
+                         _dev(ws), ws.numel(), _stream()), "prl_gae")
+
+
+def adv_stats(x, sums):
+    n = x.numel()
+    ws = workspace(OP_STATS, n, x.device)
+    _check(lib().prl_adv_stats(_dev(x, torch.float32, "x"), n, _dev(sums, torch.float64, "sums"),
+                               _dev(ws), ws.numel(), _stream()), "prl_adv_stats")
+
+
+def adv_normalize(x, sums, count, eps, out):
+    _check(lib().prl_adv_normalize(_dev(x, torch.float32, "x"), x.numel(),
+                                   _dev(sums, torch.float64, "sums"), float(count), float(eps),
+                                   _dev(out, torch.float32, "out"), _stream()),
+           "prl_adv_normalize")
+
+
+def surrogate_fwd(logp, old_logp, adv, V, ret, entropy, clip, vf_coef, ent_coef, loss_out,
+                  dlogp=None, dV=None):
+    mb = logp.numel()
+    ws = workspace(OP_SURROGATE, mb, logp.device)
+    _check(lib().prl_ppo_surrogate_fwd(
+        _dev(logp, torch.float32, "logp"), _dev(old_logp, torch.float32, "old_logp"),
+        _dev(adv, torch.float32, "adv"), _dev(V, torch.float32, "V"),
+        _dev(ret, torch.float32, "ret"), _dev(entropy, torch.float32, "entropy"), mb,
+        float(clip), float(vf_coef), float(ent_coef), _dev(loss_out, torch.float32, "loss"),
+        _dev(dlogp, torch.float32, "dlogp"), _dev(dV, torch.float32, "dV"), _dev(ws),
+        ws.numel(), _stream()), "prl_ppo_surrogate_fwd")
+
+
+def surrogate_bwd(grad_out, dlogp_unit, dV_unit, dlogp, dV):
+    _check(lib().prl_ppo_surrogate_bwd(_dev(grad_out, torch.float32, "grad_out"),
+                                       _dev(dlogp_unit, torch.float32, "dlogp_unit"),
+                                       _dev(dV_unit, torch.float32, "dV_unit"), dlogp_unit.numel(),
+                                       _dev(dlogp, torch.float32, "dlogp"),
+                                       _dev(dV, torch.float32, "dV"), _stream()),
+           "prl_ppo_surrogate_bwd")
+
+
+def rnd_forward(x, tnet, pnet, beta, out):
+    """tnet/pnet: sequences (w1, b1, gw, gb, w2, b2) of contiguous float32 device tensors."""
+    n, D = x.shape
+    ptrs = [_dev(p.contiguous() if not p.is_contiguous() else p, torch.float32, "rnd param")
+            for p in (*tnet, *pnet)]
+    _check(lib().prl_rnd_forward(_dev(x, torch.float32, "x"), n, D, *ptrs, float(beta),
+                                 _dev(out, torch.float32, "out"), _stream()), "prl_rnd_forward")
