@@ -1,0 +1,230 @@
+#!/usr/bin/env python
+"""bench.py — BASELINE.json metric: env-steps/sec + PPO.learn() wall-ms per 1M-step batch.
+
+    python bench.py --gpus N --steps K --warmup W [--config c2|c3|c5] [--mb 512] [--k-epochs 11]
+
+A STEP is one full AsyncPPO iteration on synthetic (freshly simulated) data: the device-resident
+worker() rolls one episode per env to termination (fused HIP env/sampling/mask kernel per vector
+step, PyTorch policy MLP), then ppo.learn() runs on that rollout (HIP GAE scan, advantage
+normalisation, surrogate; PyTorch MLP backward + AdamW; k_epochs x sequential minibatches).
+`value` = transitions collected by ALL ranks / wall time of the K timed steps (max over ranks):
+whole-job env-steps/s including learn().  Also reported: rollout-only env-steps/s and learn()
+wall-ms normalised to a 2^20-transition batch.  Multi-GPU (torchrun): one process per GPU over
+RCCL, num_envs per rank fixed (weak scaling), gradients all-reduced every optimizer step.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "parallel-reinforcement-learning_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "env-steps/sec + PPO.learn() wall-ms per 1M-step batch, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    # BASELINE.json configs[1] (per GPU; configs[3] is the same per-GPU shape on 8 GPUs)
+    "c2": dict(env="CartPole-v1", num_envs=65536, batch_size=1 << 20, cont=False, scaling=None,
+               rnd=False, mb=512, k_epochs=11),
+    # configs[2]
+    "c3": dict(env="Pendulum-v1", num_envs=65536, batch_size=1 << 20, cont=True, scaling=2.0,
+               rnd=False, mb=65536, k_epochs=11),
+    # configs[4] per GPU (131072 envs over 8 GPUs)
+    "c5": dict(env="SyntheticHumanoid-v0", num_envs=16384, batch_size=1 << 18, cont=True,
+               scaling=1.0, rnd=True, mb=65536, k_epochs=11),
+}
+
+# algorithmic HBM bytes per unit: GAE = r, d, V in + ret, adv out (f32)
+GAE_BYTES_PER_TRANSITION = 20
+# fused CartPole rollout step per env-step: phys f64 r/w 64, probs 8, t r/w 8, terminal r/w 2,
+# next obs 16, action 4, reward 4, done 1, ep_len 4
+CARTPOLE_STEP_BYTES = 111
+
+
+class LastCall:
+    """Remembers the arguments of the last call of a wrapped op (to re-time it afterwards)."""
+
+    def __init__(self, fn):
+        self.fn = fn
+        self.args = None
+
+    def __call__(self, *a, **k):
+        self.args = (a, k)
+        return self.fn(*a, **k)
+
+
+def time_kernel(launch, reps=10, cold=True):
+    """Average device time of one launch, with HIP events on the launching stream.  The GPU is
+    kept busy (a 512 MiB cache-flushing fill when cold, else a spin kernel) while the host
+    enqueues start-event / launch / end-event, so no host overhead lands between the events;
+    cold=True also evicts the 256 MiB Infinity Cache, so inputs come from HBM."""
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda") if cold else None
+    launch()
+    ms = []
+    for _ in range(reps):
+        if cold:
+            flush.fill_(1)
+        torch.cuda._sleep(2_000_000)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        launch()
+        e.record()
+        e.synchronize()
+        ms.append(s.elapsed_time(e))
+    return float(np.median(ms)), float(np.min(ms))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--num-envs", type=int, default=None, help="per GPU")
+    ap.add_argument("--mb", type=int, default=None)
+    ap.add_argument("--k-epochs", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-envs", type=int, default=8192)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from AsyncTools.AsyncPPO import AsyncPPO
+    from AsyncTools.envs import make
+    import prl_native
+    from PPO import PPO
+
+    cfg = dict(CONFIGS[args.config])
+    if args.num_envs:
+        cfg["num_envs"] = args.num_envs
+    if args.mb:
+        cfg["mb"] = args.mb
+    if args.k_epochs:
+        cfg["k_epochs"] = args.k_epochs
+    spec = make(cfg["env"])
+    torch.manual_seed(1234)
+    ppo = PPO(is_continuous=cfg["cont"], observ_dim=spec.obs_dim, action_dim=spec.act_dim,
+              action_scaling=cfg["scaling"], lr=1e-3, k_epochs=cfg["k_epochs"], policy_clip=0.2,
+              GAE_lambda=0.95, gamma=0.995, batch_size=cfg["batch_size"],
+              mini_batch_size=cfg["mb"],
+              use_RND=cfg["rnd"], beta=1e-3)
+    ppo.show_progress = False
+    runner = AsyncPPO(spec, ppo, num_envs=cfg["num_envs"], seed=1000 + rank * 7919)
+
+    # remember learn()'s GAE arguments: the roofline kernel is re-timed on that exact input
+    gae_call = LastCall(prl_native.gae)
+    ppo._ops = type("Ops", (), {})()
+    for name in ("adv_normalize", "surrogate_fwd", "surrogate_bwd"):
+        setattr(ppo._ops, name, getattr(prl_native, name))
+    ppo._ops.gae = gae_call
+
+    def iteration():
+        t0 = time.perf_counter()
+        runner.step_score, runner.reward_score = 0, 0
+        n = runner.worker()
+        t1 = time.perf_counter()
+        ppo.learn()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        return n, t1 - t0, t2 - t1, runner.last_vector_steps
+
+    for _ in range(args.warmup):
+        iteration()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    recs = [iteration() for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+
+    n_local = float(sum(r[0] for r in recs))
+    roll_t = float(sum(r[1] for r in recs))
+    learn_t = float(sum(r[2] for r in recs))
+    vec_steps = float(np.mean([r[3] for r in recs]))
+    stats = torch.tensor([elapsed, n_local, roll_t, learn_t, learn_t / max(n_local, 1)],
+                         dtype=torch.float64, device="cuda")
+    if world > 1:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, total_n = float(mx[0]), float(sm[1])
+        roll_max, learn_per_tr = float(mx[2]), float(mx[4])
+    else:
+        total_n, roll_max, learn_per_tr = n_local, roll_t, learn_t / max(n_local, 1)
+
+    roofline = None
+    if gae_call.args is not None:
+        a, k = gae_call.args
+        n_gae = a[2].numel()
+        cold_med, cold_min = time_kernel(lambda: prl_native.gae(*a, **k), cold=True)
+        warm_med, _ = time_kernel(lambda: prl_native.gae(*a, **k), cold=False)
+        achieved = GAE_BYTES_PER_TRANSITION * n_gae / (cold_med * 1e-3) / 1e9
+        roofline = {"kernel": "prl_gae: gae_kernel<true> (single-pass segmented GAE scan)",
+                    "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_us": round(cold_med * 1e3, 2), "cache": "cold (512 MiB flush)",
+                    "warm_launch_us": round(warm_med * 1e3, 2),
+                    "warm_achieved": round(GAE_BYTES_PER_TRANSITION * n_gae / (warm_med * 1e-3)
+                                           / 1e9, 1),
+                    "transitions_per_launch": int(n_gae),
+                    "bytes_per_transition": GAE_BYTES_PER_TRANSITION}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["env"] == "CartPole-v1":
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import cpu_port
+        n_cpu, tr, tl, threads = cpu_port.cpu_iteration(E=args.cpu_envs, mb=cfg["mb"],
+                                                        k_epochs=cfg["k_epochs"])
+        cpu = {"value": round(n_cpu / (tr + tl), 1), "unit": "env-steps/s", "cores": threads,
+               "kind": "port",
+               "sample": f"one CartPole iteration at num_envs={args.cpu_envs} ({n_cpu} "
+                         f"transitions): C per-env stepping {tr:.2f}s + torch-CPU learn "
+                         f"(mb={cfg['mb']}, k={cfg['k_epochs']}) {tl:.2f}s",
+               "rollout_env_steps_per_s": round(n_cpu / tr, 1),
+               "learn_ms_per_1M": round(tl / n_cpu * (1 << 20) * 1e3, 1)}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(total_n / elapsed, 1), "unit": "env-steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{args.config}: {cfg['env']} num_envs={cfg['num_envs']}/GPU, "
+                                   f"one episode per env per iteration, learn() batch>="
+                                   f"{cfg['batch_size']} gamma=0.995 GAE_lambda=0.95 "
+                                   f"k_epochs={cfg['k_epochs']} mini_batch={cfg['mb']}"
+                                   + (" use_RND" if cfg["rnd"] else ""),
+                       "env": cfg["env"], "num_envs_per_gpu": cfg["num_envs"],
+                       "global_num_envs": cfg["num_envs"] * world,
+                       "mini_batch_size": cfg["mb"], "k_epochs": cfg["k_epochs"],
+                       "parallelism": f"dp{world}"},
+            "rollout_env_steps_per_s": round(total_n / max(roll_max, 1e-9), 1),
+            "learn_ms_per_1M": round(learn_per_tr * (1 << 20) * 1e3, 1),
+            "transitions_per_step": round(total_n / args.steps, 1),
+            "vector_steps_per_rollout": vec_steps,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -10,7 +10,10 @@
  *
  * Conventions (all entry points):
  *   - every pointer is a caller-owned DEVICE pointer unless the comment says "host";
- *   - nothing allocates: scratch comes in through `workspace` (size from prl_workspace_bytes);
+ *   - nothing allocates: scratch comes in through `workspace` (size from prl_workspace_bytes).
+ *     The GAE / statistics / surrogate workspaces carry in-launch synchronisation state: they
+ *     must be zero-initialised ONCE, dedicated to one op and one stream, and every launch
+ *     leaves them re-armed (so each call is a single kernel launch, graph-capturable);
  *   - every call is asynchronous on `stream` (a hipStream_t passed as void*; NULL = null stream)
  *     and contains no host synchronisation, so callers may capture it into a hipGraph;
  *   - return 0 on success, a negative prl_status on failure; prl_last_error() then holds a
@@ -45,7 +48,8 @@ enum prl_op {
   PRL_OP_GAE = 0,        /* n = transitions                 */
   PRL_OP_SURROGATE = 1,  /* n = minibatch size              */
   PRL_OP_SCAN = 2,       /* n = elements (scan/compaction)  */
-  PRL_OP_STATS = 3       /* n = elements (prl_adv_stats)    */
+  PRL_OP_STATS = 3,      /* n = elements (prl_adv_stats)    */
+  PRL_OP_GN = 4          /* n = rows (prl_gn_silu_bwd)      */
 };
 
 /* ---- housekeeping ------------------------------------------------------------------------- */
@@ -164,6 +168,18 @@ int prl_rnd_forward(const float* x, int64_t n, int32_t D,
                     const float* t_w2, const float* t_b2,
                     const float* p_w1, const float* p_b1, const float* p_gw, const float* p_gb,
                     const float* p_w2, const float* p_b2, float beta, float* out, void* stream);
+
+/* ---- actor-critic / RND hidden blocks ------------------------------------------------------ */
+/* GroupNorm(groups=8, C=64, eps) + SiLU over x[N][64] (PPO/ActorCritic.py:19-60, PPO/RND.py:25-30):
+ * out = silu(groupnorm(x) * w + b) (silu = 0: groupnorm only).  Replaces nn.GroupNorm + nn.SiLU on
+ * device tensors (the PyTorch-ROCm GroupNorm backward in this image returns wrong dw/db for
+ * N >= 512 rows).  x/out 16-B aligned. */
+int prl_gn_silu_fwd(const float* x, int64_t N, int32_t C, int32_t groups, const float* w,
+                    const float* b, float eps, int32_t silu, float* out, void* stream);
+/* Backward of the above: dx[N][64], dw[64], db[64] (column sums over rows, deterministic). */
+int prl_gn_silu_bwd(const float* x, const float* dout, int64_t N, int32_t C, int32_t groups,
+                    const float* w, const float* b, float eps, int32_t silu, float* dx, float* dw,
+                    float* db, void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -9,7 +9,7 @@ so `Policy_weights.pth` state_dicts load either way (SURVEY.md §3.5 keys):
 The continuous policy is the reference's MultivariateNormal(mu, diag(std^2)) with
 std = softplus(clamp(log_std, -2, 2)) (ActorCritic.py:90-102); it is evaluated as the equivalent
 diagonal Normal (Independent(Normal(mu, std), 1)): identical density/entropy, no batched
-Cholesky per minibatch.
+Cholesky per minibatch.  GroupNorm + SiLU run as one fused HIP op (layers.py).
 """
 from __future__ import annotations
 
@@ -17,9 +17,7 @@ import torch
 import torch.nn.functional as F
 from torch import distributions, nn
 
-
-def _block(i, o, bias=False):
-    return [nn.Linear(i, o, bias=bias), nn.GroupNorm(64 // 8, 64), nn.SiLU(inplace=True)]
+from .layers import GroupNormSiLU, hidden_block as _block
 
 
 class ActorCritic(nn.Module):
@@ -45,7 +43,7 @@ class ActorCritic(nn.Module):
                 nn.init.xavier_uniform_(m.weight)
                 if m.bias is not None:
                     nn.init.normal_(m.bias, mean=0, std=0.01)
-            elif isinstance(m, nn.GroupNorm):
+            elif isinstance(m, (nn.GroupNorm, GroupNormSiLU)):
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
 

@@ -7,6 +7,7 @@
 int64_t prl_gae_workspace_bytes(int64_t n);
 int64_t prl_surrogate_workspace_bytes(int64_t mb);
 int64_t prl_scan_workspace_bytes(int64_t n);
+int64_t prl_gn_workspace_bytes(int64_t n);
 
 namespace prl {
 static thread_local char g_err[512] = "";
@@ -31,6 +32,7 @@ extern "C" int64_t prl_workspace_bytes(int op, int64_t n) {
     case PRL_OP_STATS: return prl_gae_workspace_bytes(n);
     case PRL_OP_SURROGATE: return prl_surrogate_workspace_bytes(n);
     case PRL_OP_SCAN: return prl_scan_workspace_bytes(n);
+    case PRL_OP_GN: return prl_gn_workspace_bytes(n);
     default: return -1;
   }
 }

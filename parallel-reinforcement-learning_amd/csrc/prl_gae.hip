@@ -16,49 +16,103 @@
 // output is bit-identical for finite inputs (a non-finite carry would leak through 0*inf = NaN in
 // the reference; here the chain restarts at d = 1).
 //
-// Work decomposition (single pass, one launch):
-//   * a tile = 256 threads x 8 consecutive elements = 2048 elements, loaded with 16-B vector
-//     loads; delta_t and c_t are formed elementwise and staged in LDS;
-//   * each thread first finishes everything at or left of the LAST break in its own chunk, then
+// Work decomposition (single pass, ONE launch, no host-side memset):
+//   * tile = 256 threads x 8 consecutive elements = 2048 elements, 16-B vector loads; delta_t and
+//     c_t are formed elementwise and staged in LDS;
+//   * each thread finishes everything at or left of the LAST break in its own chunk, then
 //     resolves its tail from the nearest chunk to the right that has a break (LDS), re-evaluating
 //     break-free chunks in between sequentially;
-//   * tiles are claimed in REVERSE order from an atomic ticket, and a tile publishes its carry-out
-//     g[first element] as one 8-byte {tag, value} granule with a single agent-scope store (the
-//     data is the flag, MI355X guide Guideline 16 R2) as soon as it is known — before it waits.
-//     A tile whose tail runs into the next tile polls that tile's granule (relaxed agent-scope
-//     loads, bounded spin).  Tickets guarantee the waited-on tile has been dispatched, so the
-//     look-back chain always drains; with episodes shorter than a tile it is one hop long.
-//   * when adv is requested, each tile writes {sum adv, sum adv^2} (f64) and the last tile to
-//     arrive reduces all tiles IN TILE ORDER (deterministic) into sums_out (release fence ->
-//     counter -> acquire fence, Guideline 16 counter form).
+//   * workgroup b owns tile ntiles-1-b (reverse), so a tile's successor is normally already
+//     running.  A tile publishes its carry-out g[first element] as one 8-byte {epoch, value}
+//     granule with one agent-scope store (data = flag, MI355X guide Guideline 16 R2) as soon as
+//     it is known, before it ever waits.  A tile whose tail runs into the next tile polls that
+//     granule for a bounded time; if it does not appear (the successor was not dispatched yet —
+//     HIP promises no dispatch order), the tile computes the carry itself by look-ahead: the same
+//     sequential chain over the successor's head segment, so the result is bit-identical and
+//     correctness never depends on placement or order.  No ticket atomic: a single contended word
+//     caps at ~88 ops/us on MI355X (guide: dequeue row), i.e. ~73 us at 6400 tiles.
+//   * statistics: when adv is requested each tile hands {sum adv, sum adv^2} (f64) to its
+//     64-tile group with write-through (sc1) stores + s_waitcnt vmcnt(0) + the group counter
+//     (one counter per 64-B line); the last tile of a group folds the group (tile order) and
+//     bumps the global counter; the last group folds the groups (group order) -> sums_out.
+//     Deterministic, no L2 write-back fences, <= 64 arrivals per contended word.
+//   * the workspace is zero-initialised once by the caller and re-armed by every launch (the
+//     last arriver resets the counters and advances the epoch used as the granule tag); its
+//     layout depends only on the buffer's size, so calls of different n can share it.
 #include "prl_common.h"
+
+#include <algorithm>
 
 namespace prl {
 
 constexpr int GAE_THREADS = 256;
 constexpr int GAE_EPT = 8;
 constexpr int GAE_TILE = GAE_THREADS * GAE_EPT;
-constexpr unsigned GAE_SPIN_LIMIT = 1u << 26;
-
-struct GaeWs {
-  unsigned* ctrs;               // [0] ticket, [1] arrivals, [2] timeout flag, [3] pad
-  unsigned long long* gran;     // [ntiles] {tag << 32 | float bits}
-  double2* tile_sums;           // [ntiles]
-};
+constexpr int GAE_GROUP = 64;                 // tiles per arrival group
+constexpr unsigned GAE_SPIN_LIMIT = 4096;     // ~100 us of s_sleep(1) polls before look-ahead
 
 __host__ __device__ inline int64_t gae_ntiles(int64_t n) { return (n + GAE_TILE - 1) / GAE_TILE; }
-inline int64_t gae_memset_bytes(int64_t ntiles) { return ((16 + 8 * ntiles) + 15) / 16 * 16; }
-inline int64_t gae_ws_bytes(int64_t n) {
-  const int64_t nt = gae_ntiles(n);
-  return gae_memset_bytes(nt) + 16 * nt + 16;
+__host__ __device__ inline int64_t gae_ngroups(int64_t nt) { return (nt + GAE_GROUP - 1) / GAE_GROUP; }
+
+struct GaeWs {
+  unsigned* ctrs;               // [0] spare, [1] group arrivals, [2] look-ahead count, [3] epoch
+  unsigned* group_ctr;          // [ngroups], one per 64-B line (stride 16 words)
+  unsigned long long* gran;     // [ntiles] {epoch << 32 | float bits}
+  double2* tile_sums;           // [ntiles]
+  double2* group_sums;          // [ngroups]
+};
+
+inline int64_t gae_ws_bytes_tiles(int64_t nt) {
+  const int64_t ng = gae_ngroups(nt);
+  return 64 + 64 * ng + ((8 * nt + 15) / 16) * 16 + 16 * nt + 16 * ng + 64;
 }
-inline GaeWs gae_ws_carve(void* ws, int64_t ntiles) {
+inline int64_t gae_ws_bytes(int64_t n) { return gae_ws_bytes_tiles(gae_ntiles(n)); }
+// The layout is carved for the largest tile count the BUFFER can hold, never for the current n:
+// one buffer serves calls of every size, and the counters it keeps armed between launches must
+// sit at the same offsets in all of them (bytes(nt) <= 216 + 25.25 * nt).
+inline int64_t gae_capacity_tiles(int64_t bytes) {
+  int64_t nt = std::max<int64_t>(1, (int64_t)((double)(bytes - 216) / 25.25));
+  while (nt > 1 && gae_ws_bytes_tiles(nt) > bytes) --nt;
+  return nt;
+}
+inline GaeWs gae_ws_carve(void* ws, int64_t nt) {
+  const int64_t ng = gae_ngroups(nt);
   char* p = static_cast<char*>(ws);
   GaeWs w;
   w.ctrs = reinterpret_cast<unsigned*>(p);
-  w.gran = reinterpret_cast<unsigned long long*>(p + 16);
-  w.tile_sums = reinterpret_cast<double2*>(p + gae_memset_bytes(ntiles));
+  p += 64;
+  w.group_ctr = reinterpret_cast<unsigned*>(p);
+  p += 64 * ng;
+  w.gran = reinterpret_cast<unsigned long long*>(p);
+  p += ((8 * nt + 15) / 16) * 16;
+  w.tile_sums = reinterpret_cast<double2*>(p);
+  p += 16 * nt;
+  w.group_sums = reinterpret_cast<double2*>(p);
   return w;
+}
+
+__device__ inline unsigned long long ld_sc1(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_sc1(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_sc1_d2(double2* p, double2 v) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  st_sc1(q, __double_as_longlong(v.x));
+  st_sc1(q + 1, __double_as_longlong(v.y));
+}
+__device__ inline double2 ld_sc1_d2(const double2* p) {
+  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+  return double2{__longlong_as_double(ld_sc1(q)), __longlong_as_double(ld_sc1(q + 1))};
+}
+
+// one GAE step in the reference's float32 order
+__device__ inline float gae_delta(float r, float d, float v, float nv, float gf) {
+  float a = gf * nv;
+  a = a * (1.0f - d);
+  const float s = r + a;
+  return s - v;
 }
 
 __device__ inline float chunk_chain(const float* s_delta, const float* s_c, int chunk, float carry) {
@@ -69,49 +123,89 @@ __device__ inline float chunk_chain(const float* s_delta, const float* s_c, int 
   return carry;
 }
 
-__device__ inline void publish_granule(unsigned long long* g, float v) {
-  const unsigned long long word = (1ull << 32) | (unsigned long long)__float_as_uint(v);
-  __hip_atomic_store(g, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// g at index `start` computed from global memory: walk forward to the first break (c == 0) or
+// the end, then run the chain backward in the reference's order.  Used only when a successor's
+// granule did not show up in time; bit-identical to the granule path.
+__device__ float gae_lookahead(const float* r, const float* d, const float* V, float nv_end,
+                               int64_t n, float gf, float glf, int64_t start) {
+  int64_t p = start;
+  while (p < n && glf * (1.0f - d[p]) != 0.0f) ++p;
+  float g = 0.0f;
+  for (int64_t t = (p < n ? p : n - 1); t >= start; --t) {
+    const float nv = (t + 1 < n) ? V[t + 1] : nv_end;
+    g = gae_delta(r[t], d[t], V[t], nv, gf) + (glf * (1.0f - d[t])) * g;
+  }
+  return g;
 }
 
-// Last-arriver reduction of per-tile {sum, sumsq} into out[2], in tile order.
-__device__ inline void finalize_tile_sums(const double2* tile_sums, int64_t ntiles, unsigned* arrivals,
-                                          unsigned* flags, double* out, double2 mine, int64_t tile) {
-  __shared__ int s_last;
+// Block end.  Hands the tile's statistics to its group, the group's to the global fold, and
+// re-arms the workspace (see the file header).  Every thread of the block calls it.
+__device__ inline void gae_arrive(const GaeWs& ws, int64_t ntiles, int64_t tile, unsigned tag,
+                                  bool with_sums, double2 mine, double* out) {
+  __shared__ int s_stage;  // 0: done, 1: last of group, 2: last overall
   __shared__ double s_part[2][GAE_THREADS / 64];
+  const int64_t ng = gae_ngroups(ntiles);
+  const int64_t g = tile / GAE_GROUP;
+  const int64_t g0 = g * GAE_GROUP;
+  const int64_t gsize = std::min<int64_t>(GAE_GROUP, ntiles - g0);
   if (threadIdx.x == 0) {
-    double2* ts = const_cast<double2*>(tile_sums);
-    ts[tile] = mine;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (old == (unsigned)(ntiles - 1)) ? 1 : 0;
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (with_sums) {
+      st_sc1_d2(ws.tile_sums + tile, mine);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    unsigned* gc = ws.group_ctr + 16 * g;
+    const unsigned old = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_stage = (old == (unsigned)(gsize - 1)) ? 1 : 0;
   }
   __syncthreads();
-  if (!s_last) return;
-  // fixed partition: thread j sums tiles j, j+256, ... in order; then a fixed-order tree.
-  double a = 0.0, b = 0.0;
-  for (int64_t t = threadIdx.x; t < ntiles; t += GAE_THREADS) {
-    const double2 v = tile_sums[t];
-    a += v.x;
-    b += v.y;
-  }
-  a = wave_sum(a);
-  b = wave_sum(b);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0) { s_part[0][wid] = a; s_part[1][wid] = b; }
+  if (s_stage == 0) return;
+  // last tile of group g: fold the group's tile sums in tile order (lanes load in parallel)
+  __shared__ double2 s_tiles[GAE_GROUP];
+  if (with_sums && threadIdx.x < gsize) s_tiles[threadIdx.x] = ld_sc1_d2(ws.tile_sums + g0 + threadIdx.x);
   __syncthreads();
   if (threadIdx.x == 0) {
-    double sa = 0.0, sb = 0.0;
-    for (int w = 0; w < GAE_THREADS / 64; ++w) { sa += s_part[0][w]; sb += s_part[1][w]; }
-    out[0] = sa;
-    out[1] = sb;
-    (void)flags;
+    double2 acc{0.0, 0.0};
+    if (with_sums)
+      for (int64_t t = 0; t < gsize; ++t) {
+        acc.x += s_tiles[t].x;
+        acc.y += s_tiles[t].y;
+      }
+    __hip_atomic_store(ws.group_ctr + 16 * g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (with_sums) st_sc1_d2(ws.group_sums + g, acc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(&ws.ctrs[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_stage = (old == (unsigned)(ng - 1)) ? 2 : 0;
   }
+  __syncthreads();
+  if (s_stage != 2) return;
+  if (with_sums) {  // last group: fold the groups in group order
+    double a = 0.0, b = 0.0;
+    for (int64_t t = threadIdx.x; t < ng; t += GAE_THREADS) {
+      const double2 v = ld_sc1_d2(ws.group_sums + t);
+      a += v.x;
+      b += v.y;
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) { s_part[0][wid] = a; s_part[1][wid] = b; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double sa = 0.0, sb = 0.0;
+      for (int w = 0; w < GAE_THREADS / 64; ++w) { sa += s_part[0][w]; sb += s_part[1][w]; }
+      out[0] = sa;
+      out[1] = sb;
+    }
+  }
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&ws.ctrs[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ws.ctrs[3], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ inline unsigned gae_tag(const GaeWs& ws) {
+  const unsigned t = __hip_atomic_load(&ws.ctrs[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  return t ? t : 1u;
 }
 
 template <bool VEC>
@@ -123,17 +217,16 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
   __shared__ __attribute__((aligned(16))) float s_c[GAE_TILE];
   __shared__ float s_out[GAE_THREADS];
   __shared__ unsigned char s_hb[GAE_THREADS];
-  __shared__ unsigned s_ticket;
+  __shared__ unsigned s_tag;
   __shared__ int s_need;
   __shared__ float s_carry;
 
   const int tid = threadIdx.x;
   if (tid == 0) {
-    s_ticket = __hip_atomic_fetch_add(&ws.ctrs[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tag = gae_tag(ws);
     s_need = 0;
   }
-  __syncthreads();
-  const int64_t tile = ntiles - 1 - (int64_t)s_ticket;
+  const int64_t tile = ntiles - 1 - (int64_t)blockIdx.x;
   const int64_t i0 = tile * GAE_TILE + (int64_t)tid * GAE_EPT;
 
   float rr[GAE_EPT], dd[GAE_EPT], vv[GAE_EPT];
@@ -167,12 +260,8 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
     const int64_t i = i0 + k;
     float nv = (k + 1 < GAE_EPT) ? vv[k + 1] : vnext;
     if (i + 1 == n) nv = nv_end;
-    const float omd = 1.0f - dd[k];
-    float a = gf * nv;
-    a = a * omd;
-    const float s = rr[k] + a;
-    dl[k] = s - vv[k];
-    cc[k] = glf * omd;
+    dl[k] = gae_delta(rr[k], dd[k], vv[k], nv, gf);
+    cc[k] = glf * (1.0f - dd[k]);
   }
   {
     float4* sd4 = reinterpret_cast<float4*>(s_delta + tid * GAE_EPT);
@@ -201,6 +290,7 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
   s_hb[tid] = (pb >= 0) ? 1 : 0;
   s_out[tid] = (pb >= 0) ? g[0] : 0.0f;
   __syncthreads();
+  const unsigned tag = s_tag;
 
   // tail: resolve from the nearest chunk to the right that has a break
   bool resolved = (pb == GAE_EPT - 1);
@@ -224,7 +314,8 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
       s_need = 1;
     }
   }
-  if (tid == 0 && resolved) publish_granule(&ws.gran[tile], g[0]);
+  if (tid == 0 && resolved)
+    st_sc1(&ws.gran[tile], ((unsigned long long)tag << 32) | __float_as_uint(g[0]));
   __syncthreads();
 
   if (s_need) {
@@ -232,18 +323,21 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
       float cin = 0.0f;  // beyond the last element: gae = 0 (PPO.py:110)
       if (tile + 1 < ntiles) {
         unsigned spins = 0;
-        unsigned long long w;
+        bool got = false;
         for (;;) {
-          w = __hip_atomic_load(&ws.gran[tile + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((w >> 32) == 1ull) break;
-          if (++spins >= GAE_SPIN_LIMIT) {
-            __hip_atomic_fetch_or(&ws.ctrs[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            w = 0;
+          const unsigned long long w = ld_sc1(&ws.gran[tile + 1]);
+          if ((unsigned)(w >> 32) == tag) {
+            cin = __uint_as_float((unsigned)(w & 0xffffffffull));
+            got = true;
             break;
           }
+          if (++spins >= GAE_SPIN_LIMIT) break;
           __builtin_amdgcn_s_sleep(1);
         }
-        cin = __uint_as_float((unsigned)(w & 0xffffffffull));
+        if (!got) {
+          cin = gae_lookahead(r, d, V, nv_end, n, gf, glf, (tile + 1) * (int64_t)GAE_TILE);
+          __hip_atomic_fetch_add(&ws.ctrs[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       s_carry = cin;
     }
@@ -258,7 +352,8 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
           g[k] = carry;
         }
       }
-      if (tid == 0) publish_granule(&ws.gran[tile], g[0]);
+      if (tid == 0)
+        st_sc1(&ws.gran[tile], ((unsigned long long)tag << 32) | __float_as_uint(g[0]));
     }
   }
 
@@ -287,6 +382,7 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
       }
     }
   }
+  double2 mine{0.0, 0.0};
   if (adv) {
     double s1 = 0.0, s2 = 0.0;
 #pragma unroll
@@ -303,17 +399,18 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
     const int lane = tid & 63, wid = tid >> 6;
     if (lane == 0) { s_red[0][wid] = s1; s_red[1][wid] = s2; }
     __syncthreads();
-    double2 mine{0.0, 0.0};
     if (tid == 0)
       for (int w = 0; w < GAE_THREADS / 64; ++w) { mine.x += s_red[0][w]; mine.y += s_red[1][w]; }
-    finalize_tile_sums(ws.tile_sums, ntiles, &ws.ctrs[1], &ws.ctrs[2], sums_out, mine, tile);
   }
+  gae_arrive(ws, ntiles, tile, tag, adv != nullptr, mine, sums_out);
 }
 
-// Plain statistics pass (prl_adv_stats): per-tile sums + last-arriver ordered reduction.
+// Plain statistics pass (prl_adv_stats): per-tile sums + grouped ordered fold.
 __global__ __launch_bounds__(GAE_THREADS) void stats_kernel(const float* __restrict__ x, int64_t n,
                                                             GaeWs ws, int64_t ntiles,
                                                             double* __restrict__ sums_out) {
+  __shared__ unsigned s_tag;
+  if (threadIdx.x == 0) s_tag = gae_tag(ws);
   const int64_t tile = blockIdx.x;
   const int64_t i0 = tile * GAE_TILE + (int64_t)threadIdx.x * GAE_EPT;
   double s1 = 0.0, s2 = 0.0;
@@ -335,7 +432,7 @@ __global__ __launch_bounds__(GAE_THREADS) void stats_kernel(const float* __restr
   double2 mine{0.0, 0.0};
   if (threadIdx.x == 0)
     for (int w = 0; w < GAE_THREADS / 64; ++w) { mine.x += s_red[0][w]; mine.y += s_red[1][w]; }
-  finalize_tile_sums(ws.tile_sums, ntiles, &ws.ctrs[1], &ws.ctrs[2], sums_out, mine, tile);
+  gae_arrive(ws, ntiles, tile, s_tag, true, mine, sums_out);
 }
 
 // (x - mean) / (std_unbiased + eps) in float32, statistics from f64 sums (PPO.py:199).
@@ -385,8 +482,7 @@ extern "C" int prl_gae(const float* r, const float* d, const float* V, const flo
               "prl_gae: workspace too small (%lld < %lld)", (long long)workspace_bytes,
               (long long)gae_ws_bytes(n));
   hipStream_t s = as_stream(stream);
-  GaeWs ws = gae_ws_carve(workspace, nt);
-  PRL_HIP_TRY(hipMemsetAsync(workspace, 0, gae_memset_bytes(nt), s));
+  GaeWs ws = gae_ws_carve(workspace, gae_capacity_tiles(workspace_bytes));
   // gamma * nv * (1 - d): gamma is a weak Python float -> float32; gamma * lambda is a Python
   // float product (float64), rounded to float32 when it meets the float32 (1 - d).
   const float gf = (float)gamma;
@@ -415,8 +511,7 @@ extern "C" int prl_adv_stats(const float* x, int64_t n, double* sums_out, void* 
   PRL_REQUIRE(x, "prl_adv_stats: null x");
   const int64_t nt = gae_ntiles(n);
   PRL_REQUIRE(workspace && workspace_bytes >= gae_ws_bytes(n), "prl_adv_stats: workspace too small");
-  GaeWs ws = gae_ws_carve(workspace, nt);
-  PRL_HIP_TRY(hipMemsetAsync(workspace, 0, gae_memset_bytes(nt), s));
+  GaeWs ws = gae_ws_carve(workspace, gae_capacity_tiles(workspace_bytes));
   hipLaunchKernelGGL(stats_kernel, dim3((unsigned)nt), dim3(GAE_THREADS), 0, s, x, n, ws, nt, sums_out);
   PRL_LAUNCH_CHECK("adv_stats");
   return PRL_OK;

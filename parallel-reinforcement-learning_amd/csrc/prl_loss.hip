@@ -81,22 +81,24 @@ __global__ __launch_bounds__(SUR_THREADS) void surrogate_fwd_kernel(
     *loss_out = (float)loss;
     return;
   }
-  partials[blockIdx.x] = double2{bp, bv};
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  // hand-off of the block partials: write-through stores, drained, then the counter; the last
+  // arriver reads them with sc1 loads (no L2 write-back / invalidate fences)
+  unsigned long long* pp = reinterpret_cast<unsigned long long*>(partials + blockIdx.x);
+  __hip_atomic_store(pp, __double_as_longlong(bp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(pp + 1, __double_as_longlong(bv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned old = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (old != nb - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   double tp = 0.0, tv = 0.0;
+  const unsigned long long* pa = reinterpret_cast<const unsigned long long*>(partials);
   for (unsigned b = 0; b < nb; ++b) {  // block order: deterministic
-    const double2 v = partials[b];
-    tp += v.x;
-    tv += v.y;
+    tp += __longlong_as_double(__hip_atomic_load(pa + 2 * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    tv += __longlong_as_double(__hip_atomic_load(pa + 2 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
   const double loss = tp / (double)mb + (double)vf_coef * (tv / (double)mb) -
                       (double)ent_coef * (double)(entropy ? *entropy : 0.0f);
   *loss_out = (float)loss;
+  __hip_atomic_store(arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
 }
 
 __global__ __launch_bounds__(256) void surrogate_bwd_kernel(const float* __restrict__ grad_out,
@@ -136,9 +138,8 @@ extern "C" int prl_ppo_surrogate_fwd(const float* logp, const float* old_logp, c
   if (nb > 1) {
     PRL_REQUIRE(workspace && workspace_bytes >= prl_surrogate_workspace_bytes(mb),
                 "prl_ppo_surrogate_fwd: workspace too small");
-    arrivals = static_cast<unsigned*>(workspace);
+    arrivals = static_cast<unsigned*>(workspace);  // zero-initialised once; kernel re-arms it
     partials = reinterpret_cast<double2*>(static_cast<char*>(workspace) + 16);
-    PRL_HIP_TRY(hipMemsetAsync(workspace, 0, 16, s));
   }
   hipLaunchKernelGGL(surrogate_fwd_kernel, dim3((unsigned)nb), dim3(SUR_THREADS), 0, s, logp,
                      old_logp, adv, V, ret, entropy, mb, clip, vf_coef, ent_coef, loss_out, dlogp,

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PRL_HIP_LIB", os.path.join(_HERE, "libprl_hip.so"))
 
 ENV_KINDS = {"CartPole-v1": 0, "Pendulum-v1": 1, "SyntheticHumanoid-v0": 2}
-OP_GAE, OP_SURROGATE, OP_SCAN, OP_STATS = 0, 1, 2, 3
+OP_GAE, OP_SURROGATE, OP_SCAN, OP_STATS, OP_GN = 0, 1, 2, 3, 4
 
 _P = ctypes.c_void_p
 _I64, _I32, _U64, _F32, _F64, _INT = (ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64,
@@ -45,6 +45,8 @@ SIGNATURES = {
                               _I64, _P],
     "prl_ppo_surrogate_bwd": [_P, _P, _P, _I64, _P, _P, _P],
     "prl_rnd_forward": [_P, _I64, _I32] + [_P] * 12 + [_F32, _P, _P],
+    "prl_gn_silu_fwd": [_P, _I64, _I32, _I32, _P, _P, _F32, _I32, _P, _P],
+    "prl_gn_silu_bwd": [_P, _P, _I64, _I32, _I32, _P, _P, _F32, _I32, _P, _P, _P, _P, _I64, _P],
 }
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64}
 
@@ -97,17 +99,20 @@ def _stream():
 
 # ------------------------------------------------------------------------- workspace
 class _Workspace:
-    """Per-device scratch (grown, never shrunk).  Callers that capture graphs reserve first."""
+    """Per-(op, device) scratch, zero-initialised when (re)allocated, grown never shrunk.
+    The GAE / statistics / surrogate kernels keep their in-launch synchronisation state here
+    and leave it re-armed after every launch (include/prl_abi.h), so each op owns its buffer.
+    Callers that capture graphs reserve first (reserve_workspace)."""
 
     def __init__(self):
         self.buf = {}
 
-    def get(self, nbytes: int, device) -> torch.Tensor:
+    def get(self, op: int, nbytes: int, device) -> torch.Tensor:
         dev = torch.device(device)
-        key = (dev.type, dev.index)
+        key = (op, dev.type, dev.index)
         b = self.buf.get(key)
         if b is None or b.numel() < nbytes:
-            b = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+            b = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
             self.buf[key] = b
         return b
 
@@ -120,13 +125,14 @@ def workspace_bytes(op: int, n: int) -> int:
 
 
 def workspace(op: int, n: int, device) -> torch.Tensor:
-    return _ws.get(workspace_bytes(op, n), device)
+    return _ws.get(op, workspace_bytes(op, n), device)
 
 
 def reserve_workspace(n: int, device):
-    """Pre-grow the shared scratch so later calls (e.g. under graph capture) do not allocate."""
-    need = max(workspace_bytes(op, n) for op in (OP_GAE, OP_SURROGATE, OP_SCAN, OP_STATS))
-    return _ws.get(need, device)
+    """Pre-grow every op's scratch for n elements so later calls (e.g. under graph capture)
+    do not allocate."""
+    for op in (OP_GAE, OP_SURROGATE, OP_SCAN, OP_STATS, OP_GN):
+        workspace(op, n, device)
 
 
 # ------------------------------------------------------------------------- envs
@@ -290,3 +296,23 @@ def rnd_forward(x, tnet, pnet, beta, out):
             for p in (*tnet, *pnet)]
     _check(lib().prl_rnd_forward(_dev(x, torch.float32, "x"), n, D, *ptrs, float(beta),
                                  _dev(out, torch.float32, "out"), _stream()), "prl_rnd_forward")
+
+
+# ------------------------------------------------------------------------- GroupNorm + SiLU
+def gn_silu_fwd(x, w, b, eps, silu, out):
+    N = x.shape[0]
+    _check(lib().prl_gn_silu_fwd(_dev(x, torch.float32, "x"), N, x.shape[1], 8,
+                                 _dev(w, torch.float32, "w"), _dev(b, torch.float32, "b"),
+                                 float(eps), int(bool(silu)), _dev(out, torch.float32, "out"),
+                                 _stream()), "prl_gn_silu_fwd")
+
+
+def gn_silu_bwd(x, dout, w, b, eps, silu, dx, dw, db):
+    N = x.shape[0]
+    ws = workspace(OP_GN, N, x.device)
+    _check(lib().prl_gn_silu_bwd(_dev(x, torch.float32, "x"), _dev(dout, torch.float32, "dout"),
+                                 N, x.shape[1], 8, _dev(w, torch.float32, "w"),
+                                 _dev(b, torch.float32, "b"), float(eps), int(bool(silu)),
+                                 _dev(dx, torch.float32, "dx"), _dev(dw, torch.float32, "dw"),
+                                 _dev(db, torch.float32, "db"), _dev(ws), ws.numel(), _stream()),
+           "prl_gn_silu_bwd")

@@ -143,8 +143,8 @@ def test_surrogate_vs_reference_autograd(golden, tag):
             - 0.01 * float(g["step_H"][s])
         assert float(loss) == pytest.approx(ref_loss, rel=2e-5, abs=1e-6)
         scale = np.abs(g["step_dlogp"][sl]).max() + 1e-30
-        np.testing.assert_allclose(dl.cpu().numpy(), g["step_dlogp"][sl], rtol=2e-4,
-                                   atol=2e-6 * scale)
+        np.testing.assert_allclose(dl.cpu().numpy(), g["step_dlogp"][sl], rtol=4e-6,
+                                   atol=1e-7 * scale)
         np.testing.assert_allclose(dv.cpu().numpy(), g["step_dV"][sl], rtol=1e-5, atol=1e-9)
         # backward: upstream gradient scales the unit gradients
         go = torch.tensor(2.5, device=DEV)
@@ -173,7 +173,7 @@ def test_surrogate_multiblock_vs_oracle(mb):
     N.surrogate_fwd(T(lp), T(old), T(adv), T(V), T(ret), T(np.float32(H).reshape(())), 0.2, 0.5,
                     0.01, loss, dl, dv)
     assert float(loss) == pytest.approx(loss_ref, rel=1e-5, abs=1e-6)
-    np.testing.assert_allclose(dl.cpu().numpy(), dl_ref, rtol=1e-4, atol=1e-6 / mb)
+    np.testing.assert_allclose(dl.cpu().numpy(), dl_ref, rtol=4e-6, atol=1e-8 / mb)
     np.testing.assert_allclose(dv.cpu().numpy(), dv_ref, rtol=1e-5, atol=1e-9)
 
 
@@ -515,3 +515,58 @@ def test_flatten_large_vs_numpy(E, D):
     np.testing.assert_array_equal(A.cpu().numpy(), act[t_of, e_of])
     np.testing.assert_array_equal(R.cpu().numpy(), rew[t_of, e_of])
     np.testing.assert_array_equal(Dn.cpu().numpy(), done[t_of, e_of].astype(np.float32))
+
+
+# ---------------------------------------------------------------------------------- GroupNorm
+def _gn_silu_f64(x, w, b, dout, eps=1e-5):
+    x = torch.tensor(x, dtype=torch.float64, requires_grad=True)
+    w = torch.tensor(w, dtype=torch.float64, requires_grad=True)
+    b = torch.tensor(b, dtype=torch.float64, requires_grad=True)
+    N = x.shape[0]
+    g = x.view(N, 8, 8)
+    mu = g.mean(-1, keepdim=True)
+    var = g.var(-1, unbiased=False, keepdim=True)
+    y = ((g - mu) / torch.sqrt(var + eps)).view(N, 64) * w + b
+    z = y * torch.sigmoid(y)
+    z.backward(torch.tensor(dout, dtype=torch.float64))
+    return z.detach().numpy(), x.grad.numpy(), w.grad.numpy(), b.grad.numpy()
+
+
+@pytest.mark.parametrize("N", [1, 7, 31, 512, 513, 7681, 65_536])
+def test_gn_silu_fwd_bwd_vs_float64(N):
+    """The fused GroupNorm(8,64)+SiLU against a float64 restatement — including N >= 512, where
+    PyTorch-ROCm's own GroupNorm backward returns wrong dw/db (tools/diag_groupnorm.py)."""
+    N_ = native()
+    rng = np.random.default_rng(N)
+    x = (rng.normal(size=(N, 64)) * 3 + 1).astype(np.float32)
+    w = (rng.normal(size=64) * 0.5 + 1).astype(np.float32)
+    b = (rng.normal(size=64) * 0.1).astype(np.float32)
+    dz = rng.normal(size=(N, 64)).astype(np.float32)
+    z_ref, dx_ref, dw_ref, db_ref = _gn_silu_f64(x, w, b, dz)
+    out = torch.empty(N, 64, dtype=torch.float32, device=DEV)
+    N_.gn_silu_fwd(T(x), T(w), T(b), 1e-5, True, out)
+    dx = torch.empty_like(out)
+    dw = torch.empty(64, dtype=torch.float32, device=DEV)
+    db = torch.empty(64, dtype=torch.float32, device=DEV)
+    for _ in range(2):   # twice: the multi-block hand-off re-arms its workspace
+        N_.gn_silu_bwd(T(x), T(dz), T(w), T(b), 1e-5, True, dx, dw, db)
+    rel = lambda a, r: float(np.abs(a - r).max() / (np.abs(r).max() + 1e-30))  # noqa: E731
+    assert rel(out.cpu().numpy(), z_ref) < 2e-6
+    assert rel(dx.cpu().numpy(), dx_ref) < 1e-5
+    assert rel(dw.cpu().numpy(), dw_ref) < 2e-5
+    assert rel(db.cpu().numpy(), db_ref) < 2e-5
+
+
+def test_gn_silu_module_grads_match_cpu_reference():
+    from PPO.layers import GroupNormSiLU
+    torch.manual_seed(0)
+    m_cpu = torch.nn.Sequential(torch.nn.Linear(4, 64, bias=False), torch.nn.GroupNorm(8, 64),
+                                torch.nn.SiLU())
+    m_gpu = torch.nn.Sequential(torch.nn.Linear(4, 64, bias=False), GroupNormSiLU(8, 64),
+                                torch.nn.Identity()).cuda()
+    m_gpu.load_state_dict(m_cpu.state_dict())
+    x = torch.randn(2048, 4)
+    (m_cpu(x) ** 2).sum().backward()
+    (m_gpu(x.cuda()) ** 2).sum().backward()
+    for (n, a), (_, g) in zip(m_cpu.named_parameters(), m_gpu.named_parameters()):
+        torch.testing.assert_close(g.grad.cpu(), a.grad, rtol=2e-5, atol=2e-5, msg=n)

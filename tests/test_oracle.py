@@ -54,7 +54,7 @@ def test_surrogate_grads_vs_reference_autograd(golden, tag):
         loss, dlogp, dV = O.surrogate(lp[sl], old[sl], g["step_adv"][sl], V[sl], g["step_ret"][sl],
                                       H[s])
         scale = np.abs(g["step_dlogp"][sl]).max() + 1e-30
-        np.testing.assert_allclose(dlogp, g["step_dlogp"][sl], rtol=2e-4, atol=2e-6 * scale)
+        np.testing.assert_allclose(dlogp, g["step_dlogp"][sl], rtol=2e-6, atol=1e-7 * scale)
         np.testing.assert_allclose(dV, g["step_dV"][sl], rtol=1e-5, atol=1e-9)
         # the loss the reference back-propagated, rebuilt from its own captured pieces
         ref_loss = np.mean(-g["step_min"][sl].astype(np.float64)) + 0.5 * float(g["step_sl1"][s]) \

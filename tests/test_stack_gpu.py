@@ -1,0 +1,243 @@
+"""The drop-in API on the GPU: EnvVectorizer / utils / AsyncPPO.worker / PPO.learn against the
+reference's golden vectors and the oracle."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def test_env_vectorizer_vs_reference_fixture(golden):
+    """The reference's EnvVectorizer over (restated) gymnasium envs, same seeds, same actions:
+    compacted outputs and envs_active masks; masks exact, observations within trig ulps."""
+    from AsyncTools.AsyncPPO import EnvVectorizer
+    g = golden("envs")
+    for name, env_id in (("cartpole", "CartPole-v1"), ("pendulum", "Pendulum-v1")):
+        seeds = g[f"{name}_seeds"]
+        vec = EnvVectorizer(env_id, len(seeds), seed=int(seeds[0]))
+        vec.reset()                        # the reset(seed=...) draw
+        obs0, infos = vec.reset()          # EnvVectorizer.reset(): second draw
+        np.testing.assert_array_equal(obs0, g[f"{name}_obs0"])
+        assert len(infos) == len(seeds)
+        off = 0
+        for step, n in enumerate(g[f"{name}_nact"]):
+            n = int(n)
+            if n < 0:
+                o, _ = vec.reset()
+                np.testing.assert_array_equal(o, g[f"{name}_obs"][off:off - n])
+                off += -n
+                continue
+            acts = g[f"{name}_act"][off:off + n]
+            if name == "cartpole":
+                acts = acts[:, 0].astype(np.int64)
+            o, r, d, tr, inf = vec.step(acts)
+            sl = slice(off, off + n)
+            assert o.shape == (n, g[f"{name}_obs"].shape[1]) and len(inf) == n
+            np.testing.assert_allclose(o, g[f"{name}_obs"][sl], rtol=0, atol=1e-5)
+            np.testing.assert_allclose(r, g[f"{name}_rew"][sl], rtol=1e-9, atol=1e-9)
+            np.testing.assert_array_equal(d, g[f"{name}_term"][sl])
+            np.testing.assert_array_equal(tr, g[f"{name}_trunc"][sl])
+            m = vec.envs_active
+            m[np.where(~m)[0]] = d | tr
+            vec.envs_active = m
+            np.testing.assert_array_equal(vec.envs_active, g[f"{name}_mask"][step])
+            off += n
+
+
+def test_utils_numpy_api_vs_oracle():
+    import AsyncTools.utils as U
+    rng = np.random.default_rng(0)
+    for E in (1, 4, 33, 5000):
+        m = rng.random(E) < 0.4
+        np.testing.assert_array_equal(U.indexes_of_active_environments(E, m),
+                                      O.indexes_of_active_environments(E, m))
+        assert U.number_of_active_environments(m) == O.number_of_active_environments(m)
+        np.testing.assert_array_equal(U.range_of_active_environments(m),
+                                      np.arange(O.number_of_active_environments(m)))
+        s = rng.normal(size=(E, 4))
+        d = rng.random(E) < 0.5
+        np.testing.assert_array_equal(U.inactive_states_dropout(s, d), O.inactive_states_dropout(s, d))
+        n = int(np.sum(~m))
+        dn = rng.random(n) < 0.3
+        ref = O.update_active_environments_list(m, dn)
+        out = U.update_active_environments_list(m, dn)
+        assert out is m                                # in place, like the reference
+        np.testing.assert_array_equal(out, ref)
+
+
+class _DetPPO:
+    """Duck-typed ppo for the compat worker: deterministic actions from the observation."""
+
+    def __init__(self):
+        from PPO import Memory
+        self.memory = Memory()
+
+    def get_action(self, states):
+        s = states.numpy()
+        return (s[:, 2] + 0.1 * s[:, 3] > 0).astype(np.int64)
+
+    def learn(self):
+        pass
+
+
+def test_compat_worker_vs_oracle_worker():
+    from AsyncTools.AsyncPPO import AsyncPPO
+    E, seed = 300, 42
+    ppo = _DetPPO()
+    a = AsyncPPO("CartPole-v1", ppo, num_envs=E, seed=seed)
+    a.step_score, a.reward_score = 0, 0
+    a.worker()
+    orc = O.CartPoleOracle(E)
+    orc.seed(np.arange(E) + seed)
+    ref = O.worker_oracle(orc, lambda s, idx, t: (s[:, 2] + 0.1 * s[:, 3] > 0).astype(np.int64))
+    np.testing.assert_array_equal(np.array(ppo.memory.states), ref["S"])
+    np.testing.assert_array_equal(np.array(ppo.memory.actions), ref["A"])
+    np.testing.assert_array_equal(np.array(ppo.memory.dones), ref["D"])
+    assert int(a.step_score) == ref["step_score"] == len(ref["S"])
+
+
+class _FixedDist:
+    def __init__(self, rows, scaling=None):
+        from PPO import Memory
+        self.memory = Memory()
+        self.rows = rows
+        self.action_scaling = scaling
+
+    def dist_params(self, obs):
+        return self.rows
+
+
+@pytest.mark.parametrize("E", [1, 2048, 65536])
+def test_device_worker_bit_exact_vs_oracle_worker(E):
+    from AsyncTools.AsyncPPO import AsyncPPO
+    seed = 7
+    probs = np.random.default_rng(E).dirichlet([2, 2], E).astype(np.float32)
+    stub = _FixedDist(torch.from_numpy(probs).cuda())
+    a = AsyncPPO("CartPole-v1", stub, num_envs=E, seed=seed)
+    n = a.worker()
+    S, A, R, Dn = (x.cpu().numpy() for x in stub.memory.device_tensors("cuda"))
+    orc = O.CartPoleOracle(E)
+    orc.seed(np.arange(E) + seed)
+    ss = a.sample_seed
+    ref = O.worker_oracle(orc, lambda s, idx, t: O.sample_categorical(
+        probs, ss, np.full(E, t, np.int32))[idx])
+    assert n == len(ref["S"]) == int(a.step_score)
+    np.testing.assert_array_equal(S, ref["S"])
+    np.testing.assert_array_equal(A, ref["A"])
+    np.testing.assert_array_equal(R, ref["R"])
+    np.testing.assert_array_equal(Dn, ref["D"])
+    assert float(a.reward_score) == float(ref["reward_score"])
+    # a second rollout reuses the buffers, continues every env's PCG64 stream
+    a.worker()
+    assert len(stub.memory) == n + len(stub.memory._segments[1][0])
+
+
+def test_device_worker_pendulum_shapes_and_truncation():
+    from AsyncTools.AsyncPPO import AsyncPPO
+    E = 4096
+    rows = torch.zeros(E, 2, device="cuda")
+    rows[:, 1] = 0.5
+    stub = _FixedDist(rows, scaling=2.0)
+    a = AsyncPPO("Pendulum-v1", stub, num_envs=E, seed=3)
+    n = a.worker()
+    assert n == 200 * E
+    S, A, R, Dn = stub.memory.device_tensors("cuda")
+    assert S.shape == (n, 3) and A.shape == (n, 1)
+    assert float(A.abs().max()) <= 2.0
+    d = Dn.view(E, 200)
+    assert int(d[:, -1].sum()) == E and int(d[:, :-1].sum()) == 0
+    assert a.last_vector_steps <= 200 + a.poll_lag + 1
+
+
+def test_learn_on_gpu_matches_reference_learn(golden):
+    """PPO.learn() through libprl_hip.so vs the reference's learn(): same seeded policy, same
+    memory -> same updated weights (GPU float32 GEMMs differ from CPU ones in rounding)."""
+    from PPO import PPO
+    for tag, cont in (("learn", False), ("learn_cont", True)):
+        g = golden(tag)
+        torch.manual_seed(0)
+        D, A = (3, 1) if cont else (4, 2)
+        p = PPO(is_continuous=cont, observ_dim=D, action_dim=A,
+                action_scaling=2.0 if cont else None, lr=1e-3, k_epochs=int(g["k_epochs"]),
+                policy_clip=0.2, GAE_lambda=0.95, gamma=0.995, batch_size=1024,
+                mini_batch_size=int(g["mb"]))
+        p.show_progress = False
+        for i in range(int(g["N"])):
+            p.memory.push(g["S"][i], g["A"][i] if cont else np.asarray(g["A"][i]), g["R"][i],
+                          g["Dn"][i])
+        p.learn()
+        sd = p.policy.state_dict()
+        for k in sd:
+            np.testing.assert_allclose(sd[k].cpu().numpy(), g["final/" + k], rtol=0, atol=2e-6,
+                                       err_msg=f"{tag}:{k}")
+
+
+def test_compute_gae_api_returns_reference_list(golden):
+    from PPO import PPO
+    g = golden("gae")
+    p = PPO(False, 4, 2, gamma=float(g["c_gamma"]), GAE_lambda=float(g["c_lam"]))
+    out = p.compute_gae(g["c_r"], g["c_d"], g["c_V"], g["c_nv"])
+    assert isinstance(out, list) and isinstance(out[0], np.float32)
+    np.testing.assert_array_equal(np.array(out).view(np.uint32), g["c_ret"].view(np.uint32))
+
+
+def test_rnd_module_matches_reference(golden):
+    from PPO import RND
+    g = golden("rnd")
+    for D in (4, 348):
+        r = RND(D, D, beta=0.001)
+        sd = {k[len(f"D{D}/"):]: torch.from_numpy(g[k]) for k in g.files if k.startswith(f"D{D}/")}
+        r.load_state_dict(sd)
+        x = torch.from_numpy(g[f"D{D}_x"]).cuda()
+        out = r.compute_intrinsic_reward(list(x.split(64)))
+        np.testing.assert_allclose(out.cpu().numpy(), g[f"D{D}_r"], rtol=2e-5, atol=1e-8)
+        r.update_pred(list(x.split(64)))   # stays PyTorch; must run
+
+
+def test_gae_graph_capture_replay():
+    """One prl_gae call is one kernel launch with a self-re-arming workspace: capture it in a
+    HIP graph and replay it; every replay is bit-exact."""
+    import prl_native
+    n = 300_000
+    g = torch.Generator(device="cuda").manual_seed(1)
+    r = torch.randn(n, device="cuda", generator=g)
+    V = torch.randn(n, device="cuda", generator=g)
+    d = (torch.rand(n, device="cuda", generator=g) < 0.05).float()
+    ret = torch.empty_like(V)
+    adv = torch.empty_like(V)
+    sums = torch.zeros(2, dtype=torch.float64, device="cuda")
+    prl_native.gae(r, d, V, None, 0.995, 0.95, ret, adv, sums)   # warm + allocate workspace
+    ref = O.gae(r.cpu().numpy(), d.cpu().numpy(), V.cpu().numpy(), float(V[-1]), 0.995, 0.95)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            prl_native.gae(r, d, V, None, 0.995, 0.95, ret, adv, sums)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(5):
+        ret.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(ret.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    a64 = (ref - V.cpu().numpy()).astype(np.float32).astype(np.float64)
+    assert float(sums[0]) == pytest.approx(a64.sum(), rel=1e-10, abs=1e-6)
+
+
+def test_training_improves_cartpole():
+    """End to end: AsyncPPO.run() with the device worker learns CartPole (episode length grows)."""
+    from AsyncTools.AsyncPPO import AsyncPPO
+    from PPO import PPO
+    torch.manual_seed(0)
+    ppo = PPO(False, 4, 2, lr=1e-3, k_epochs=4, batch_size=4096, mini_batch_size=4096)
+    ppo.show_progress = False
+    a = AsyncPPO("CartPole-v1", ppo, num_envs=1024, seed=0)
+    lens = []
+    for _ in range(12):
+        a.step_score, a.reward_score = 0, 0
+        n = a.worker()
+        lens.append(n / 1024)
+        ppo.learn()
+    assert np.mean(lens[-3:]) > 1.5 * np.mean(lens[:2]), lens
