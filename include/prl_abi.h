@@ -181,6 +181,22 @@ int prl_gn_silu_bwd(const float* x, const float* dout, int64_t N, int32_t C, int
                     const float* w, const float* b, float eps, int32_t silu, float* dx, float* dw,
                     float* db, void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ---- graph-captured optimizer step (PPO/PPO.py:219-255) ------------------------------------- */
+/* Copy rows [cursor[0]*mb, cursor[0]*mb + mb) of `count` (<= 6) row-major float tensors (widths in
+ * floats) into static minibatch buffers; rows past nrows are zero-filled.  srcs/dsts/widths are
+ * HOST arrays of device pointers; cursor is a device int64 (the minibatch index j). */
+int prl_gather_minibatch(const float* const* srcs, float* const* dsts, const int32_t* widths,
+                         int32_t count, const int64_t* cursor, int64_t mb, int64_t nrows,
+                         void* stream);
+/* torch.distributions.Categorical(probs).log_prob(actions) and .entropy() per row
+ * (ActorCritic.py:105,136-142): q = p/sum(p), logits = log(clamp(q, eps, 1-eps)).  entropy may be
+ * NULL.  actions are float class indices (the reference stores them as float32). */
+int prl_categorical_fwd(const float* probs, const float* actions, int64_t n, int32_t A,
+                        float* logp, float* entropy, void* stream);
+/* d log_prob / d probs for an upstream gradient dlogp[n]. */
+int prl_categorical_bwd(const float* probs, const float* actions, const float* dlogp, int64_t n,
+                        int32_t A, float* dprobs, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

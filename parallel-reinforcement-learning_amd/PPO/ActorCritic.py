@@ -17,7 +17,33 @@ import torch
 import torch.nn.functional as F
 from torch import distributions, nn
 
+import prl_native
+
 from .layers import GroupNormSiLU, hidden_block as _block
+
+
+class _CategoricalLogProb(torch.autograd.Function):
+    """Categorical(probs).log_prob(actions) + per-row entropy in one HIP kernel each way
+    (prl_categorical_fwd/bwd): same formulas as torch.distributions.Categorical, no host sync
+    (torch validates the simplex constraint with a host round trip), graph-capturable."""
+
+    @staticmethod
+    def forward(ctx, probs, actions):
+        probs = probs.contiguous()
+        actions = actions.to(torch.float32).contiguous()
+        logp = torch.empty(probs.shape[0], dtype=torch.float32, device=probs.device)
+        ent = torch.empty_like(logp)
+        prl_native.categorical_fwd(probs, actions, logp, ent)
+        ctx.save_for_backward(probs, actions)
+        ctx.mark_non_differentiable(ent)
+        return logp, ent
+
+    @staticmethod
+    def backward(ctx, dlogp, dent):
+        probs, actions = ctx.saved_tensors
+        dprobs = torch.empty_like(probs)
+        prl_native.categorical_bwd(probs, actions, dlogp.contiguous(), dprobs)
+        return dprobs, None
 
 
 class ActorCritic(nn.Module):
@@ -64,7 +90,8 @@ class ActorCritic(nn.Module):
         if self.is_continuous:
             mu = self.mu_head(features)
             std = F.softplus(torch.clamp(self.log_std_head(features), min=-2, max=2))
-            return distributions.Independent(distributions.Normal(mu, std), 1)
+            return distributions.Independent(
+                distributions.Normal(mu, std, validate_args=False), 1, validate_args=False)
         return distributions.Categorical(self.actor(features))
 
     def get_dist(self, state: torch.Tensor):  # ActorCritic.py:85-110
@@ -75,8 +102,12 @@ class ActorCritic(nn.Module):
 
     def get_evaluate(self, states: torch.Tensor, actions: torch.Tensor):  # :118-146
         features = self.model(states)
-        dist = self._dist(features)
-        log_probs = dist.log_prob(actions)
-        dist_entropy = dist.entropy().mean().detach()
+        if not self.is_continuous and features.is_cuda:
+            log_probs, ent = _CategoricalLogProb.apply(self.actor(features), actions)
+            dist_entropy = ent.mean().detach()
+        else:
+            dist = self._dist(features)
+            log_probs = dist.log_prob(actions)
+            dist_entropy = dist.entropy().mean().detach()
         state_value = self.critic(features).squeeze(-1)
         return log_probs, state_value, dist_entropy

@@ -86,7 +86,7 @@ class PPO:
         if use_RND:
             self.rnd.eval()
         self.loss_fn = nn.SmoothL1Loss()
-        self.optimizer = optim.AdamW(params=self.policy.parameters(), lr=lr)
+        self.optimizer = self._make_optimizer(lr)
 
         self.is_continuous = is_continuous
         self.action_scaling = action_scaling
@@ -108,19 +108,53 @@ class PPO:
         self.show_progress = True
         self.last_loss = None
         self._ops = prl_native              # HIP entry points (tests may substitute a fake)
+        self.use_graphs = True              # replay one captured optimizer step per minibatch
+        self.graph_min_steps = 16           # below this many graphable steps, stay eager
         self._flat_grad = None
         self._sync_initial_weights()
+
+    def _make_optimizer(self, lr):
+        """AdamW (PPO.py:53-56).  On the GPU: capturable (step count on device, so the step can
+        live in a HIP graph) and the fused single-kernel implementation when available."""
+        params = list(self.policy.parameters())
+        if params[0].is_cuda:
+            for kw in (dict(capturable=True, fused=True), dict(capturable=True, foreach=True)):
+                try:
+                    return optim.AdamW(params=params, lr=lr, **kw)
+                except (RuntimeError, TypeError, ValueError):
+                    continue
+        return optim.AdamW(params=params, lr=lr)
 
     # ---------------------------------------------------------------- data parallel helpers
     @staticmethod
     def _world():
         return tdist.get_world_size() if tdist.is_available() and tdist.is_initialized() else 1
 
+    @staticmethod
+    def _device_collectives():
+        return tdist.get_backend() == "nccl"   # RCCL on ROCm: device tensors directly
+
+    @classmethod
+    def all_reduce(cls, t):
+        """SUM over ranks in place (RCCL on device tensors; gloo through a host copy)."""
+        if cls._device_collectives() or not t.is_cuda:
+            tdist.all_reduce(t)
+        else:
+            h = t.cpu()
+            tdist.all_reduce(h)
+            t.copy_(h)
+        return t
+
     def _sync_initial_weights(self):
         if self._world() > 1:
             for m in (self.policy, self.policy_old) + ((self.rnd,) if self.use_RND else ()):
                 for t in list(m.parameters()) + list(m.buffers()):
-                    tdist.broadcast(t.data, src=0)
+                    if self._device_collectives() or not t.is_cuda:
+                        tdist.broadcast(t.data, src=0)
+                    else:
+                        h = t.data.cpu()
+                        tdist.broadcast(h, src=0)
+                        t.data.copy_(h)
 
     def _ensure_flat_grads(self):
         """Make every policy gradient a view of one flat buffer: one all-reduce per step."""
@@ -128,10 +162,12 @@ class PPO:
         total = sum(p.numel() for p in params)
         if self._flat_grad is None or self._flat_grad.numel() != total:
             self._flat_grad = torch.zeros(total, dtype=torch.float32, device=params[0].device)
-            off = 0
-            for p in params:
+        off = 0
+        base = self._flat_grad.data_ptr()
+        for p in params:  # re-attach views a set_to_none / graph epoch may have replaced
+            if p.grad is None or p.grad.data_ptr() != base + 4 * off:
                 p.grad = self._flat_grad[off:off + p.numel()].view_as(p)
-                off += p.numel()
+            off += p.numel()
         return self._flat_grad
 
     # ---------------------------------------------------------------- reference API
@@ -194,7 +230,8 @@ class PPO:
         world = self._world()
         n_local = len(self.memory)
         if world > 1:
-            ns = torch.tensor([n_local], dtype=torch.int64, device=self.device)
+            ns = torch.tensor([n_local], dtype=torch.int64,
+                              device=self.device if self._device_collectives() else "cpu")
             gathered = [torch.zeros_like(ns) for _ in range(world)]
             tdist.all_gather(gathered, ns)
             n_ranks = [int(x.item()) for x in gathered]
@@ -218,47 +255,71 @@ class PPO:
         sums = torch.zeros(2, dtype=torch.float64, device=self.device)
         self._ops.gae(R, Dn, old_V, old_V[-1:], self.gamma, self.GAE_lambda, returns, adv, sums)
         if world > 1:
-            tdist.all_reduce(sums)
+            self.all_reduce(sums)
         self._ops.adv_normalize(adv, sums, float(sum(n_ranks)), 1e-8, adv)
 
         self._update(S, A, old_logp, adv, returns, n_ranks)
         self.policy_old.load_state_dict(self.policy.state_dict())
 
     def _update(self, S, A, old_logp, adv, returns, n_ranks):
-        """k_epochs x sequential minibatches (PPO.py:219-255)."""
+        """k_epochs x sequential minibatches (PPO.py:219-255).  Full minibatches that every rank
+        has replay one captured HIP graph (update.py); the rest run eagerly, in order."""
         mb = self.mini_batch_size
         world = len(n_ranks)
-        N = S.shape[0]
         nb = max(-(-n // mb) for n in n_ranks)
         counts = [sum(min(mb, max(0, n - j * mb)) for n in n_ranks) for j in range(nb)]
-        params = [p for p in self.policy.parameters() if p.requires_grad]
-        flat = self._ensure_flat_grads() if world > 1 else None
+        n_graph = min(n // mb for n in n_ranks)
+        use_graph = (self.use_graphs and S.is_cuda
+                     and self.k_epochs * n_graph >= self.graph_min_steps)
+        graphed = None
+        if use_graph:
+            from .update import GraphedUpdate
+            scales = None
+            if world > 1:
+                scales = torch.tensor([mb / counts[j] for j in range(n_graph)],
+                                      dtype=torch.float32, device=S.device)
+            graphed = GraphedUpdate(self, S, A, old_logp, adv, returns, scales)
         pbar = tqdm(total=sum(n_ranks) * self.k_epochs, leave=False,
                     disable=not self.show_progress or (world > 1 and tdist.get_rank() != 0))
         loss = None
         for _ in range(self.k_epochs):
-            for j in range(nb):
-                lo, hi = j * mb, min((j + 1) * mb, N)
-                if flat is not None:
-                    flat.zero_()
-                else:
-                    self.optimizer.zero_grad()
-                if lo < hi:
-                    logp, V, H = self.policy.get_evaluate(S[lo:hi], A[lo:hi])
-                    loss = SurrogateLoss.apply(logp, old_logp[lo:hi], adv[lo:hi], V,
-                                               returns[lo:hi], H, self.policy_clip,
-                                               self.value_coef, self.entropy_coef, self._ops)
-                    scaled = loss * ((hi - lo) / counts[j]) if world > 1 else loss
-                    scaled.backward()
-                if flat is not None:
-                    tdist.all_reduce(flat)
-                nn.utils.clip_grad_norm_(params, 2.0)
-                self.optimizer.step()
+            j0 = 0
+            if graphed is not None:
+                j0 = graphed.run_epoch(n_graph)
+                loss = graphed.loss_out
+                pbar.update(sum(counts[:j0]))
+            for j in range(j0, nb):
+                out = self._eager_step(S, A, old_logp, adv, returns, j, counts[j], world)
+                loss = out if out is not None else loss
                 pbar.update(counts[j])
-        self.last_loss = loss.detach() if loss is not None else None
+        self.last_loss = loss.detach().clone() if loss is not None else None
+        self.last_graph_replays = graphed.replays if graphed is not None else 0
         if loss is not None and self.show_progress:
             pbar.set_description(f"Loss: {float(self.last_loss): .6f}")
         pbar.close()
+
+    def _eager_step(self, S, A, old_logp, adv, returns, j, count_j, world):
+        """One optimizer step on minibatch j (this rank's rows [j*mb, (j+1)*mb) ∩ [0, N))."""
+        mb = self.mini_batch_size
+        lo, hi = j * mb, min((j + 1) * mb, S.shape[0])
+        params = [p for p in self.policy.parameters() if p.requires_grad]
+        flat = self._ensure_flat_grads() if world > 1 else None
+        if flat is not None:
+            flat.zero_()
+        else:
+            self.optimizer.zero_grad()
+        loss = None
+        if lo < hi:
+            logp, V, H = self.policy.get_evaluate(S[lo:hi], A[lo:hi])
+            loss = SurrogateLoss.apply(logp, old_logp[lo:hi], adv[lo:hi], V, returns[lo:hi], H,
+                                       self.policy_clip, self.value_coef, self.entropy_coef,
+                                       self._ops)
+            (loss * ((hi - lo) / count_j) if world > 1 else loss).backward()
+        if flat is not None:
+            self.all_reduce(flat)
+        nn.utils.clip_grad_norm_(params, 2.0)
+        self.optimizer.step()
+        return loss
 
     def load_weights(self, path: str):  # PPO.py:262-277
         try:

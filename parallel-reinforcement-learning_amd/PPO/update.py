@@ -1,0 +1,124 @@
+"""Graph-captured PPO optimizer step (PPO/PPO.py:219-255).
+
+The reference runs k_epochs x ceil(N / mini_batch_size) optimizer steps in sequence (22,528 at
+N = 2^20, mb = 512): at that size each step is a few dozen tiny kernels, so the loop is bound by
+launch overhead, not by the GPU.  Here ONE full step — minibatch gather (device cursor) ->
+policy forward (PyTorch GEMMs, HIP GroupNorm+SiLU and Categorical) -> HIP surrogate -> autograd
+backward -> [RCCL all-reduce of the flat gradient] -> clip_grad_norm_(2.0) -> capturable AdamW ->
+cursor += 1 — is captured once per learn() into a HIP graph and replayed for every full
+minibatch, in order.  With world_size > 1 the step is two graphs (forward/backward/flatten, then
+clip/AdamW) and the RCCL all-reduce of the flat gradient is issued eagerly between the two
+replays: no collective is ever captured.  The first two minibatches of epoch 0 run eagerly on a side stream (the
+warm-up PyTorch requires before capture) and are real steps, so the sequence of updates is the
+reference's exactly.  Ragged / uneven minibatches (the last partial one, or ranks with fewer rows)
+run through PPO._eager_step.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+import prl_native
+
+
+class GraphedUpdate:
+    WARMUP = 2
+
+    def __init__(self, ppo, S, A, old_logp, adv, ret, scales=None):
+        from .PPO import SurrogateLoss
+        self.ppo = ppo
+        self.SurrogateLoss = SurrogateLoss
+        mb = ppo.mini_batch_size
+        dev = S.device
+        self.mb = mb
+        self.cursor = torch.zeros(1, dtype=torch.int64, device=dev)
+        A2 = A if A.dim() == 2 else A.view(-1, 1)
+        self.sources = [S.contiguous(), A2.contiguous(), old_logp.contiguous(), adv.contiguous(),
+                        ret.contiguous()]
+        self.S_mb = torch.empty(mb, S.shape[1], dtype=torch.float32, device=dev)
+        self.A_mb = torch.empty(mb, A2.shape[1], dtype=torch.float32, device=dev)
+        self.old_mb = torch.empty(mb, dtype=torch.float32, device=dev)
+        self.adv_mb = torch.empty(mb, dtype=torch.float32, device=dev)
+        self.ret_mb = torch.empty(mb, dtype=torch.float32, device=dev)
+        self.gather = prl_native.MinibatchGather(
+            self.sources, [self.S_mb, self.A_mb, self.old_mb, self.adv_mb, self.ret_mb],
+            self.cursor, mb)
+        self.A_eval = self.A_mb if A.dim() == 2 else self.A_mb.view(-1)
+        self.scales = scales          # device [n_steps] f32, world > 1 only
+        self.params = [p for p in ppo.policy.parameters() if p.requires_grad]
+        self.sizes = [p.numel() for p in self.params]
+        self.flat = torch.zeros(sum(self.sizes), dtype=torch.float32, device=dev)
+        self.graph_b = None
+        self.loss_out = torch.zeros((), dtype=torch.float32, device=dev)
+        self.graph = None
+        self.replays = 0
+        prl_native.reserve_workspace(mb, dev)
+
+    def _forward_backward(self):
+        ppo = self.ppo
+        self.gather()
+        logp, V, H = ppo.policy.get_evaluate(self.S_mb, self.A_eval)
+        loss = self.SurrogateLoss.apply(logp, self.old_mb, self.adv_mb, V, self.ret_mb, H,
+                                        ppo.policy_clip, ppo.value_coef, ppo.entropy_coef,
+                                        ppo._ops)
+        if self.scales is not None:
+            (loss * self.scales.index_select(0, self.cursor).reshape(())).backward()
+            torch.cat([p.grad.reshape(-1) for p in self.params], out=self.flat)
+        else:
+            loss.backward()
+        self.loss_out.copy_(loss.detach())
+
+    def _apply(self):
+        if self.scales is not None:
+            grads = [p.grad for p in self.params]
+            torch._foreach_copy_(grads, [f.view_as(g) for f, g in
+                                         zip(self.flat.split(self.sizes), grads)])
+        nn.utils.clip_grad_norm_(self.params, 2.0)
+        self.ppo.optimizer.step()
+        self.cursor.add_(1)
+
+    def _step_eager(self):
+        self.ppo.optimizer.zero_grad(set_to_none=True)
+        self._forward_backward()
+        if self.scales is not None:
+            self.ppo.all_reduce(self.flat)
+        self._apply()
+
+    def _replay(self):
+        self.replays += 1
+        if self.scales is None:
+            self.graph.replay()
+        else:  # the collective stays outside the graphs (eager RCCL between two replays)
+            self.graph.replay()
+            self.ppo.all_reduce(self.flat)
+            self.graph_b.replay()
+
+    def run_epoch(self, n_steps: int) -> int:
+        """Run minibatches 0 .. n_steps-1 of one epoch; returns n_steps."""
+        self.cursor.zero_()
+        done = 0
+        if self.graph is None:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(min(self.WARMUP, n_steps)):
+                    self._step_eager()
+                    done += 1
+            torch.cuda.current_stream().wait_stream(side)
+            if done == n_steps:
+                return done
+            self.ppo.optimizer.zero_grad(set_to_none=True)
+            self.graph = torch.cuda.CUDAGraph()
+            if self.scales is None:
+                with torch.cuda.graph(self.graph):
+                    self._forward_backward()
+                    self._apply()
+            else:
+                with torch.cuda.graph(self.graph):
+                    self._forward_backward()
+                self.graph_b = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph_b, pool=self.graph.pool()):
+                    self._apply()
+        for _ in range(n_steps - done):
+            self._replay()
+        return n_steps

@@ -1,0 +1,138 @@
+// prl_update.hip — pieces of the graph-captured PPO optimizer step (PPO/PPO.py:219-255).
+//
+// prl_gather_minibatch: the k_epochs x sequential, unshuffled minibatches of the reference
+//   (batch_packer = DataLoader without shuffle, PPO.py:98-105, :202-211) are row ranges of the
+//   env-major device tensors.  One captured graph serves every full minibatch: this kernel reads
+//   the minibatch index from a device cursor and copies rows [cursor*mb, cursor*mb + mb) of up to
+//   6 tensors into the graph's static inputs.
+// prl_categorical_fwd / _bwd: Categorical(probs).log_prob(a) and .entropy() exactly as
+//   torch.distributions.Categorical evaluates them (ActorCritic.py:105,136-142):
+//     q = p / sum(p);  logits = log(clamp(q, eps, 1 - eps));  logp = logits[a];
+//     H = -sum_k logits_k * q_k  (detached in the reference, so no gradient)
+//   and d logp / d p_j = m_a * (delta_aj / q_a - 1) / sum(p), m_a = [eps <= q_a <= 1 - eps]
+//   (clamp passes the gradient on the closed interval).
+#include "prl_common.h"
+
+#include <float.h>
+
+#include <algorithm>
+
+namespace prl {
+
+constexpr int GATHER_MAX = 6;
+struct GatherArgs {
+  const float* src[GATHER_MAX];
+  float* dst[GATHER_MAX];
+  int32_t width[GATHER_MAX];
+  int32_t count;
+};
+
+__global__ __launch_bounds__(256) void gather_minibatch_kernel(GatherArgs a, const int64_t* cursor,
+                                                               int64_t mb, int64_t nrows) {
+  const int64_t base = cursor[0] * mb;
+  for (int t = 0; t < a.count; ++t) {
+    const int w = a.width[t];
+    const int64_t total = mb * w;
+    const float* src = a.src[t] + base * w;
+    float* dst = a.dst[t];
+    const int64_t limit = (nrows - base) * w;  // never read past the source
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x)
+      dst[i] = i < limit ? src[i] : 0.0f;
+  }
+}
+
+__global__ __launch_bounds__(256) void categorical_fwd_kernel(const float* __restrict__ probs,
+                                                              const float* __restrict__ actions,
+                                                              int64_t n, int A,
+                                                              float* __restrict__ logp,
+                                                              float* __restrict__ entropy) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* p = probs + i * A;
+  float S = 0.f;
+  for (int k = 0; k < A; ++k) S += p[k];
+  const int a = (int)(int64_t)actions[i];  // value.long()
+  if (a < 0 || a >= A) {  // torch's gather would fault; flag the row instead of reading OOB
+    logp[i] = __builtin_nanf("");
+    if (entropy) entropy[i] = __builtin_nanf("");
+    return;
+  }
+  float h = 0.f, la = 0.f;
+  for (int k = 0; k < A; ++k) {
+    const float q = p[k] / S;
+    const float c = q < FLT_EPSILON ? FLT_EPSILON : (q > 1.0f - FLT_EPSILON ? 1.0f - FLT_EPSILON : q);
+    const float l = logf(c);
+    if (k == a) la = l;
+    h += l * q;
+  }
+  logp[i] = la;
+  if (entropy) entropy[i] = -h;
+}
+
+__global__ __launch_bounds__(256) void categorical_bwd_kernel(const float* __restrict__ probs,
+                                                              const float* __restrict__ actions,
+                                                              const float* __restrict__ dlogp,
+                                                              int64_t n, int A,
+                                                              float* __restrict__ dprobs) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* p = probs + i * A;
+  float S = 0.f;
+  for (int k = 0; k < A; ++k) S += p[k];
+  const int a = (int)(int64_t)actions[i];
+  if (a < 0 || a >= A) {
+    for (int k = 0; k < A; ++k) dprobs[i * A + k] = __builtin_nanf("");
+    return;
+  }
+  const float qa = p[a] / S;
+  const float m = (qa >= FLT_EPSILON && qa <= 1.0f - FLT_EPSILON) ? 1.0f : 0.0f;
+  const float g = dlogp[i] * m;
+  for (int k = 0; k < A; ++k) dprobs[i * A + k] = g * (((k == a) ? 1.0f / qa : 0.0f) - 1.0f) / S;
+}
+
+}  // namespace prl
+
+using namespace prl;
+
+extern "C" int prl_gather_minibatch(const float* const* srcs, float* const* dsts,
+                                    const int32_t* widths, int32_t count, const int64_t* cursor,
+                                    int64_t mb, int64_t nrows, void* stream) {
+  PRL_REQUIRE(count > 0 && count <= GATHER_MAX, "prl_gather_minibatch: 1..6 tensors");
+  PRL_REQUIRE(srcs && dsts && widths && cursor && mb > 0, "prl_gather_minibatch: bad arguments");
+  GatherArgs a{};
+  a.count = count;
+  for (int t = 0; t < count; ++t) {
+    PRL_REQUIRE(srcs[t] && dsts[t] && widths[t] > 0, "prl_gather_minibatch: tensor %d", t);
+    a.src[t] = srcs[t];
+    a.dst[t] = dsts[t];
+    a.width[t] = widths[t];
+  }
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(mb * 4, 256), 256);
+  hipLaunchKernelGGL(gather_minibatch_kernel, dim3(grid), dim3(256), 0, as_stream(stream), a,
+                     cursor, mb, nrows);
+  PRL_LAUNCH_CHECK("gather_minibatch");
+  return PRL_OK;
+}
+
+extern "C" int prl_categorical_fwd(const float* probs, const float* actions, int64_t n, int32_t A,
+                                   float* logp, float* entropy, void* stream) {
+  PRL_REQUIRE(n >= 0 && A >= 1, "prl_categorical_fwd: bad sizes");
+  if (n == 0) return PRL_OK;
+  PRL_REQUIRE(probs && actions && logp, "prl_categorical_fwd: null pointer");
+  hipLaunchKernelGGL(categorical_fwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), probs, actions, n, (int)A, logp, entropy);
+  PRL_LAUNCH_CHECK("categorical_fwd");
+  return PRL_OK;
+}
+
+extern "C" int prl_categorical_bwd(const float* probs, const float* actions, const float* dlogp,
+                                   int64_t n, int32_t A, float* dprobs, void* stream) {
+  PRL_REQUIRE(n >= 0 && A >= 1, "prl_categorical_bwd: bad sizes");
+  if (n == 0) return PRL_OK;
+  PRL_REQUIRE(probs && actions && dlogp && dprobs, "prl_categorical_bwd: null pointer");
+  hipLaunchKernelGGL(categorical_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), probs, actions, dlogp, n, (int)A, dprobs);
+  PRL_LAUNCH_CHECK("categorical_bwd");
+  return PRL_OK;
+}

@@ -47,6 +47,9 @@ SIGNATURES = {
     "prl_rnd_forward": [_P, _I64, _I32] + [_P] * 12 + [_F32, _P, _P],
     "prl_gn_silu_fwd": [_P, _I64, _I32, _I32, _P, _P, _F32, _I32, _P, _P],
     "prl_gn_silu_bwd": [_P, _P, _I64, _I32, _I32, _P, _P, _F32, _I32, _P, _P, _P, _P, _I64, _P],
+    "prl_gather_minibatch": [_P, _P, _P, _I32, _P, _I64, _I64, _P],
+    "prl_categorical_fwd": [_P, _P, _I64, _I32, _P, _P, _P],
+    "prl_categorical_bwd": [_P, _P, _P, _I64, _I32, _P, _P],
 }
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64}
 
@@ -316,3 +319,48 @@ def gn_silu_bwd(x, dout, w, b, eps, silu, dx, dw, db):
                                  _dev(dx, torch.float32, "dx"), _dev(dw, torch.float32, "dw"),
                                  _dev(db, torch.float32, "db"), _dev(ws), ws.numel(), _stream()),
            "prl_gn_silu_bwd")
+
+
+# ------------------------------------------------------------------------- optimizer step
+class MinibatchGather:
+    """prl_gather_minibatch bound to fixed source / destination tensors (graph-capturable)."""
+
+    def __init__(self, sources, dests, cursor, mb):
+        if not 1 <= len(sources) <= 6 or len(sources) != len(dests):
+            raise ValueError("1..6 source/destination pairs")
+        for s_, d_ in zip(sources, dests):
+            _dev(s_, torch.float32, "source")
+            _dev(d_, torch.float32, "dest")
+        self._keep = (list(sources), list(dests), cursor)
+        n = len(sources)
+        self.srcs = (ctypes.c_void_p * n)(*[s_.data_ptr() for s_ in sources])
+        self.dsts = (ctypes.c_void_p * n)(*[d_.data_ptr() for d_ in dests])
+        self.widths = (ctypes.c_int32 * n)(*[int(s_[0].numel()) if s_.dim() > 1 else 1
+                                             for s_ in sources])
+        self.n = n
+        self.cursor = cursor
+        self.mb = int(mb)
+        self.nrows = int(sources[0].shape[0])
+
+    def __call__(self):
+        _check(lib().prl_gather_minibatch(self.srcs, self.dsts, self.widths, self.n,
+                                          _dev(self.cursor, torch.int64, "cursor"), self.mb,
+                                          self.nrows, _stream()), "prl_gather_minibatch")
+
+
+def categorical_fwd(probs, actions, logp, entropy=None):
+    n, A = probs.shape
+    _check(lib().prl_categorical_fwd(_dev(probs, torch.float32, "probs"),
+                                     _dev(actions, torch.float32, "actions"), n, A,
+                                     _dev(logp, torch.float32, "logp"),
+                                     _dev(entropy, torch.float32, "entropy"), _stream()),
+           "prl_categorical_fwd")
+
+
+def categorical_bwd(probs, actions, dlogp, dprobs):
+    n, A = probs.shape
+    _check(lib().prl_categorical_bwd(_dev(probs, torch.float32, "probs"),
+                                     _dev(actions, torch.float32, "actions"),
+                                     _dev(dlogp, torch.float32, "dlogp"), n, A,
+                                     _dev(dprobs, torch.float32, "dprobs"), _stream()),
+           "prl_categorical_bwd")

@@ -241,3 +241,33 @@ def test_training_improves_cartpole():
         lens.append(n / 1024)
         ppo.learn()
     assert np.mean(lens[-3:]) > 1.5 * np.mean(lens[:2]), lens
+
+
+@pytest.mark.parametrize("cont", [False, True])
+def test_graphed_update_equals_eager_update(cont):
+    """The HIP-graph optimizer step (replayed per minibatch, device cursor) produces exactly the
+    eager step's updates: same kernels, same order, same minibatches."""
+    from PPO import PPO
+    rng = np.random.default_rng(5)
+    N, D, A = 20_000 + 77, (3 if cont else 4), 1 if cont else 2
+    S = torch.from_numpy((rng.normal(size=(N, D)) * 0.5).astype(np.float32)).cuda()
+    Aa = (torch.from_numpy(np.tanh(rng.normal(size=(N, 1))).astype(np.float32) * 2).cuda() if cont
+          else torch.from_numpy((rng.random(N) < 0.5).astype(np.float32)).cuda())
+    R = torch.from_numpy(rng.normal(1, 0.5, N).astype(np.float32)).cuda()
+    Dn = torch.from_numpy((rng.random(N) < 0.05).astype(np.float32)).cuda()
+    Dn[-1] = 1
+    results = []
+    for graphs in (False, True):
+        torch.manual_seed(0)
+        p = PPO(cont, D, A, action_scaling=2.0 if cont else None, k_epochs=3, batch_size=1024,
+                mini_batch_size=256)
+        p.show_progress = False
+        p.use_graphs = graphs
+        p.memory.push_device(S, Aa, R, Dn)
+        p.learn()
+        results.append({k: v.clone() for k, v in p.policy.state_dict().items()})
+        results.append(p.last_loss.clone())
+    sd_e, loss_e, sd_g, loss_g = results
+    for k in sd_e:
+        torch.testing.assert_close(sd_g[k], sd_e[k], rtol=0, atol=0, msg=k)
+    assert float(loss_g) == float(loss_e)

@@ -1,0 +1,60 @@
+"""PPO.learn() on the survey's fixed C2 learn workload: N = 2^20 synthetic
+CartPole transitions, S ~ 0.05 N(0,1), A ~ Bernoulli(1/2), r = 1, d ~ Bernoulli(0.05) with the
+last d = 1 (numpy default_rng(0)); gamma 0.995, lambda 0.95, k_epochs / mini_batch from flags.
+Prints one JSON line: learn wall-ms for the batch (device-synchronised), optimizer steps, us/step.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "parallel-reinforcement-learning_amd")]
+from PPO import PPO  # noqa: E402
+
+
+def synthetic_batch(N, seed=0, device="cuda"):
+    rng = np.random.default_rng(seed)
+    S = (0.05 * rng.normal(size=(N, 4))).astype(np.float32)
+    A = (rng.random(N) < 0.5).astype(np.float32)
+    R = np.ones(N, np.float32)
+    D = (rng.random(N) < 0.05).astype(np.float32)
+    D[-1] = 1
+    return [torch.from_numpy(x).to(device) for x in (S, A, R, D)]
+
+
+def run(N=1 << 20, mb=512, k=11, graphs=True, reps=1):
+    batch = synthetic_batch(N)
+    torch.manual_seed(0)
+    ppo = PPO(False, 4, 2, lr=1e-3, k_epochs=k, batch_size=1, mini_batch_size=mb)
+    ppo.show_progress = False
+    ppo.use_graphs = graphs
+    times = []
+    for _ in range(reps + 1):          # first call warms up allocator / libraries
+        ppo.memory.push_device(*batch)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ppo.learn()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    steps = k * -(-N // mb)
+    t = min(times[1:])
+    return {"N": N, "mini_batch": mb, "k_epochs": k, "graphs": graphs,
+            "learn_ms": round(t * 1e3, 1), "optimizer_steps": steps,
+            "us_per_step": round(t / steps * 1e6, 1),
+            "learn_ms_per_1M": round(t * 1e3 * (1 << 20) / N, 1)}
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--mb", type=int, default=512)
+    ap.add_argument("--k", type=int, default=11)
+    ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--reps", type=int, default=1)
+    a = ap.parse_args()
+    print(json.dumps(run(a.n, a.mb, a.k, not a.eager, a.reps)), flush=True)
