@@ -80,6 +80,21 @@ def time_kernel(launch, reps=10, cold=True):
     return float(np.median(ms)), float(np.min(ms))
 
 
+def pmc_traffic(n):
+    """HBM bytes per GAE launch from the committed PMC summary (profiles/*gae_pmc.json, written by
+    tools/gpu_benchprof.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the same
+    input, FETCH_SIZE doubled for gfx950).  Scaled per transition when n differs."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*gae_pmc.json")))
+    if not files:
+        return None, None
+    rec = json.load(open(files[-1]))
+    per = (rec["read_bytes_corrected"] + rec["write_bytes"]) / rec["n"]
+    src = os.path.relpath(files[-1], ROOT) + (" (same n)" if rec["n"] == n else
+                                              f" (measured at n={rec['n']}, scaled per transition)")
+    return round(per * n), src
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -91,6 +106,8 @@ def main():
     ap.add_argument("--k-epochs", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-envs", type=int, default=8192)
+    ap.add_argument("--dump-gae", default=None,
+                    help="save the roofline GAE launch's inputs (torch.save) for PMC passes")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,9 +192,15 @@ def main():
         cold_med, cold_min = time_kernel(lambda: prl_native.gae(*a, **k), cold=True)
         warm_med, _ = time_kernel(lambda: prl_native.gae(*a, **k), cold=False)
         achieved = GAE_BYTES_PER_TRANSITION * n_gae / (cold_med * 1e-3) / 1e9
+        if args.dump_gae and rank == 0:
+            torch.save({"r": a[0].cpu(), "d": a[1].cpu(), "V": a[2].cpu(),
+                        "next_value": None if a[3] is None else a[3].cpu(),
+                        "gamma": a[4], "lam": a[5]}, args.dump_gae)
+        traffic, traffic_src = pmc_traffic(n_gae)
         roofline = {"kernel": "prl_gae: gae_kernel<true> (single-pass segmented GAE scan)",
                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_source": traffic_src,
                     "avg_launch_us": round(cold_med * 1e3, 2), "cache": "cold (512 MiB flush)",
                     "warm_launch_us": round(warm_med * 1e3, 2),
                     "warm_achieved": round(GAE_BYTES_PER_TRANSITION * n_gae / (warm_med * 1e-3)

@@ -37,6 +37,20 @@ def gae_case(n, pd=0.05, seg=None, reps=10):
             "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
+def gae_file_case(path, reps=10):
+    x = torch.load(path, weights_only=True)
+    r, d, V = (x[k].cuda() for k in ("r", "d", "V"))
+    nv = x["next_value"].cuda() if x["next_value"] is not None else None
+    n = V.numel()
+    ret, adv = torch.empty_like(V), torch.empty_like(V)
+    sums = torch.zeros(2, dtype=torch.float64, device="cuda")
+    med, mn = time_kernel(lambda: prl_native.gae(r, d, V, nv, x["gamma"], x["lam"], ret, adv, sums),
+                          reps=reps)
+    gbs = GAE_BYTES_PER_TRANSITION * n / (med * 1e-3) / 1e9
+    return {"kernel": "gae", "n": n, "source": path, "us": round(med * 1e3, 2),
+            "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+
 def cartpole_step_case(E, reps=10):
     from AsyncTools.AsyncPPO import DeviceTrajectory, EnvVectorizer
     vec = EnvVectorizer("CartPole-v1", E, seed=0)
@@ -77,7 +91,15 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--gae-n", type=int, default=0, help="only the GAE scan at this size")
+    ap.add_argument("--gae-file", default=None, help="only the GAE scan on bench.py --dump-gae")
     a = ap.parse_args()
+    if a.gae_file:
+        print(json.dumps(gae_file_case(a.gae_file, reps=a.reps)), flush=True)
+        sys.exit(0)
+    if a.gae_n:
+        print(json.dumps(gae_case(a.gae_n, reps=a.reps)), flush=True)
+        sys.exit(0)
     out = []
     sizes = [1 << 20] if a.quick else [1 << 20, 2_300_000, 65536 * 200]
     for n in sizes:
