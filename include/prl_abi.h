@@ -197,6 +197,32 @@ int prl_categorical_fwd(const float* probs, const float* actions, int64_t n, int
 int prl_categorical_bwd(const float* probs, const float* actions, const float* dlogp, int64_t n,
                         int32_t A, float* dprobs, void* stream);
 
+/* ---- fused update engine (PPO/PPO.py:216-255 in ONE persistent launch) --------------------- */
+/* Host call: parameter count, device workspace bytes and grid of the fused engine for the
+ * reference's ActorCritic(is_continuous = !discrete, observ_dim = D, action_dim = A) at
+ * mini_batch.  Returns PRL_ERR_ARG (all outputs 0) for shapes outside the engine (D > 64, A > 8,
+ * LDS > 160 KiB): the caller then runs the per-step path. */
+int prl_ppo_update_info(int32_t D, int32_t A, int32_t discrete, int64_t mini_batch,
+                        int64_t* n_params, int64_t* workspace_bytes, int32_t* grid);
+/* All k_epochs x ceil(N / mini_batch) optimizer steps of PPO.learn (PPO.py:216-255) in order:
+ * per minibatch j (rows [j*mb, min((j+1)*mb, N)) of S/actions/old_logp/adv/ret, unshuffled):
+ * ActorCritic.get_evaluate (ActorCritic.py:118-146), loss = mean(-min(surr1, surr2)) +
+ * vf_coef * SmoothL1(V, ret) - ent_coef * H (PPO.py:225-245), its gradient,
+ * clip_grad_norm_(max_norm) and AdamW(lr, (beta1, beta2), eps, weight_decay).  params /
+ * exp_avg / exp_avg_sq: the flat parameter vector and moments in torch parameters() order
+ * (updated in place); adam_step: device f32 step count (read, then advanced by the step count);
+ * loss_out: device f32, the last step's loss.  Workspace: prl_ppo_update_info's size (its status
+ * word, see prl_ppo_update_status_ptr, is 0 after a good launch).  Cooperative launch. */
+int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, int32_t D,
+                   int32_t A, int32_t discrete, const float* S, const float* actions,
+                   const float* old_logp, const float* adv, const float* ret, int64_t N,
+                   int32_t mini_batch, int32_t k_epochs, float clip, float vf_coef,
+                   float ent_coef, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, float max_norm, float* loss_out, void* workspace,
+                   int64_t workspace_bytes, void* stream);
+/* Host call: device address of the u32 status word inside an engine workspace. */
+int prl_ppo_update_status_ptr(void* workspace, uint32_t** status);
+
 #ifdef __cplusplus
 }
 #endif

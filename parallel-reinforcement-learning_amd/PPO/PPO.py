@@ -108,7 +108,8 @@ class PPO:
         self.show_progress = True
         self.last_loss = None
         self._ops = prl_native              # HIP entry points (tests may substitute a fake)
-        self.use_graphs = True              # replay one captured optimizer step per minibatch
+        self.use_fused = True               # whole update loop in one persistent HIP kernel
+        self.use_graphs = True              # else: replay one captured optimizer step per minibatch
         self.graph_min_steps = 16           # below this many graphable steps, stay eager
         self._flat_grad = None
         self._sync_initial_weights()
@@ -261,11 +262,33 @@ class PPO:
         self._update(S, A, old_logp, adv, returns, n_ranks)
         self.policy_old.load_state_dict(self.policy.state_dict())
 
+    def _fused_engine(self):
+        """The fused update engine for this policy / mini_batch (None: shape outside it)."""
+        eng = getattr(self, "_engine", None)
+        if eng is not None and eng.mini_batch == self.mini_batch_size:
+            return eng
+        from .engine import FusedUpdate
+        try:
+            self._engine = FusedUpdate(self, self.mini_batch_size)
+        except ValueError:
+            self._engine = None
+        return self._engine
+
     def _update(self, S, A, old_logp, adv, returns, n_ranks):
-        """k_epochs x sequential minibatches (PPO.py:219-255).  Full minibatches that every rank
-        has replay one captured HIP graph (update.py); the rest run eagerly, in order."""
+        """k_epochs x sequential minibatches (PPO.py:219-255).  One GPU: the whole loop is one
+        persistent HIP kernel (engine.py).  Otherwise full minibatches that every rank has replay
+        one captured HIP graph (update.py); the rest run eagerly, in order."""
         mb = self.mini_batch_size
         world = len(n_ranks)
+        self._last_update_inputs = (S, A, old_logp, adv, returns)   # references (tests, debugging)
+        if world == 1 and self.use_fused and S.is_cuda:
+            eng = self._fused_engine()
+            if eng is not None:
+                self.last_loss = eng.run(S, A, old_logp, adv, returns, self.k_epochs).clone()
+                self.last_graph_replays = 0
+                self.last_update_path = "fused"
+                return
+        self.last_update_path = "graph" if self.use_graphs else "eager"
         nb = max(-(-n // mb) for n in n_ranks)
         counts = [sum(min(mb, max(0, n - j * mb)) for n in n_ranks) for j in range(nb)]
         n_graph = min(n // mb for n in n_ranks)

@@ -1,0 +1,101 @@
+"""Fused update engine: PPO.learn's whole update loop (PPO/PPO.py:216-255) as ONE persistent HIP
+kernel (csrc/prl_ppo_update.hip, C-ABI prl_ppo_update).
+
+The kernel needs the policy's parameters and AdamW moments as flat vectors in torch
+parameters() order.  FusedUpdate re-points every policy Parameter's .data at a view of one flat
+buffer (Parameter objects, state_dict keys and the optimizer's param list are unchanged) and
+makes the optimizer's `exp_avg` / `exp_avg_sq` state tensors views of two flat buffers, so the
+engine and torch's AdamW share one copy of the state: an eager step taken afterwards (world > 1,
+shapes outside the engine) continues exactly where the engine stopped.
+"""
+from __future__ import annotations
+
+import torch
+
+import prl_native
+
+
+class FusedUpdate:
+    def __init__(self, ppo, mini_batch: int):
+        pol = ppo.policy
+        self.ppo = ppo
+        self.discrete = not ppo.is_continuous
+        self.D, self.A = int(ppo.observ_dim), int(ppo.action_dim)
+        info = prl_native.ppo_update_info(self.D, self.A, self.discrete, mini_batch)
+        if info is None:
+            raise ValueError("shape outside the fused engine")
+        n_params, ws_bytes, self.grid = info
+        self.params = [p for p in pol.parameters()]
+        if sum(p.numel() for p in self.params) != n_params:
+            raise ValueError("policy parameter count does not match the engine's layout")
+        dev = self.params[0].device
+        self.flat = torch.empty(n_params, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(n_params, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(n_params, dtype=torch.float32, device=dev)
+        self.step = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
+        self.mini_batch = int(mini_batch)
+        self._bind()
+
+    def _views(self, buf):
+        out, off = [], 0
+        for p in self.params:
+            out.append(buf[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        return out
+
+    def _bind(self):
+        """Alias parameters and optimizer state onto the flat buffers (copies current values)."""
+        opt = self.ppo.optimizer
+        with torch.no_grad():
+            for p, fv, mv, vv in zip(self.params, self._views(self.flat), self._views(self.m),
+                                     self._views(self.v)):
+                fv.copy_(p.data)
+                p.data = fv
+                st = opt.state.get(p)
+                if st and "exp_avg" in st:
+                    mv.copy_(st["exp_avg"])
+                    vv.copy_(st["exp_avg_sq"])
+                    self.step.copy_(torch.as_tensor(st["step"], dtype=torch.float32).reshape(1))
+                    st["exp_avg"], st["exp_avg_sq"] = mv, vv
+        self._opt_views = (self._views(self.m), self._views(self.v))
+
+    def bound(self) -> bool:
+        """True while the policy parameters still live in the flat buffer."""
+        return all(p.data.data_ptr() == fv.data_ptr()
+                   for p, fv in zip(self.params, self._views(self.flat)))
+
+    def _sync_optimizer_state(self):
+        """Make the optimizer's state the engine's: moments as views, step counts = engine's."""
+        opt = self.ppo.optimizer
+        group = opt.param_groups[0]
+        on_device = bool(group.get("capturable") or group.get("fused"))
+        for p, mv, vv in zip(self.params, *self._opt_views):
+            st = opt.state[p]
+            st["exp_avg"], st["exp_avg_sq"] = mv, vv
+            if "step" in st and torch.is_tensor(st["step"]):
+                st["step"].copy_(self.step.reshape(st["step"].shape))
+            else:
+                st["step"] = (self.step.reshape(()).clone() if on_device
+                              else torch.tensor(float(self.step.item())))
+
+    def run(self, S, A, old_logp, adv, ret, k_epochs: int):
+        """k_epochs x ceil(N / mini_batch) optimizer steps; returns the last step's loss (device)."""
+        if not self.bound():
+            self._bind()
+        group = self.ppo.optimizer.param_groups[0]
+        beta1, beta2 = group["betas"]
+        A2 = A if A.dim() == 2 else A.reshape(-1, 1)
+        prl_native.ppo_update(
+            self.flat, self.m, self.v, self.step, self.D, self.A, self.discrete,
+            S.contiguous(), A2.contiguous(), old_logp.contiguous(), adv.contiguous(),
+            ret.contiguous(), self.mini_batch, k_epochs, self.ppo.policy_clip,
+            self.ppo.value_coef, self.ppo.entropy_coef, group["lr"], beta1, beta2, group["eps"],
+            group["weight_decay"], 2.0, self.loss, self.ws)
+        self._sync_optimizer_state()
+        status = int(prl_native.ppo_update_status(self.ws).item())
+        if status != 0:
+            raise RuntimeError(f"prl_ppo_update: in-kernel timeout (status {status}); the policy "
+                               "parameters are undefined")
+        return self.loss.reshape(())

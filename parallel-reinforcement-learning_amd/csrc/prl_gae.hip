@@ -69,10 +69,14 @@ inline int64_t gae_ws_bytes_tiles(int64_t nt) {
 inline int64_t gae_ws_bytes(int64_t n) { return gae_ws_bytes_tiles(gae_ntiles(n)); }
 // The layout is carved for the largest tile count the BUFFER can hold, never for the current n:
 // one buffer serves calls of every size, and the counters it keeps armed between launches must
-// sit at the same offsets in all of them (bytes(nt) <= 216 + 25.25 * nt).
+// sit at the same offsets in all of them.  Exact: the largest nt with bytes(nt) <= bytes (the
+// estimate from bytes(nt) <= 216 + 25.25 * nt is only a starting point; rounding down from it
+// once under-sized the carve by a tile, so the last tile's carry granule overwrote tile 0's
+// statistics).
 inline int64_t gae_capacity_tiles(int64_t bytes) {
   int64_t nt = std::max<int64_t>(1, (int64_t)((double)(bytes - 216) / 25.25));
   while (nt > 1 && gae_ws_bytes_tiles(nt) > bytes) --nt;
+  while (gae_ws_bytes_tiles(nt + 1) <= bytes) ++nt;
   return nt;
 }
 inline GaeWs gae_ws_carve(void* ws, int64_t nt) {
@@ -481,6 +485,7 @@ extern "C" int prl_gae(const float* r, const float* d, const float* V, const flo
   PRL_REQUIRE(workspace && workspace_bytes >= gae_ws_bytes(n),
               "prl_gae: workspace too small (%lld < %lld)", (long long)workspace_bytes,
               (long long)gae_ws_bytes(n));
+  PRL_REQUIRE(gae_capacity_tiles(workspace_bytes) >= nt, "prl_gae: workspace layout too small");
   hipStream_t s = as_stream(stream);
   GaeWs ws = gae_ws_carve(workspace, gae_capacity_tiles(workspace_bytes));
   // gamma * nv * (1 - d): gamma is a weak Python float -> float32; gamma * lambda is a Python
@@ -511,6 +516,7 @@ extern "C" int prl_adv_stats(const float* x, int64_t n, double* sums_out, void* 
   PRL_REQUIRE(x, "prl_adv_stats: null x");
   const int64_t nt = gae_ntiles(n);
   PRL_REQUIRE(workspace && workspace_bytes >= gae_ws_bytes(n), "prl_adv_stats: workspace too small");
+  PRL_REQUIRE(gae_capacity_tiles(workspace_bytes) >= nt, "prl_adv_stats: workspace layout too small");
   GaeWs ws = gae_ws_carve(workspace, gae_capacity_tiles(workspace_bytes));
   hipLaunchKernelGGL(stats_kernel, dim3((unsigned)nt), dim3(GAE_THREADS), 0, s, x, n, ws, nt, sums_out);
   PRL_LAUNCH_CHECK("adv_stats");

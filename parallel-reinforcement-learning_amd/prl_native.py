@@ -50,6 +50,10 @@ SIGNATURES = {
     "prl_gather_minibatch": [_P, _P, _P, _I32, _P, _I64, _I64, _P],
     "prl_categorical_fwd": [_P, _P, _I64, _I32, _P, _P, _P],
     "prl_categorical_bwd": [_P, _P, _P, _I64, _I32, _P, _P],
+    "prl_ppo_update_info": [_I32, _I32, _I32, _I64, _P, _P, _P],
+    "prl_ppo_update": [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I32]
+                      + [_F32] * 9 + [_P, _P, _I64, _P],
+    "prl_ppo_update_status_ptr": [_P, _P],
 }
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64}
 
@@ -364,3 +368,38 @@ def categorical_bwd(probs, actions, dlogp, dprobs):
                                      _dev(dlogp, torch.float32, "dlogp"), n, A,
                                      _dev(dprobs, torch.float32, "dprobs"), _stream()),
            "prl_categorical_bwd")
+
+
+def ppo_update_info(D: int, A: int, discrete: bool, mini_batch: int):
+    """(n_params, workspace_bytes, grid) of the fused update engine, or None when the shape is
+    outside it (the caller then uses the graph-replayed PyTorch step)."""
+    n_params, ws, grid = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(0)
+    rc = lib().prl_ppo_update_info(int(D), int(A), int(bool(discrete)), int(mini_batch),
+                                   ctypes.byref(n_params), ctypes.byref(ws), ctypes.byref(grid))
+    if rc != 0:
+        return None
+    return n_params.value, ws.value, grid.value
+
+
+def ppo_update(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp, adv,
+               ret, mini_batch, k_epochs, clip, vf_coef, ent_coef, lr, beta1, beta2, eps,
+               weight_decay, max_norm, loss_out, workspace):
+    N = int(S.shape[0])
+    _check(lib().prl_ppo_update(
+        _dev(params, torch.float32, "params"), _dev(exp_avg, torch.float32, "exp_avg"),
+        _dev(exp_avg_sq, torch.float32, "exp_avg_sq"), _dev(adam_step, torch.float32, "adam_step"),
+        int(D), int(A), int(bool(discrete)), _dev(S, torch.float32, "S"),
+        _dev(actions, torch.float32, "actions"), _dev(old_logp, torch.float32, "old_logp"),
+        _dev(adv, torch.float32, "adv"), _dev(ret, torch.float32, "ret"), N, int(mini_batch),
+        int(k_epochs), float(clip), float(vf_coef), float(ent_coef), float(lr), float(beta1),
+        float(beta2), float(eps), float(weight_decay), float(max_norm),
+        _dev(loss_out, torch.float32, "loss_out"), _dev(workspace, torch.uint8, "workspace"),
+        workspace.numel(), _stream()), "prl_ppo_update")
+
+
+def ppo_update_status(workspace) -> torch.Tensor:
+    """Device u32 view of the engine's status word (0 ok, 1 in-kernel timeout)."""
+    ptr = ctypes.c_void_p()
+    _check(lib().prl_ppo_update_status_ptr(_dev(workspace, torch.uint8, "workspace"),
+                                           ctypes.byref(ptr)), "prl_ppo_update_status_ptr")
+    return workspace[12:16].view(torch.int32)

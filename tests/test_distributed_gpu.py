@@ -57,6 +57,7 @@ def test_two_ranks_graphed_equal_one_process_on_the_union(tmp_path):
             for c in range(4)]
     torch.manual_seed(1234)
     p = _make_ppo(2 * mb, k)
+    p.use_fused = False        # world 1 would take the fused engine; compare graph with graph
     p.memory.push_device(*(torch.from_numpy(x).cuda() for x in cols))
     p.learn()
     assert p.last_graph_replays == k * nb - 2

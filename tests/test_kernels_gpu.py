@@ -570,3 +570,40 @@ def test_gn_silu_module_grads_match_cpu_reference():
     (m_gpu(x.cuda()) ** 2).sum().backward()
     for (n, a), (_, g) in zip(m_cpu.named_parameters(), m_gpu.named_parameters()):
         torch.testing.assert_close(g.grad.cpu(), a.grad, rtol=2e-5, atol=2e-5, msg=n)
+
+
+def test_gae_statistics_exact_size_workspace_every_tile_count():
+    """Regression: the workspace layout is carved from the buffer's size; an exact-size buffer
+    (prl_workspace_bytes(n), fresh) must hold every tile's carry granule AND statistics record.
+    A rounding error once carved one tile too few, so the last tile's granule overwrote tile 0's
+    sum of advantages — only when that block happened to finish late, so the check runs under a
+    concurrent load on another stream and repeats each size."""
+    import ctypes
+    import prl_native as P
+    side = torch.cuda.Stream()
+    big = torch.empty(32 << 20, device="cuda")
+    for nt in list(range(1, 70)) + [127, 128, 129, 700]:
+        n = nt * 2048 - 5
+        g = torch.Generator(device="cuda").manual_seed(nt)
+        r = torch.randn(n, device="cuda", generator=g)
+        V = torch.randn(n, device="cuda", generator=g)
+        d = (torch.rand(n, device="cuda", generator=g) < 0.05).float()
+        d[-1] = 1
+        nbytes = P.workspace_bytes(P.OP_GAE, n)
+        ws = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+        for rep in range(3):
+            with torch.cuda.stream(side):
+                big.mul_(1.0001)
+            ret, adv = torch.empty_like(V), torch.empty_like(V)
+            sums = torch.zeros(2, dtype=torch.float64, device="cuda")
+            rc = P.lib().prl_gae(ctypes.c_void_p(r.data_ptr()), ctypes.c_void_p(d.data_ptr()),
+                                 ctypes.c_void_p(V.data_ptr()), None, n, 0.995, 0.95,
+                                 ctypes.c_void_p(ret.data_ptr()), ctypes.c_void_p(adv.data_ptr()),
+                                 ctypes.c_void_p(sums.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                 nbytes, P._stream())
+            assert rc == 0, P.lib().prl_last_error()
+            a = adv.double()
+            host = torch.stack([a.sum(), (a * a).sum()])
+            torch.testing.assert_close(sums, host, rtol=1e-12, atol=1e-9,
+                                       msg=f"nt={nt} rep={rep}")
+    torch.cuda.synchronize()

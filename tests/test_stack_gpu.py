@@ -151,9 +151,11 @@ def test_device_worker_pendulum_shapes_and_truncation():
     assert a.last_vector_steps <= 200 + a.poll_lag + 1
 
 
-def test_learn_on_gpu_matches_reference_learn(golden):
+@pytest.mark.parametrize("path", ["fused", "graph"])
+def test_learn_on_gpu_matches_reference_learn(golden, path):
     """PPO.learn() through libprl_hip.so vs the reference's learn(): same seeded policy, same
-    memory -> same updated weights (GPU float32 GEMMs differ from CPU ones in rounding)."""
+    memory -> same updated weights (GPU float32 GEMMs differ from CPU ones in rounding).
+    path "fused": the whole update loop in the persistent engine; "graph": per-step graphs."""
     from PPO import PPO
     for tag, cont in (("learn", False), ("learn_cont", True)):
         g = golden(tag)
@@ -164,10 +166,12 @@ def test_learn_on_gpu_matches_reference_learn(golden):
                 policy_clip=0.2, GAE_lambda=0.95, gamma=0.995, batch_size=1024,
                 mini_batch_size=int(g["mb"]))
         p.show_progress = False
+        p.use_fused = path == "fused"
         for i in range(int(g["N"])):
             p.memory.push(g["S"][i], g["A"][i] if cont else np.asarray(g["A"][i]), g["R"][i],
                           g["Dn"][i])
         p.learn()
+        assert p.last_update_path == path
         sd = p.policy.state_dict()
         for k in sd:
             np.testing.assert_allclose(sd[k].cpu().numpy(), g["final/" + k], rtol=0, atol=2e-6,
@@ -262,6 +266,7 @@ def test_graphed_update_equals_eager_update(cont):
         p = PPO(cont, D, A, action_scaling=2.0 if cont else None, k_epochs=3, batch_size=1024,
                 mini_batch_size=256)
         p.show_progress = False
+        p.use_fused = False            # this test is about the per-step graph path
         p.use_graphs = graphs
         p.memory.push_device(S, Aa, R, Dn)
         p.learn()

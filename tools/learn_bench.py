@@ -27,12 +27,13 @@ def synthetic_batch(N, seed=0, device="cuda"):
     return [torch.from_numpy(x).to(device) for x in (S, A, R, D)]
 
 
-def run(N=1 << 20, mb=512, k=11, graphs=True, reps=1):
+def run(N=1 << 20, mb=512, k=11, graphs=True, reps=1, fused=True):
     batch = synthetic_batch(N)
     torch.manual_seed(0)
     ppo = PPO(False, 4, 2, lr=1e-3, k_epochs=k, batch_size=1, mini_batch_size=mb)
     ppo.show_progress = False
     ppo.use_graphs = graphs
+    ppo.use_fused = fused
     times = []
     for _ in range(reps + 1):          # first call warms up allocator / libraries
         ppo.memory.push_device(*batch)
@@ -43,7 +44,7 @@ def run(N=1 << 20, mb=512, k=11, graphs=True, reps=1):
         times.append(time.perf_counter() - t0)
     steps = k * -(-N // mb)
     t = min(times[1:])
-    return {"N": N, "mini_batch": mb, "k_epochs": k, "graphs": graphs,
+    return {"N": N, "mini_batch": mb, "k_epochs": k, "path": ppo.last_update_path,
             "learn_ms": round(t * 1e3, 1), "optimizer_steps": steps,
             "us_per_step": round(t / steps * 1e6, 1),
             "learn_ms_per_1M": round(t * 1e3 * (1 << 20) / N, 1)}
@@ -55,6 +56,7 @@ if __name__ == "__main__":
     ap.add_argument("--mb", type=int, default=512)
     ap.add_argument("--k", type=int, default=11)
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--no-fused", action="store_true")
     ap.add_argument("--reps", type=int, default=1)
     a = ap.parse_args()
-    print(json.dumps(run(a.n, a.mb, a.k, not a.eager, a.reps)), flush=True)
+    print(json.dumps(run(a.n, a.mb, a.k, not a.eager, a.reps, not a.no_fused)), flush=True)
