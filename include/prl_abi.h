@@ -220,6 +220,13 @@ int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, float* adam
                    float ent_coef, float lr, float beta1, float beta2, float eps,
                    float weight_decay, float max_norm, float* loss_out, void* workspace,
                    int64_t workspace_bytes, void* stream);
+/* ActorCritic.get_evaluate (ActorCritic.py:118-146) over N rows, as PPO.learn evaluates
+ * policy_old (PPO.py:127-154): logp[N], V[N] and optionally entropy[N] (NULL = skip), with the
+ * fused update's forward arithmetic (so learn()'s first minibatch has ratio == 1 exactly).
+ * params: flat, torch parameters() order.  No workspace, no inter-workgroup communication. */
+int prl_ppo_evaluate(const float* params, int32_t D, int32_t A, int32_t discrete, const float* S,
+                     const float* actions, int64_t N, float* logp, float* V, float* entropy,
+                     void* stream);
 /* Host call: device address of the u32 status word inside an engine workspace. */
 int prl_ppo_update_status_ptr(void* workspace, uint32_t** status);
 

@@ -216,8 +216,18 @@ class PPO:
             return list(ret.cpu().numpy())
         return ret
 
+    def _fused_path(self, world):
+        return world == 1 and self.use_fused and self.device.type == "cuda"
+
     @torch.no_grad()
-    def _evaluate_old(self, S, A):
+    def _evaluate_old(self, S, A, world=1):
+        """policy_old.get_evaluate over the batch (PPO.py:127-154).  When the fused engine runs
+        the update, it also evaluates here, so both log-probs come from the same arithmetic and
+        the first minibatch sees ratio == 1 exactly, as in the reference."""
+        if self._fused_path(world) and S.is_cuda:
+            eng = self._fused_engine()
+            if eng is not None:
+                return eng.evaluate(self.policy_old, S, A)
         lps, vs = [], []
         for lo in range(0, S.shape[0], self.eval_chunk):
             lp, v, _ = self.policy_old.get_evaluate(S[lo:lo + self.eval_chunk],
@@ -243,7 +253,7 @@ class PPO:
         _require_gpu("PPO.learn") if self._ops is prl_native else None
         S, A, R, Dn = self.memory.device_tensors(self.device)
         N = S.shape[0]
-        old_logp, old_V = self._evaluate_old(S, A)
+        old_logp, old_V = self._evaluate_old(S, A, world)
 
         if self.use_RND:
             r_int = self.rnd.compute_intrinsic_reward(S)
@@ -281,7 +291,7 @@ class PPO:
         mb = self.mini_batch_size
         world = len(n_ranks)
         self._last_update_inputs = (S, A, old_logp, adv, returns)   # references (tests, debugging)
-        if world == 1 and self.use_fused and S.is_cuda:
+        if self._fused_path(world) and S.is_cuda:
             eng = self._fused_engine()
             if eng is not None:
                 self.last_loss = eng.run(S, A, old_logp, adv, returns, self.k_epochs).clone()

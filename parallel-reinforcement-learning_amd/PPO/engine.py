@@ -80,6 +80,37 @@ class FusedUpdate:
                 st["step"] = (self.step.reshape(()).clone() if on_device
                               else torch.tensor(float(self.step.item())))
 
+    def evaluate(self, module, S, A):
+        """module.get_evaluate(S, A)'s log_prob and value for all rows (module: policy_old, same
+        architecture) with the engine's forward arithmetic."""
+        with torch.no_grad():
+            flat = torch.cat([p.detach().reshape(-1) for p in module.parameters()])
+        A2 = A if A.dim() == 2 else A.reshape(-1, 1)
+        n = S.shape[0]
+        logp = torch.empty(n, dtype=torch.float32, device=S.device)
+        V = torch.empty(n, dtype=torch.float32, device=S.device)
+        prl_native.ppo_evaluate(flat, self.D, self.A, self.discrete, S.contiguous(),
+                                A2.contiguous(), logp, V)
+        return logp, V
+
+    PHASES = ("forward+backward", "publish", "wait A", "slice reduce", "wait B", "norm",
+              "AdamW")
+
+    CHUNK_STAGES = ("inputs", "trunk fwd", "heads fwd", "outputs+loss", "heads bwd",
+                    "weight grads+dF", "trunk bwd", "dW0")
+
+    def profile(self):
+        """Workgroup 0's time per phase of the last launch, us per step (s_memrealtime, 100 MHz);
+        'chunk' splits forward+backward by stage (summed over the step's row chunks)."""
+        p = self.ws[256:512].view(torch.int64).tolist()
+        steps = max(p[7], 1)
+        out = {name: round(p[i] * 0.01 / steps, 2) for i, name in enumerate(self.PHASES)}
+        out["chunk"] = {name: round(p[8 + i] * 0.01 / steps, 2)
+                        for i, name in enumerate(self.CHUNK_STAGES)}
+        if p[30] > 0:
+            out["shader_clock_GHz"] = round(p[31] / (p[30] * 10.0), 3)
+        return out
+
     def run(self, S, A, old_logp, adv, ret, k_epochs: int):
         """k_epochs x ceil(N / mini_batch) optimizer steps; returns the last step's loss (device)."""
         if not self.bound():

@@ -83,28 +83,30 @@ struct UpdArgs {
   float* part;      // [G][Qtot * 4]
   float* red;       // [Qtot * 4]
   float* sq;        // [G]
-  float* priv;      // [G][2][Lp]
   unsigned* ctr;    // [0] arrivals A, [1] arrivals B, [2] abort, [3] status
+  unsigned long long* prof;  // [8] workgroup 0's time per phase (100 MHz ticks, summed over steps)
 };
 
 // ---- sc1 (write-through / L1-bypassing) accessors -------------------------------------------
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
-__device__ inline __amdgpu_buffer_rsrc_t upd_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+// The resource is built from a WAVE-UNIFORM base (a kernel argument); the per-lane part of the
+// address goes in the byte offset.  (A per-lane base forces a 64-iteration waterfall loop.)
+__device__ inline __amdgpu_buffer_rsrc_t upd_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
-__device__ inline float4 ld4_sc1(const float* p) {
-  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(upd_rsrc(p), 0, 0, 16);
+__device__ inline float4 ld4_sc1(__amdgpu_buffer_rsrc_t rs, size_t float_off) {
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(float_off * 4), 0, 16);
   return float4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
                 __uint_as_float(v.w)};
 }
-__device__ inline void st4_sc1(float* p, float4 x) {
+__device__ inline void st4_sc1(__amdgpu_buffer_rsrc_t rs, size_t float_off, float4 x) {
   v4u v;
   v.x = __float_as_uint(x.x);
   v.y = __float_as_uint(x.y);
   v.z = __float_as_uint(x.z);
   v.w = __float_as_uint(x.w);
-  __builtin_amdgcn_raw_buffer_store_b128(v, upd_rsrc(p), 0, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (unsigned)(float_off * 4), 0, 16);
 }
 __device__ inline float ld_sc1f(const float* p) {
   return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
@@ -160,18 +162,20 @@ struct UpdAct {
   float* adv;     // [RC]
   float* ret;     // [RC]
   float* lossp;   // [RC][4]
-  float* T0;      // [RC][HS]  H0 raw -> dF -> dH0
+  float* T0;      // [RC][HS]  dH0
   float* XH0;     // [RC][HS]
   float* F;       // [RC][HS]
   float* DU0;     // [RC][HS]
   float* rstd0;   // [RC][8]
   float* heads;   // per head h at heads + h * UPD_HEAD_FLOATS:
-                  //   ZB [RC][HS] (Z raw -> dG -> dZ), XH, Gh, DU [RC][HS], rstd [RC][8]
+                  //   ZB [RC][HS] (dZ), XH, Gh, DU [RC][HS], rstd [RC][8]
   __device__ float* ZB(int h) const { return heads + h * UPD_HEAD_FLOATS; }
   __device__ float* XH(int h) const { return heads + h * UPD_HEAD_FLOATS + UPD_RC * UPD_HS; }
   __device__ float* Gh(int h) const { return heads + h * UPD_HEAD_FLOATS + 2 * UPD_RC * UPD_HS; }
   __device__ float* DU(int h) const { return heads + h * UPD_HEAD_FLOATS + 3 * UPD_RC * UPD_HS; }
   __device__ float* rstd(int h) const { return heads + h * UPD_HEAD_FLOATS + 4 * UPD_RC * UPD_HS; }
+  float* dFh;     // [MAXH][RC][HS] per-head parts of dF
+  __device__ float* dF(int h) const { return dFh + h * UPD_RC * UPD_HS; }
   float* O;       // [RC][OX]
   float* dO;      // [RC][OX]
   int DX, AX, OX;
@@ -181,7 +185,7 @@ __host__ __device__ inline int upd_act_floats(int D, int A, int nout, int& DX, i
   DX = (D + 3) & ~3;
   AX = (A + 3) & ~3;
   OX = (nout + 3) & ~3;
-  return UPD_RC * (DX + AX + 4 + 4 + 4 * UPD_HS + 8 + UPD_MAXH * (4 * UPD_HS + 8) + 2 * OX) + 16;
+  return UPD_RC * (DX + AX + 4 + 4 + 4 * UPD_HS + 8 + UPD_MAXH * (5 * UPD_HS + 8) + 2 * OX) + 16;
 }
 
 __device__ inline UpdAct upd_carve(float* base, const UpdNet& n) {
@@ -201,18 +205,16 @@ __device__ inline UpdAct upd_carve(float* base, const UpdNet& n) {
   a.DU0 = take(UPD_RC * UPD_HS);
   a.rstd0 = take(UPD_RC * 8);
   a.heads = take(UPD_MAXH * UPD_HEAD_FLOATS);
+  a.dFh = take(UPD_MAXH * UPD_RC * UPD_HS);
   a.O = take(UPD_RC * a.OX);
   a.dO = take(UPD_RC * a.OX);
   return a;
 }
 
-// GroupNorm(8 groups of 8) + SiLU forward of one (row, group): same arithmetic as gn_silu_fwd.
-__device__ inline void upd_gn_fwd(const float* raw, const float* gw, const float* gb, float* xh_out,
-                                  float* y_out, float* rstd_out) {
-  float v[8];
-  const float4 a = *reinterpret_cast<const float4*>(raw);
-  const float4 b = *reinterpret_cast<const float4*>(raw + 4);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+// GroupNorm(8 groups of 8) + SiLU forward of one (row, group) held in registers: same
+// arithmetic as gn_silu_fwd.  Writes xhat and the block output (16-B aligned LDS rows).
+__device__ inline void upd_gn_fwd(const float (&v)[8], const float* gw, const float* gb,
+                                  float* xh_out, float* y_out, float* rstd_out) {
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < 8; ++k) s += v[k];
@@ -235,14 +237,11 @@ __device__ inline void upd_gn_fwd(const float* raw, const float* gw, const float
   *rstd_out = rstd;
 }
 
-// backward of the above for one (row, group): dio holds dOut on entry, dX on exit; du_out = dy
-__device__ inline void upd_gn_bwd(float* dio, const float* xh_in, const float* gw, const float* gb,
-                                  float rstd, float* du_out) {
-  float go[8], xh[8];
+// backward of the above: go = d(block output) in registers; writes dX and du = d(pre-SiLU)
+__device__ inline void upd_gn_bwd(const float (&go)[8], const float* xh_in, const float* gw,
+                                  const float* gb, float rstd, float* dx_out, float* du_out) {
+  float xh[8];
   {
-    const float4 a = *reinterpret_cast<const float4*>(dio);
-    const float4 b = *reinterpret_cast<const float4*>(dio + 4);
-    go[0] = a.x; go[1] = a.y; go[2] = a.z; go[3] = a.w; go[4] = b.x; go[5] = b.y; go[6] = b.z; go[7] = b.w;
     const float4 c = *reinterpret_cast<const float4*>(xh_in);
     const float4 d = *reinterpret_cast<const float4*>(xh_in + 4);
     xh[0] = c.x; xh[1] = c.y; xh[2] = c.z; xh[3] = c.w; xh[4] = d.x; xh[5] = d.y; xh[6] = d.z; xh[7] = d.w;
@@ -263,24 +262,33 @@ __device__ inline void upd_gn_bwd(float* dio, const float* xh_in, const float* g
   float dx[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) dx[k] = rstd * (dxh[k] - m1 - xh[k] * m2);
-  *reinterpret_cast<float4*>(dio) = float4{dx[0], dx[1], dx[2], dx[3]};
-  *reinterpret_cast<float4*>(dio + 4) = float4{dx[4], dx[5], dx[6], dx[7]};
+  *reinterpret_cast<float4*>(dx_out) = float4{dx[0], dx[1], dx[2], dx[3]};
+  *reinterpret_cast<float4*>(dx_out + 4) = float4{dx[4], dx[5], dx[6], dx[7]};
   *reinterpret_cast<float4*>(du_out) = float4{dy[0], dy[1], dy[2], dy[3]};
   *reinterpret_cast<float4*>(du_out + 4) = float4{dy[4], dy[5], dy[6], dy[7]};
 }
 
-// Per-row loss (surrogate, prl_loss.hip semantics) and the gradient w.r.t. the head outputs.
-// Loops run to the compile-time UPD_MAXA with `k < A` guards so everything stays in registers.
-__device__ inline void upd_row_loss(const UpdNet& n, const UpdAct& a, int r, float invB, float clip,
-                                    float vf_coef) {
-  const float* O = a.O + r * a.OX;
-  float* dO = a.dO + r * a.OX;
-  const int A = n.A;
-  float logp = 0.f, H = 0.f;
+// log_prob and entropy of one row's action under the head outputs O (ActorCritic.get_evaluate,
+// ActorCritic.py:118-146): discrete softmax -> Categorical(probs) (torch's normalise + clamped
+// log); continuous diagonal Gaussian with std = softplus(clamp(log_std, -2, 2)).  Shared by the
+// update and the evaluation kernel so old and new log-probs come from identical arithmetic.
+struct UpdDist {
   float p[UPD_MAXA], q[UPD_MAXA];
-  float S2 = 0.f, qa = 1.f;
-  int ai = 0;
-  if (n.discrete) {
+  float S2, qa, logp, H;
+  int ai;
+};
+// KD: 1 discrete / 0 continuous / -1 runtime;  KA: action dim (0 = runtime).  Specialised
+// kernels keep the per-row code (executed by 8 lanes, but fetched every step) small.
+template <int KD, int KA>
+__device__ inline void upd_row_dist(const UpdNet& n, const float* O, const float* act, UpdDist& d) {
+  const int A = KA > 0 ? KA : n.A;
+  const bool discrete = KD >= 0 ? (KD != 0) : (n.discrete != 0);
+  d.logp = 0.f;
+  d.H = 0.f;
+  d.S2 = 0.f;
+  d.qa = 1.f;
+  d.ai = 0;
+  if (discrete) {
     float mx = O[0];
 #pragma unroll
     for (int k = 1; k < UPD_MAXA; ++k)
@@ -288,29 +296,30 @@ __device__ inline void upd_row_loss(const UpdNet& n, const UpdAct& a, int r, flo
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < UPD_MAXA; ++k) {
-      p[k] = k < A ? expf(O[k] - mx) : 0.f;
-      s += p[k];
+      d.p[k] = k < A ? expf(O[k] - mx) : 0.f;
+      s += d.p[k];
     }
 #pragma unroll
     for (int k = 0; k < UPD_MAXA; ++k) {
-      p[k] = k < A ? p[k] / s : 0.f;
-      S2 += p[k];
+      d.p[k] = k < A ? d.p[k] / s : 0.f;
+      d.S2 += d.p[k];
     }
-    ai = (int)a.Ar[r * a.AX];
-    const bool bad = ai < 0 || ai >= A;   // torch's gather would raise: poison the step instead
+    d.ai = (int)act[0];
+    const bool bad = d.ai < 0 || d.ai >= A;   // torch's gather would raise: poison instead
     float la = 0.f;
 #pragma unroll
     for (int k = 0; k < UPD_MAXA; ++k) {
-      q[k] = p[k] / S2;
+      d.q[k] = d.p[k] / d.S2;
       if (k < A) {
-        const float c = q[k] < FLT_EPSILON ? FLT_EPSILON : (q[k] > 1.0f - FLT_EPSILON ? 1.0f - FLT_EPSILON : q[k]);
+        const float c = d.q[k] < FLT_EPSILON ? FLT_EPSILON
+                                             : (d.q[k] > 1.0f - FLT_EPSILON ? 1.0f - FLT_EPSILON : d.q[k]);
         const float l = logf(c);
-        H += l * q[k];
-        if (k == ai) { la = l; qa = q[k]; }
+        d.H += l * d.q[k];
+        if (k == d.ai) { la = l; d.qa = d.q[k]; }
       }
     }
-    H = -H;
-    logp = bad ? __builtin_nanf("") : la;
+    d.H = -d.H;
+    d.logp = bad ? __builtin_nanf("") : la;
   } else {
     const float half_log_2pi = 0.91893853320467274f;  // log(sqrt(2 pi))
 #pragma unroll
@@ -320,14 +329,31 @@ __device__ inline void upd_row_loss(const UpdNet& n, const UpdAct& a, int r, flo
         const float lsr = O[A + k];
         const float lsc = lsr < -2.0f ? -2.0f : (lsr > 2.0f ? 2.0f : lsr);
         const float sd = log1pf(expf(lsc));               // softplus, beta 1 (lsc <= 2 < 20)
-        const float d = a.Ar[r * a.AX + k] - mu;
+        const float dd = act[k] - mu;
         const float lsd = logf(sd);
-        logp += -(d * d) / (2.0f * (sd * sd)) - lsd - half_log_2pi;
-        H += 0.5f + half_log_2pi + lsd;
+        d.logp += -(dd * dd) / (2.0f * (sd * sd)) - lsd - half_log_2pi;
+        d.H += 0.5f + half_log_2pi + lsd;
       }
     }
   }
-  const float V = O[n.ocol[n.nh - 1]];
+}
+
+// Per-row loss (surrogate, prl_loss.hip semantics) and the gradient w.r.t. the head outputs.
+// Loops run to the compile-time UPD_MAXA with `k < A` guards so everything stays in registers.
+template <int KD, int KA>
+__device__ inline void upd_row_loss(const UpdNet& n, const UpdAct& a, int r, float invB, float clip,
+                                    float vf_coef) {
+  const float* O = a.O + r * a.OX;
+  float* dO = a.dO + r * a.OX;
+  const int A = KA > 0 ? KA : n.A;
+  const bool discrete = KD >= 0 ? (KD != 0) : (n.discrete != 0);
+  const int vcol = discrete ? A : 2 * A;      // critic output column
+  UpdDist dist;
+  upd_row_dist<KD, KA>(n, O, a.Ar + r * a.AX, dist);
+  const float logp = dist.logp, H = dist.H, S2 = dist.S2, qa = dist.qa;
+  const int ai = dist.ai;
+  const float* p = dist.p;
+  const float V = O[vcol];
   // surrogate
   const float diff = logp - a.oldlp[r];
   const float cl = diff < -20.0f ? -20.0f : (diff > 20.0f ? 20.0f : diff);
@@ -349,12 +375,12 @@ __device__ inline void upd_row_loss(const UpdNet& n, const UpdAct& a, int r, flo
   const float ax = fabsf(x);
   const float sl = ax < 1.0f ? 0.5f * ax * ax : ax - 0.5f;
   const float gx = ax < 1.0f ? x : (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f));
-  dO[n.ocol[n.nh - 1]] = vf_coef * invB * gx;
+  dO[vcol] = vf_coef * invB * gx;
   a.lossp[r * 4 + 0] = -m;
   a.lossp[r * 4 + 1] = sl;
   a.lossp[r * 4 + 2] = H;
   // d logp / d head outputs
-  if (n.discrete) {
+  if (discrete) {
     const float mk = (qa >= FLT_EPSILON && qa <= 1.0f - FLT_EPSILON) ? 1.0f : 0.0f;
     const float gq = (logp != logp) ? logp : dlogp * mk;
     float dp[UPD_MAXA];
@@ -386,21 +412,177 @@ __device__ inline void upd_row_loss(const UpdNet& n, const UpdAct& a, int r, flo
   }
 }
 
-// one chunk of rc <= RC rows: forward, loss, backward; gradients accumulated into Ga (LDS image)
-__device__ void upd_chunk(const UpdArgs& args, const float* W, float* Ga, const UpdAct& a,
-                          int64_t row0, int rc, float invB) {
-  const UpdNet& n = args.net;
+// Cross-lane moves within 8-lane groups by DPP (no LDS round trip, unlike __shfl*, which lowers
+// to ds_bpermute): quad_perm [1,0,3,2] = xor 1, [2,3,0,1] = xor 2, row_half_mirror (lane i <->
+// 7 - i) carries the other quad's sum.  Every lane of a group ends with the same bits (IEEE add
+// is commutative).
+template <int CTRL>
+__device__ inline float upd_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ inline float upd_xor1(float v) { return upd_dpp<0xB1>(v); }
+__device__ inline float upd_xor2(float v) { return upd_dpp<0x4E>(v); }
+// sum over the 8 consecutive lanes of a GroupNorm group (lanes = channels)
+__device__ inline float upd_gsum8(float v) {
+  v += upd_xor1(v);
+  v += upd_xor2(v);
+  v += upd_dpp<0x141>(v);
+  return v;
+}
+
+// GroupNorm(8, 64) + SiLU forward of one element, lanes = channels o (group = 8 lanes)
+__device__ inline void upd_gn_fwd_lane(float v, float gw, float gb, float* xh_out, float* y_out,
+                                       float* rstd_out, bool write_rstd) {
+  const float mean = upd_gsum8(v) * (1.0f / 8);
+  const float dv = v - mean;
+  const float rstd = 1.0f / sqrtf(upd_gsum8(dv * dv) * (1.0f / 8) + 1e-5f);
+  const float xh = dv * rstd;
+  const float u = xh * gw + gb;
+  *xh_out = xh;
+  *y_out = u / (1.0f + expf(-u));
+  if (write_rstd) *rstd_out = rstd;
+}
+
+// backward of the above: go = d(block output); writes dX, returns du (= d pre-SiLU)
+__device__ inline float upd_gn_bwd_lane(float go, float xh, float gw, float gb, float rstd,
+                                        float* dx_out) {
+  const float u = xh * gw + gb;
+  const float sg = upd_sigmoid(u);
+  const float dy = go * (sg * (1.0f + u * (1.0f - sg)));
+  const float dxh = dy * gw;
+  const float m1 = upd_gsum8(dxh) * (1.0f / 8);
+  const float m2 = upd_gsum8(dxh * xh) * (1.0f / 8);
+  *dx_out = rstd * (dxh - m1 - xh * m2);
+  return dy;
+}
+
+__device__ inline int upd_head_of(const UpdNet& n, int j) {
+  int h = 0;
+  while (h + 1 < n.nh && j >= n.ocol[h + 1]) ++h;
+  return h;
+}
+
+// Forward of rc <= RC rows (ActorCritic.get_evaluate's network part): S0 inputs, S1 trunk,
+// S2 heads, then the head outputs O gathered to each row's leader lane (t == 32 r) — the only
+// reader of O[r] in the caller's per-row epilogue, so no barrier follows.
+__device__ inline void upd_forward(const UpdNet& n, const float* W, const UpdAct& a,
+                                   const float* Sg, const float* actg, int64_t row0, int rc,
+                                   unsigned long long* tm, bool timer, unsigned long long& tl) {
   const int t = threadIdx.x;
   const int D = n.D, A = n.A, nh = n.nh;
-  // 0. inputs
+#define UPD_CMARK(i)                                                   \
+  if (timer) {                                                         \
+    const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();  \
+    tm[i] += now_ - tl;                                                \
+    tl = now_;                                                         \
+  }
+  // S0. inputs
   for (int i = t; i < UPD_RC * a.DX; i += UPD_THREADS) {
     const int r = i / a.DX, d = i % a.DX;
-    a.X[i] = (r < rc && d < D) ? args.S[(row0 + r) * D + d] : 0.0f;
+    a.X[i] = (r < rc && d < D) ? Sg[(row0 + r) * D + d] : 0.0f;
   }
   const int Aw = n.discrete ? 1 : A;
   for (int i = t; i < UPD_RC * a.AX; i += UPD_THREADS) {
     const int r = i / a.AX, k = i % a.AX;
-    a.Ar[i] = (r < rc && k < Aw) ? args.act[(row0 + r) * Aw + k] : 0.0f;
+    a.Ar[i] = (r < rc && k < Aw) ? actg[(row0 + r) * Aw + k] : 0.0f;
+  }
+  __syncthreads();
+  UPD_CMARK(0)
+  // Lanes = the 64 channels o of a row; wave w takes rows w and w + 4 (wave-uniform).
+  const int o = t & 63, wv = t >> 6;
+  // S1. trunk: H0 = X W0^T -> GroupNorm -> SiLU
+  for (int r = wv; r < rc; r += 4) {
+    const float* x = a.X + r * a.DX;
+    const float* w = W + n.w0.lds + o * n.w0.stride;
+    float acc = 0.f;
+    for (int d = 0; d < D; ++d) acc += x[d] * w[d];
+    upd_gn_fwd_lane(acc, W[n.g0.lds + o], W[n.b0.lds + o], a.XH0 + r * UPD_HS + o,
+                    a.F + r * UPD_HS + o, a.rstd0 + r * 8 + (o >> 3), (o & 7) == 0);
+  }
+  __syncthreads();
+  UPD_CMARK(1)
+  // S2. heads: Z_h = F W1_h^T -> GroupNorm -> SiLU (rows w and w + 4 share each W1 read)
+  for (int h = 0; h < nh; ++h) {
+    const float* wrow = W + n.w1[h].lds + o * UPD_HS;
+    const int r0 = wv, r1 = wv + 4;
+    const bool two = r1 < rc;
+    if (r0 >= rc) break;
+    const float* f0 = a.F + r0 * UPD_HS;
+    const float* f1 = a.F + (two ? r1 : r0) * UPD_HS;
+    float z0 = 0.f, z1 = 0.f;
+#pragma unroll 4
+    for (int i = 0; i < UPD_H; i += 4) {
+      const float4 w4 = *reinterpret_cast<const float4*>(wrow + i);
+      const float4 a4 = *reinterpret_cast<const float4*>(f0 + i);
+      const float4 b4 = *reinterpret_cast<const float4*>(f1 + i);
+      z0 += a4.x * w4.x; z0 += a4.y * w4.y; z0 += a4.z * w4.z; z0 += a4.w * w4.w;
+      z1 += b4.x * w4.x; z1 += b4.y * w4.y; z1 += b4.z * w4.z; z1 += b4.w * w4.w;
+    }
+    const float gw = W[n.g1[h].lds + o], gb = W[n.b1[h].lds + o];
+    upd_gn_fwd_lane(z0, gw, gb, a.XH(h) + r0 * UPD_HS + o, a.Gh(h) + r0 * UPD_HS + o,
+                    a.rstd(h) + r0 * 8 + (o >> 3), (o & 7) == 0);
+    if (two)
+      upd_gn_fwd_lane(z1, gw, gb, a.XH(h) + r1 * UPD_HS + o, a.Gh(h) + r1 * UPD_HS + o,
+                      a.rstd(h) + r1 * 8 + (o >> 3), (o & 7) == 0);
+  }
+  __syncthreads();
+  UPD_CMARK(2)
+  // S3. head outputs + loss: one half-wave per row; lane l = (output j % 8, quarter of the 64
+  //     inputs); quarter sums combined by shuffles, gathered by the row's leader lane, which
+  //     writes O, evaluates the loss and writes d(loss)/d(outputs)
+  {
+    const int r = t >> 5, l = t & 31, jl = l >> 2, part = l & 3;
+    for (int j0 = 0; j0 < n.nout; j0 += 8) {
+      const int j = j0 + jl;
+      float acc = 0.f;
+      if (r < rc && j < n.nout) {
+        const int h = upd_head_of(n, j), k = j - n.ocol[h];
+        const float* wv = W + n.w2[h].lds + k * UPD_HS + part * 16;
+        const float* gv = a.Gh(h) + r * UPD_HS + part * 16;
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+          const float4 w4 = *reinterpret_cast<const float4*>(wv + i);
+          const float4 g4 = *reinterpret_cast<const float4*>(gv + i);
+          acc += g4.x * w4.x;
+          acc += g4.y * w4.y;
+          acc += g4.z * w4.z;
+          acc += g4.w * w4.w;
+        }
+      }
+      acc += upd_xor1(acc);
+      acc += upd_xor2(acc);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {    // gather to the row leaders: two scalar reads per j
+        const float vlo = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), 4 * jj));
+        const float vhi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), 32 + 4 * jj));
+        const float v = (t & 32) ? vhi : vlo;
+        const int jo = j0 + jj;
+        if (l == 0 && r < rc && jo < n.nout) {
+          const int h = upd_head_of(n, jo);
+          a.O[r * a.OX + jo] = v + W[n.b2[h].lds + (jo - n.ocol[h])];
+        }
+      }
+    }
+  }
+#undef UPD_CMARK
+}
+
+// One chunk of rc <= RC rows: forward, loss, backward; gradients accumulated into Ga (LDS
+// image).  Eight barrier-separated stages; each Linear is fused with the GroupNorm that follows
+// it (one thread per (row, group) owns 8 channels end to end).
+template <int KD, int KA>
+__device__ void upd_chunk(const UpdArgs& args, const float* W, float* Ga, const UpdAct& a,
+                          int64_t row0, int rc, float invB, unsigned long long* tm) {
+  const UpdNet& n = args.net;
+  const int t = threadIdx.x;
+  const int D = n.D, A = n.A, nh = n.nh;
+  const bool timer = blockIdx.x == 0 && t == 0;
+  unsigned long long tl = timer ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#define UPD_CMARK(i)                                                   \
+  if (timer) {                                                         \
+    const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();  \
+    tm[i] += now_ - tl;                                                \
+    tl = now_;                                                         \
   }
   if (t < UPD_RC) {
     const bool ok = t < rc;
@@ -408,118 +590,31 @@ __device__ void upd_chunk(const UpdArgs& args, const float* W, float* Ga, const 
     a.adv[t] = ok ? args.adv[row0 + t] : 0.0f;
     a.ret[t] = ok ? args.ret[row0 + t] : 0.0f;
   }
-  __syncthreads();
-  // 1. H0 = X W0^T
-  for (int i = t; i < rc * UPD_H; i += UPD_THREADS) {
-    const int r = i >> 6, o = i & 63;
-    const float* w = W + n.w0.lds + o * n.w0.stride;
-    const float* x = a.X + r * a.DX;
-    float acc = 0.f;
-    for (int d = 0; d < D; ++d) acc += x[d] * w[d];
-    a.T0[r * UPD_HS + o] = acc;
-  }
-  __syncthreads();
-  // 2. trunk GroupNorm + SiLU
-  if (t < rc * 8) {
-    const int r = t >> 3, g = t & 7;
-    upd_gn_fwd(a.T0 + r * UPD_HS + g * 8, W + n.g0.lds + g * 8, W + n.b0.lds + g * 8,
-               a.XH0 + r * UPD_HS + g * 8, a.F + r * UPD_HS + g * 8, a.rstd0 + r * 8 + g);
-  }
-  __syncthreads();
-  // 3. Z_h = F W1_h^T   (thread = (head, output column), all rows)
-  if (t < nh * UPD_H) {
-    const int h = t >> 6, o = t & 63;
-    const float* w = W + n.w1[h].lds + o * UPD_HS;
-    float acc[UPD_RC];
-#pragma unroll
-    for (int r = 0; r < UPD_RC; ++r) acc[r] = 0.f;
-    for (int i = 0; i < UPD_H; i += 4) {
-      const float4 wv = *reinterpret_cast<const float4*>(w + i);
-#pragma unroll
-      for (int r = 0; r < UPD_RC; ++r) {
-        const float4 f = *reinterpret_cast<const float4*>(a.F + r * UPD_HS + i);
-        acc[r] += f.x * wv.x;
-        acc[r] += f.y * wv.y;
-        acc[r] += f.z * wv.z;
-        acc[r] += f.w * wv.w;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < UPD_RC; ++r)
-      if (r < rc) a.ZB(h)[r * UPD_HS + o] = acc[r];
-  }
-  __syncthreads();
-  // 4. head GroupNorm + SiLU
-  if (t < nh * rc * 8) {
-    const int h = t / (rc * 8), rg = t % (rc * 8), r = rg >> 3, g = rg & 7;
-    upd_gn_fwd(a.ZB(h) + r * UPD_HS + g * 8, W + n.g1[h].lds + g * 8, W + n.b1[h].lds + g * 8,
-               a.XH(h) + r * UPD_HS + g * 8, a.Gh(h) + r * UPD_HS + g * 8, a.rstd(h) + r * 8 + g);
-  }
-  __syncthreads();
-  // 5. outputs O[r][col] = G_h W2_h^T + b2_h
-  for (int i = t; i < rc * n.nout; i += UPD_THREADS) {
-    const int r = i / n.nout, j = i % n.nout;
-    int h = 0;
-    while (h + 1 < nh && j >= n.ocol[h + 1]) ++h;
-    const int k = j - n.ocol[h];
-    const float* w = W + n.w2[h].lds + k * n.w2[h].stride;
-    const float* gv = a.Gh(h) + r * UPD_HS;
-    float acc = 0.f;
-    for (int c = 0; c < UPD_H; c += 4) {
-      const float4 wv = *reinterpret_cast<const float4*>(w + c);
-      const float4 g4 = *reinterpret_cast<const float4*>(gv + c);
-      acc += g4.x * wv.x;
-      acc += g4.y * wv.y;
-      acc += g4.z * wv.z;
-      acc += g4.w * wv.w;
-    }
-    a.O[r * a.OX + j] = acc + W[n.b2[h].lds + k];
-  }
-  __syncthreads();
-  // 6. loss + d(head outputs)
-  if (t < rc) upd_row_loss(n, a, t, invB, args.clip, args.vf_coef);
-  __syncthreads();
-  // 7. dG_h = dO_h W2_h;  dW2_h += dO_h^T G_h;  db2_h;  loss partials
-  for (int i = t; i < nh * rc * UPD_H; i += UPD_THREADS) {
-    const int h = i / (rc * UPD_H), ri = i % (rc * UPD_H), r = ri >> 6, c = ri & 63;
-    const float* dO = a.dO + r * a.OX + n.ocol[h];
-    float acc = 0.f;
-    for (int k = 0; k < n.out[h]; ++k) acc += dO[k] * W[n.w2[h].lds + k * n.w2[h].stride + c];
-    a.ZB(h)[r * UPD_HS + c] = acc;
-  }
-  for (int i = t; i < n.nout * UPD_H; i += UPD_THREADS) {
-    const int j = i >> 6, c = i & 63;
-    int h = 0;
-    while (h + 1 < nh && j >= n.ocol[h + 1]) ++h;
-    const int k = j - n.ocol[h];
-    float acc = 0.f;
-    for (int r = 0; r < rc; ++r) acc += a.dO[r * a.OX + j] * a.Gh(h)[r * UPD_HS + c];
-    Ga[n.w2[h].lds + k * n.w2[h].stride + c] += acc;
-  }
-  if (t < n.nout) {
-    int h = 0;
-    while (h + 1 < nh && t >= n.ocol[h + 1]) ++h;
-    float acc = 0.f;
-    for (int r = 0; r < rc; ++r) acc += a.dO[r * a.OX + t];
-    Ga[n.b2[h].lds + (t - n.ocol[h])] += acc;
-  }
-  if (t >= 64 && t < 64 + 3) {
-    const int which = t - 64;
-    float acc = 0.f;
-    for (int r = 0; r < rc; ++r) acc += a.lossp[r * 4 + which];
-    Ga[n.Lp + which] += acc;
-  }
-  __syncthreads();
-  // 8. head GroupNorm + SiLU backward (ZB: dG -> dZ)
-  if (t < nh * rc * 8) {
-    const int h = t / (rc * 8), rg = t % (rc * 8), r = rg >> 3, g = rg & 7;
-    upd_gn_bwd(a.ZB(h) + r * UPD_HS + g * 8, a.XH(h) + r * UPD_HS + g * 8,
-               W + n.g1[h].lds + g * 8, W + n.b1[h].lds + g * 8, a.rstd(h)[r * 8 + g],
-               a.DU(h) + r * UPD_HS + g * 8);
-  }
-  __syncthreads();
-  // 9a. dW1_h += dZ_h^T F   (thread: 4 contiguous input columns x 4 output rows, per head)
+  upd_forward(n, W, a, args.S, args.act, row0, rc, tm, timer, tl);
+  const int o = t & 63, wv = t >> 6;
   {
+    const int r = t >> 5, l = t & 31;
+    if (l == 0 && r < rc) upd_row_loss<KD, KA>(n, a, r, invB, args.clip, args.vf_coef);
+  }
+  __syncthreads();
+  UPD_CMARK(3)
+  // S4. dG_h = dO_h W2_h -> head GroupNorm + SiLU backward (lanes = channels)
+  for (int h = 0; h < nh; ++h) {
+    const float gw = W[n.g1[h].lds + o], gb = W[n.b1[h].lds + o];
+    for (int r = wv; r < rc; r += 4) {
+      const float* dO = a.dO + r * a.OX + n.ocol[h];
+      float dg = 0.f;
+      for (int k = 0; k < n.out[h]; ++k) dg += dO[k] * W[n.w2[h].lds + k * UPD_HS + o];
+      a.DU(h)[r * UPD_HS + o] =
+          upd_gn_bwd_lane(dg, a.XH(h)[r * UPD_HS + o], gw, gb, a.rstd(h)[r * 8 + (o >> 3)],
+                          a.ZB(h) + r * UPD_HS + o);
+    }
+  }
+  __syncthreads();
+  UPD_CMARK(4)
+  // S5. weight gradients of the heads + per-head parts of dF
+  {
+    // dW1_h += dZ_h^T F   (thread: 4 contiguous input columns x 4 output rows, per head)
     const int i4 = (t & 15) * 4, ob = t >> 4;
     for (int h = 0; h < nh; ++h) {
       float acc[4][4];
@@ -527,7 +622,9 @@ __device__ void upd_chunk(const UpdArgs& args, const float* W, float* Ga, const 
       for (int k = 0; k < 4; ++k)
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[k][c] = 0.f;
-      for (int r = 0; r < rc; ++r) {
+#pragma unroll 4
+      for (int r = 0; r < UPD_RC; ++r) {
+        if (r >= rc) break;
         const float4 f = *reinterpret_cast<const float4*>(a.F + r * UPD_HS + i4);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -550,11 +647,12 @@ __device__ void upd_chunk(const UpdArgs& args, const float* W, float* Ga, const 
       }
     }
   }
-  // 9b. head GroupNorm weight/bias grads (column sums)
-  if (t < nh * UPD_H) {
+  if (t < nh * UPD_H) {   // head GroupNorm weight / bias
     const int h = t >> 6, c = t & 63;
     float sw = 0.f, sb = 0.f;
-    for (int r = 0; r < rc; ++r) {
+#pragma unroll
+    for (int r = 0; r < UPD_RC; ++r) {
+      if (r >= rc) break;
       const float du = a.DU(h)[r * UPD_HS + c];
       sw += du * a.XH(h)[r * UPD_HS + c];
       sb += du;
@@ -562,41 +660,73 @@ __device__ void upd_chunk(const UpdArgs& args, const float* W, float* Ga, const 
     Ga[n.g1[h].lds + c] += sw;
     Ga[n.b1[h].lds + c] += sb;
   }
-  // 9c. dF = sum_h dZ_h W1_h   (thread: one row, 2 adjacent columns)
-  for (int i = t; i < rc * 32; i += UPD_THREADS) {
-    const int r = i >> 5, c2 = (i & 31) * 2;
-    float s0 = 0.f, s1 = 0.f;
-    for (int h = 0; h < nh; ++h) {
-      const float* dz = a.ZB(h) + r * UPD_HS;
-      const float* w = W + n.w1[h].lds + c2;
-      for (int o = 0; o < UPD_H; ++o) {
-        const float2 wv = *reinterpret_cast<const float2*>(w + o * UPD_HS);
-        const float z = dz[o];
-        s0 += z * wv.x;
-        s1 += z * wv.y;
+  for (int i = t; i < n.nout * UPD_H; i += UPD_THREADS) {   // dW2 += dO^T G
+    const int j = i >> 6, c = i & 63;
+    const int h = upd_head_of(n, j), k = j - n.ocol[h];
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < UPD_RC; ++r)
+      if (r < rc) acc += a.dO[r * a.OX + j] * a.Gh(h)[r * UPD_HS + c];
+    Ga[n.w2[h].lds + k * UPD_HS + c] += acc;
+  }
+  if (t < n.nout) {   // db2
+    const int h = upd_head_of(n, t);
+    float acc = 0.f;
+    for (int r = 0; r < rc; ++r) acc += a.dO[r * a.OX + t];
+    Ga[n.b2[h].lds + (t - n.ocol[h])] += acc;
+  }
+  if (t >= 64 && t < 64 + 3) {   // loss partials
+    const int which = t - 64;
+    float acc = 0.f;
+    for (int r = 0; r < rc; ++r) acc += a.lossp[r * 4 + which];
+    Ga[n.Lp + which] += acc;
+  }
+  for (int it = t; it < nh * rc * 16; it += UPD_THREADS) {   // dF_h = dZ_h W1_h
+    const int h = it / (rc * 16), rem = it % (rc * 16), r = rem >> 4, c4 = (rem & 15) * 4;
+    const float* dz = a.ZB(h) + r * UPD_HS;
+    const float* w = W + n.w1[h].lds + c4;
+    float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int o = 0; o < UPD_H; o += 4) {
+      const float4 z4 = *reinterpret_cast<const float4*>(dz + o);
+      const float zz[4] = {z4.x, z4.y, z4.z, z4.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 w4 = *reinterpret_cast<const float4*>(w + (o + u) * UPD_HS);
+        acc.x += zz[u] * w4.x;
+        acc.y += zz[u] * w4.y;
+        acc.z += zz[u] * w4.z;
+        acc.w += zz[u] * w4.w;
       }
     }
-    a.T0[r * UPD_HS + c2] = s0;
-    a.T0[r * UPD_HS + c2 + 1] = s1;
+    *reinterpret_cast<float4*>(a.dF(h) + r * UPD_HS + c4) = acc;
   }
   __syncthreads();
-  // 10. trunk GroupNorm + SiLU backward (T0: dF -> dH0)
-  if (t < rc * 8) {
-    const int r = t >> 3, g = t & 7;
-    upd_gn_bwd(a.T0 + r * UPD_HS + g * 8, a.XH0 + r * UPD_HS + g * 8, W + n.g0.lds + g * 8,
-               W + n.b0.lds + g * 8, a.rstd0[r * 8 + g], a.DU0 + r * UPD_HS + g * 8);
+  UPD_CMARK(5)
+  // S6. trunk GroupNorm + SiLU backward (lanes = channels): dF = sum_h dF_h
+  for (int r = wv; r < rc; r += 4) {
+    float df = 0.f;
+    for (int h = 0; h < nh; ++h) df += a.dF(h)[r * UPD_HS + o];
+    a.DU0[r * UPD_HS + o] = upd_gn_bwd_lane(df, a.XH0[r * UPD_HS + o], W[n.g0.lds + o],
+                                            W[n.b0.lds + o], a.rstd0[r * 8 + (o >> 3)],
+                                            a.T0 + r * UPD_HS + o);
   }
   __syncthreads();
-  // 11. dW0 += dH0^T X;  trunk GroupNorm weight/bias grads
+  UPD_CMARK(6)
+  // S7. dW0 += dH0^T X;  trunk GroupNorm weight / bias
   for (int i = t; i < UPD_H * D; i += UPD_THREADS) {
     const int o = i / D, d = i % D;
     float acc = 0.f;
-    for (int r = 0; r < rc; ++r) acc += a.T0[r * UPD_HS + o] * a.X[r * a.DX + d];
+#pragma unroll
+    for (int r = 0; r < UPD_RC; ++r)
+      if (r < rc) acc += a.T0[r * UPD_HS + o] * a.X[r * a.DX + d];
     Ga[n.w0.lds + o * n.w0.stride + d] += acc;
   }
   if (t < UPD_H) {
     float sw = 0.f, sb = 0.f;
-    for (int r = 0; r < rc; ++r) {
+#pragma unroll
+    for (int r = 0; r < UPD_RC; ++r) {
+      if (r >= rc) break;
       const float du = a.DU0[r * UPD_HS + t];
       sw += du * a.XH0[r * UPD_HS + t];
       sb += du;
@@ -605,38 +735,77 @@ __device__ void upd_chunk(const UpdArgs& args, const float* W, float* Ga, const 
     Ga[n.b0.lds + t] += sb;
   }
   __syncthreads();
+  UPD_CMARK(7)
+#undef UPD_CMARK
 }
 
-__global__ __launch_bounds__(UPD_THREADS, 1) void ppo_update_kernel(UpdArgs args) {
+__device__ inline float f4get(const float4& v, int e) {
+  return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
+}
+__device__ inline void f4set(float4& v, int e, float x) {
+  if (e == 0) v.x = x; else if (e == 1) v.y = x; else if (e == 2) v.z = x; else v.w = x;
+}
+
+// NQ = parameter quads per thread (ceil(Lp / 4 / 256)): AdamW's moments live in registers.
+template <int NQ, int KD, int KA>
+__global__ __launch_bounds__(UPD_THREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void
+ppo_update_kernel(UpdArgs args) {
   extern __shared__ __align__(16) float upd_lds[];
   const UpdNet& n = args.net;
   const int t = threadIdx.x, g = blockIdx.x, G = args.G;
   const int Lp = n.Lp;
   const int Qp = Lp / 4;            // parameter quads
   const int Qtot = Qp + 1;          // + one quad of loss partials
-  float* hdr = upd_lds;             // [16] broadcast words
-  float* W = upd_lds + 16;          // [Lp]
+  float* hdr = upd_lds;             // [64] broadcast words + chunk stage timers
+  float* W = upd_lds + 64;          // [Lp]
   float* Ga = W + Lp;               // [Lp + 4]
   float* scratch = Ga + Lp + 4;     // activations / reduction scratch
   const UpdAct a = upd_carve(scratch, n);
   float* s_bcast = hdr;             // [0] clip coefficient, [1] loss
   float* s_ssq = hdr + 4;           // [4] per-wave sums of squares
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
-  float* pm = args.priv + (size_t)g * 2 * Lp;
-  float* pv = pm + Lp;
 
-  // ---- load parameters (LDS image) and this workgroup's private moments -----------------------
+  // ---- load parameters (LDS image) and this thread's moments (quad q = t + 256 i, registers);
+  //      the moments are scattered into the LDS image layout through Ga (free until phase A) ---
+  float4 mreg[NQ], vreg[NQ];
   for (int k = t; k < Lp; k += UPD_THREADS) {
     const int f = upd_flat_of(n, k);
     W[k] = f >= 0 ? args.params[f] : 0.0f;
-    pm[k] = f >= 0 ? args.exp_avg[f] : 0.0f;   // thread-private entries (same k mapping below)
-    pv[k] = f >= 0 ? args.exp_avg_sq[f] : 0.0f;
+    Ga[k] = f >= 0 ? args.exp_avg[f] : 0.0f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int q = t + i * UPD_THREADS;
+    mreg[i] = q < Qp ? *reinterpret_cast<const float4*>(Ga + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+  for (int k = t; k < Lp; k += UPD_THREADS) {
+    const int f = upd_flat_of(n, k);
+    Ga[k] = f >= 0 ? args.exp_avg_sq[f] : 0.0f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int q = t + i * UPD_THREADS;
+    vreg[i] = q < Qp ? *reinterpret_cast<const float4*>(Ga + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
   }
   const float step0 = args.adam_step[0];
+  if (t < 24) reinterpret_cast<unsigned long long*>(hdr + 16)[t] = 0ull;
   __syncthreads();
 
   const int R = args.R;
   float loss_last = 0.f;
+  unsigned long long pt[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tp = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long rt0 = tp, ck0 = __builtin_amdgcn_s_memtime();
+  auto mark = [&](int i) {
+    if (g == 0 && t == 0) {
+      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+      pt[i] += now - tp;
+      tp = now;
+    }
+  };
   for (int s = 0; s < args.total_steps; ++s) {
     const int j = s % args.nb;
     const int64_t mb0 = (int64_t)j * args.mb;
@@ -647,18 +816,22 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_update_kernel(UpdArgs args
     for (int k = t; k < Lp + 4; k += UPD_THREADS) Ga[k] = 0.0f;
     __syncthreads();
     for (int c0 = 0; c0 < myrows; c0 += UPD_RC)
-      upd_chunk(args, W, Ga, a, mb0 + (int64_t)g * R + c0, std::min(UPD_RC, myrows - c0), invB);
-    float* mypart = args.part + (size_t)g * Qtot * 4;
+      upd_chunk<KD, KA>(args, W, Ga, a, mb0 + (int64_t)g * R + c0, std::min(UPD_RC, myrows - c0), invB,
+                reinterpret_cast<unsigned long long*>(hdr + 16));
+    mark(0);   // phase A compute
+    const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(args.red);
     for (int q = t; q < Qtot; q += UPD_THREADS)
-      st4_sc1(mypart + 4 * q, *reinterpret_cast<const float4*>(Ga + 4 * q));
+      st4_sc1(rs_part, ((size_t)g * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    mark(1);   // publish partials
     if (t == 0) {
       __hip_atomic_fetch_add(args.ctr + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *s_abort = upd_wait(args.ctr, 0, (unsigned)G * (unsigned)(s + 1)) ? 0 : 1;
     }
     __syncthreads();
     if (*s_abort) return;
+    mark(2);   // wait A
     // ---- phase B: reduce slice [qlo, qhi) over the G partials (workgroup order) ---------------
     {
       const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
@@ -668,11 +841,12 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_update_kernel(UpdArgs args
         // wide slices (few workgroups): each thread owns whole quads, partials summed in order
         for (int qi = t; qi < nq; qi += UPD_THREADS) {
           float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
           for (int gg = 0; gg < G; ++gg) {
-            const float4 v = ld4_sc1(args.part + ((size_t)gg * Qtot + qlo + qi) * 4);
+            const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
             acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
           }
-          st4_sc1(args.red + (size_t)(qlo + qi) * 4, acc);
+          st4_sc1(rs_red, (size_t)(qlo + qi) * 4, acc);
           if (qlo + qi < Qp) ssq += acc.x * acc.x + acc.y * acc.y + acc.z * acc.z + acc.w * acc.w;
         }
       } else if (nq > 0) {
@@ -683,8 +857,9 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_update_kernel(UpdArgs args
         if (t < spl * nq) {
           const int qi = t % nq, sub = t / nq;
           float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
           for (int gg = sub; gg < G; gg += spl) {
-            const float4 v = ld4_sc1(args.part + ((size_t)gg * Qtot + qlo + qi) * 4);
+            const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
             acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
           }
           red4[sub * nq + qi] = acc;
@@ -696,7 +871,7 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_update_kernel(UpdArgs args
             const float4 v = red4[sub * nq + t];
             acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
           }
-          st4_sc1(args.red + (size_t)(qlo + t) * 4, acc);
+          st4_sc1(rs_red, (size_t)(qlo + t) * 4, acc);
           if (qlo + t < Qp) ssq = acc.x * acc.x + acc.y * acc.y + acc.z * acc.z + acc.w * acc.w;
         }
       }
@@ -711,24 +886,33 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_update_kernel(UpdArgs args
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      mark(3);   // slice reduce
       if (t == 0) {
         __hip_atomic_fetch_add(args.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *s_abort = upd_wait(args.ctr, 1, (unsigned)G * (unsigned)(s + 1)) ? 0 : 1;
       }
       __syncthreads();
       if (*s_abort) return;
+      mark(4);   // wait B
     }
     // ---- phase C: clip_grad_norm_(2.0) + AdamW on every workgroup's own copy ------------------
-    if (t == 0) {
-      float tot = 0.f;
-      for (int gg = 0; gg < G; ++gg) tot += ld_sc1f(args.sq + gg);
-      const float norm = sqrtf(tot);
-      const float coef = args.max_norm / (norm + 1e-6f);
-      s_bcast[0] = coef < 1.0f ? coef : 1.0f;
-      const float4 lp = ld4_sc1(args.red + (size_t)Qp * 4);
-      s_bcast[1] = lp.x * invB + args.vf_coef * (lp.y * invB) - args.ent_coef * (lp.z * invB);
+    {
+      float piece = t < G ? ld_sc1f(args.sq + t) : 0.f;     // every workgroup: same tree
+      piece = wave_sum(piece);
+      if ((t & 63) == 0) s_ssq[t >> 6] = piece;
+      __syncthreads();
+      if (t == 0) {
+        float tot = 0.f;
+        for (int w = 0; w < UPD_THREADS / 64; ++w) tot += s_ssq[w];
+        const float norm = sqrtf(tot);
+        const float coef = args.max_norm / (norm + 1e-6f);
+        s_bcast[0] = coef < 1.0f ? coef : 1.0f;
+        const float4 lp = ld4_sc1(rs_red, (size_t)Qp * 4);
+        s_bcast[1] = lp.x * invB + args.vf_coef * (lp.y * invB) - args.ent_coef * (lp.z * invB);
+      }
+      __syncthreads();
     }
-    __syncthreads();
+    mark(5);   // norm + loss
     const float clipc = s_bcast[0];
     loss_last = s_bcast[1];
     {
@@ -736,39 +920,121 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_update_kernel(UpdArgs args
       const double bc1 = 1.0 - pow((double)args.beta1, tstep);
       const double bc2 = 1.0 - pow((double)args.beta2, tstep);
       const float step_size = (float)((double)args.lr / bc1);
-      const float bc2_sqrt = (float)sqrt(bc2);
+      const float inv_bc2_sqrt = (float)(1.0 / sqrt(bc2));   // scalar divide -> one multiply
       const float decay = (float)(1.0 - (double)args.lr * (double)args.wd);
       const float b2 = args.beta2;
       const float omb1 = (float)(1.0 - (double)args.beta1), omb2 = (float)(1.0 - (double)args.beta2);
-      for (int k = t; k < Lp; k += UPD_THREADS) {
-        const float gr = ld_sc1f(args.red + k) * clipc;
-        float m = pm[k], v = pv[k], p = W[k];
-        p = p * decay;
-        m = m + omb1 * (gr - m);
-        v = v * b2 + omb2 * gr * gr;
-        const float denom = sqrtf(v) / bc2_sqrt + args.eps;
-        p = p - step_size * (m / denom);
-        pm[k] = m;
-        pv[k] = v;
-        W[k] = p;
+      constexpr int BATCH = NQ;  // every gradient load issued ahead of the arithmetic
+#pragma unroll
+      for (int i0 = 0; i0 < NQ; i0 += BATCH) {
+        float4 gq[BATCH];
+#pragma unroll
+        for (int b = 0; b < BATCH; ++b) {
+          const int q = t + (i0 + b) * UPD_THREADS;
+          if (i0 + b < NQ && q < Qp) gq[b] = ld4_sc1(rs_red, (size_t)q * 4);
+        }
+#pragma unroll
+        for (int b = 0; b < BATCH; ++b) {
+          const int i = i0 + b;
+          const int q = t + i * UPD_THREADS;
+          if (i < NQ && q < Qp) {
+            float4 pw = *reinterpret_cast<float4*>(W + 4 * q);
+            float4 m4 = mreg[i], v4 = vreg[i];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float gr = f4get(gq[b], e) * clipc;
+              float m = f4get(m4, e), v = f4get(v4, e), p = f4get(pw, e);
+              p = p * decay;
+              m = m + omb1 * (gr - m);
+              v = v * b2 + omb2 * gr * gr;
+              const float denom = __builtin_amdgcn_sqrtf(v) * inv_bc2_sqrt + args.eps;
+              float rq = __builtin_amdgcn_rcpf(denom);
+              rq = rq * (2.0f - denom * rq);              // one Newton step: ~0.5 ulp
+              p = p - step_size * (m * rq);
+              f4set(m4, e, m);
+              f4set(v4, e, v);
+              f4set(pw, e, p);
+            }
+            mreg[i] = m4;
+            vreg[i] = v4;
+            *reinterpret_cast<float4*>(W + 4 * q) = pw;
+          }
+        }
       }
     }
     __syncthreads();
+    mark(6);   // AdamW
   }
   // ---- write back (workgroup 0): parameters, moments, step count, last loss -------------------
   if (g == 0) {
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int q = t + i * UPD_THREADS;
+      if (q < Qp) *reinterpret_cast<float4*>(Ga + 4 * q) = mreg[i];
+    }
+    __syncthreads();
     for (int k = t; k < Lp; k += UPD_THREADS) {
       const int f = upd_flat_of(n, k);
       if (f >= 0) {
         args.params[f] = W[k];
-        args.exp_avg[f] = pm[k];
-        args.exp_avg_sq[f] = pv[k];
+        args.exp_avg[f] = Ga[k];
       }
     }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int q = t + i * UPD_THREADS;
+      if (q < Qp) *reinterpret_cast<float4*>(Ga + 4 * q) = vreg[i];
+    }
+    __syncthreads();
+    for (int k = t; k < Lp; k += UPD_THREADS) {
+      const int f = upd_flat_of(n, k);
+      if (f >= 0) args.exp_avg_sq[f] = Ga[k];
+    }
     if (t == 0) {
+      for (int i = 0; i < 7; ++i) args.prof[i] = pt[i];
+      args.prof[7] = (unsigned long long)args.total_steps;
+      args.prof[30] = __builtin_amdgcn_s_memrealtime() - rt0;
+      args.prof[31] = __builtin_amdgcn_s_memtime() - ck0;
+      for (int i = 0; i < 22; ++i) args.prof[8 + i] = reinterpret_cast<unsigned long long*>(hdr + 16)[i];
       args.adam_step[0] = step0 + (float)args.total_steps;
       if (args.loss_out) args.loss_out[0] = loss_last;
     }
+  }
+}
+
+// ActorCritic.get_evaluate over N rows (PPO.learn's policy_old pass, PPO.py:127-154):
+// log_prob, state value and (optionally) entropy per row, with exactly the update kernel's
+// forward arithmetic, so the first minibatch of learn() sees ratio == 1 exactly, as in the
+// reference.  Workgroups stride over 8-row chunks; parameters are staged once into LDS.
+template <int KD, int KA>
+__global__ __launch_bounds__(UPD_THREADS, 1) void ppo_evaluate_kernel(UpdArgs args, float* logp_out,
+                                                                    float* V_out, float* H_out) {
+  extern __shared__ __align__(16) float upd_lds[];
+  const UpdNet& n = args.net;
+  const int t = threadIdx.x;
+  float* W = upd_lds + 64;
+  const UpdAct a = upd_carve(W + n.Lp, n);
+  for (int k = t; k < n.Lp; k += UPD_THREADS) {
+    const int f = upd_flat_of(n, k);
+    W[k] = f >= 0 ? args.params[f] : 0.0f;
+  }
+  __syncthreads();
+  unsigned long long tl = 0;
+  const int64_t nchunks = (args.N + UPD_RC - 1) / UPD_RC;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t row0 = c * UPD_RC;
+    const int rc = (int)std::min<int64_t>(UPD_RC, args.N - row0);
+    upd_forward(n, W, a, args.S, args.act, row0, rc, nullptr, false, tl);
+    const int r = t >> 5, l = t & 31;
+    if (l == 0 && r < rc) {
+      UpdDist d;
+      upd_row_dist<KD, KA>(n, a.O + r * a.OX, a.Ar + r * a.AX, d);
+      logp_out[row0 + r] = d.logp;
+      V_out[row0 + r] = a.O[r * a.OX + n.ocol[n.nh - 1]];
+      if (H_out) H_out[row0 + r] = d.H;
+    }
+    __syncthreads();
   }
 }
 
@@ -817,35 +1083,51 @@ bool upd_layout(int D, int A, int discrete, UpdNet& n) {
   return true;
 }
 
+int upd_nq(const UpdNet& n) { return (int)cdiv(n.Lp / 4, UPD_THREADS); }
+// Specialisations for the configs' shapes (CartPole: discrete, A = 2; Pendulum: continuous,
+// A = 1); every other shape runs the generic (runtime head configuration) kernel.
+const void* upd_kernel_for(const UpdNet& n) {
+  const int nq = upd_nq(n);
+  if (n.discrete && n.A == 2 && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2>);
+  if (!n.discrete && n.A == 1 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1>);
+  if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0>);
+  return nullptr;
+}
+const void* upd_eval_kernel_for(const UpdNet& n) {
+  if (n.discrete && n.A == 2) return reinterpret_cast<const void*>(ppo_evaluate_kernel<1, 2>);
+  if (!n.discrete && n.A == 1) return reinterpret_cast<const void*>(ppo_evaluate_kernel<0, 1>);
+  return reinterpret_cast<const void*>(ppo_evaluate_kernel<-1, 0>);
+}
+
 int upd_grid(int64_t mb) { return (int)std::min<int64_t>(256, cdiv(mb, UPD_RC)); }
 
 size_t upd_lds_bytes(const UpdNet& n) {
   int DX, AX, OX;
   const int act = upd_act_floats(n.D, n.A, n.nout, DX, AX, OX);
-  return sizeof(float) * (size_t)(16 + 2 * n.Lp + 4 + act);
+  return sizeof(float) * (size_t)(64 + 2 * n.Lp + 4 + act);
 }
 
 struct UpdWs {
   unsigned* ctr;
+  unsigned long long* prof;
   float* sq;
   float* red;
   float* part;
-  float* priv;
 };
 
-// workspace: ctr[4] (16 B, zeroed per launch) | sq[256] | red[Qtot*4] | part[G][Qtot*4] | priv
+// workspace: ctr[4] (16 B, zeroed per launch) | prof[32] | sq[256] | red[Qtot*4] | part[G][Qtot*4]
 size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
   const size_t Qtot = (size_t)n.Lp / 4 + 1;
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-  const size_t o_ctr = take(16), o_sq = take(256 * 4), o_red = take(Qtot * 16),
-               o_part = take((size_t)G * Qtot * 16), o_priv = take((size_t)G * 2 * n.Lp * 4);
+  const size_t o_ctr = take(16), o_prof = take(256), o_sq = take(256 * 4), o_red = take(Qtot * 16),
+               o_part = take((size_t)G * Qtot * 16);
   if (ws) {
     ws->ctr = reinterpret_cast<unsigned*>(base + o_ctr);
+    ws->prof = reinterpret_cast<unsigned long long*>(base + o_prof);
     ws->sq = reinterpret_cast<float*>(base + o_sq);
     ws->red = reinterpret_cast<float*>(base + o_red);
     ws->part = reinterpret_cast<float*>(base + o_part);
-    ws->priv = reinterpret_cast<float*>(base + o_priv);
   }
   return off;
 }
@@ -866,7 +1148,7 @@ extern "C" int prl_ppo_update_info(int32_t D, int32_t A, int32_t discrete, int64
   if (n_params) *n_params = n.P;
   if (workspace_bytes) *workspace_bytes = (int64_t)upd_ws_carve(n, G, nullptr, nullptr);
   if (grid) *grid = G;
-  return upd_lds_bytes(n) <= 160 * 1024 ? PRL_OK : PRL_ERR_ARG;
+  return (upd_lds_bytes(n) <= 160 * 1024 && upd_kernel_for(n)) ? PRL_OK : PRL_ERR_ARG;
 }
 
 extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step,
@@ -918,17 +1200,41 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
   args.part = ws.part;
   args.red = ws.red;
   args.sq = ws.sq;
-  args.priv = ws.priv;
   args.ctr = ws.ctr;
+  args.prof = ws.prof;
   const size_t lds = upd_lds_bytes(args.net);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_update: %zu B of LDS needed", lds);
   hipStream_t st = as_stream(stream);
-  PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(ppo_update_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const void* kern = upd_kernel_for(args.net);
+  PRL_REQUIRE(kern, "prl_ppo_update: %d parameter quads per thread not built", upd_nq(args.net));
+  PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
   void* kargs[] = {&args};
-  PRL_HIP_TRY(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(ppo_update_kernel), dim3(G),
-                                     dim3(UPD_THREADS), kargs, (unsigned)lds, st));
+  PRL_HIP_TRY(hipLaunchCooperativeKernel(kern, dim3(G), dim3(UPD_THREADS), kargs, (unsigned)lds, st));
+  return PRL_OK;
+}
+
+extern "C" int prl_ppo_evaluate(const float* params, int32_t D, int32_t A, int32_t discrete,
+                                const float* S, const float* actions, int64_t N, float* logp,
+                                float* V, float* entropy, void* stream) {
+  UpdArgs args{};
+  PRL_REQUIRE(upd_layout(D, A, discrete, args.net), "prl_ppo_evaluate: D=%d A=%d not supported", D, A);
+  PRL_REQUIRE(N >= 0, "prl_ppo_evaluate: N < 0");
+  if (N == 0) return PRL_OK;
+  PRL_REQUIRE(params && S && actions && logp && V, "prl_ppo_evaluate: null pointer");
+  args.params = const_cast<float*>(params);
+  args.S = S;
+  args.act = actions;
+  args.N = N;
+  int DX, AX, OX;
+  const size_t lds = sizeof(float) * (size_t)(64 + args.net.Lp +
+                                              upd_act_floats(D, A, args.net.nout, DX, AX, OX));
+  PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_evaluate: %zu B of LDS needed", lds);
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(N, UPD_RC), 2 * 256);
+  const void* kern = upd_eval_kernel_for(args.net);
+  PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  void* kargs[] = {&args, &logp, &V, &entropy};
+  PRL_HIP_TRY(hipLaunchKernel(kern, dim3(grid), dim3(UPD_THREADS), kargs, lds, as_stream(stream)));
   return PRL_OK;
 }
 

@@ -54,6 +54,7 @@ SIGNATURES = {
     "prl_ppo_update": [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I32]
                       + [_F32] * 9 + [_P, _P, _I64, _P],
     "prl_ppo_update_status_ptr": [_P, _P],
+    "prl_ppo_evaluate": [_P, _I32, _I32, _I32, _P, _P, _I64, _P, _P, _P, _P],
 }
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64}
 
@@ -403,3 +404,14 @@ def ppo_update_status(workspace) -> torch.Tensor:
     _check(lib().prl_ppo_update_status_ptr(_dev(workspace, torch.uint8, "workspace"),
                                            ctypes.byref(ptr)), "prl_ppo_update_status_ptr")
     return workspace[12:16].view(torch.int32)
+
+
+def ppo_evaluate(params, D, A, discrete, S, actions, logp, V, entropy=None):
+    """ActorCritic.get_evaluate over all rows with the fused engine's forward arithmetic."""
+    N = int(S.shape[0])
+    _check(lib().prl_ppo_evaluate(_dev(params, torch.float32, "params"), int(D), int(A),
+                                  int(bool(discrete)), _dev(S, torch.float32, "S"),
+                                  _dev(actions, torch.float32, "actions"), N,
+                                  _dev(logp, torch.float32, "logp"), _dev(V, torch.float32, "V"),
+                                  _dev(entropy, torch.float32, "entropy"), _stream()),
+           "prl_ppo_evaluate")

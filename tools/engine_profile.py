@@ -1,0 +1,33 @@
+"""Fused update engine: learn() time and workgroup 0's per-phase breakdown (us per step) on the
+survey's C2 learn workload (2^20 synthetic CartPole transitions), at several mini_batch sizes."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "parallel-reinforcement-learning_amd"), os.path.join(ROOT, "tools")]
+from learn_bench import synthetic_batch  # noqa: E402
+from PPO import PPO  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+batch = synthetic_batch(N)
+for mb in (512, 2048, 65536):
+    for k in (11,):
+        torch.manual_seed(0)
+        p = PPO(False, 4, 2, lr=1e-3, k_epochs=k, batch_size=1, mini_batch_size=mb)
+        p.show_progress = False
+        p.memory.push_device(*batch)
+        p.learn()                                   # warm-up (engine creation, workspaces)
+        p.memory.push_device(*batch)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        p.learn()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        steps = k * -(-N // mb)
+        print(json.dumps({"mb": mb, "grid": p._engine.grid, "learn_ms": round(dt * 1e3, 1),
+                          "us_per_step": round(dt / steps * 1e6, 2),
+                          "phases_us": p._engine.profile()}), flush=True)
