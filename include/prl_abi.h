@@ -227,7 +227,32 @@ int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, float* adam
 int prl_ppo_evaluate(const float* params, int32_t D, int32_t A, int32_t discrete, const float* S,
                      const float* actions, int64_t N, float* logp, float* V, float* entropy,
                      void* stream);
-/* Host call: device address of the u32 status word inside an engine workspace. */
+/* ---- stepped engine (world_size > 1: one launch pair per optimizer step, gradient all-reduced
+ * by the caller between them; PPO.py:216-255 with the union of the ranks' j-th slices as the
+ * global minibatch j).  Parameters and moments live in an "image" layout (padded, Lp floats) in
+ * HBM for the whole loop. */
+/* Host call: floats of one image (Lp) + 4 (the gradient vector's loss-partials quad). */
+int64_t prl_ppo_image_floats(int32_t D, int32_t A, int32_t discrete);
+/* flat torch vectors (parameters() order) <-> images; to_image != 0: flat -> image. */
+int prl_ppo_image(int32_t D, int32_t A, int32_t discrete, float* params, float* exp_avg,
+                  float* exp_avg_sq, float* img_params, float* img_m, float* img_v,
+                  int32_t to_image, void* stream);
+/* Gradient of this rank's rows [j*mb, min((j+1)*mb, N)) of the union minibatch j, scaled by
+ * inv_count = 1 / (rows of the union), summed over the rank's rows into grad_out[Lp + 4] (last
+ * quad: loss partials).  All-reduce grad_out (SUM) over the ranks before prl_ppo_adam_step. */
+int prl_ppo_grad_step(const float* img_params, int32_t D, int32_t A, int32_t discrete,
+                      const float* S, const float* actions, const float* old_logp,
+                      const float* adv, const float* ret, int64_t N, int32_t mini_batch,
+                      int64_t minibatch_index, float inv_count, float clip, float vf_coef,
+                      float* grad_out, void* workspace, int64_t workspace_bytes, void* stream);
+/* clip_grad_norm_(max_norm) + AdamW step number `step` (1-based) on the images from the
+ * all-reduced gradient; loss_out (device f32, may be NULL) = that step's loss. */
+int prl_ppo_adam_step(float* img_params, float* img_m, float* img_v, int32_t D, int32_t A,
+                      int32_t discrete, const float* grad, int64_t step, float lr, float beta1,
+                      float beta2, float eps, float weight_decay, float max_norm, float inv_count,
+                      float vf_coef, float ent_coef, float* loss_out, void* stream);
+/* Host call: device address of the u32 status words inside an engine workspace ([0] last
+ * launch, [1] sticky timeout flag). */
 int prl_ppo_update_status_ptr(void* workspace, uint32_t** status);
 
 #ifdef __cplusplus

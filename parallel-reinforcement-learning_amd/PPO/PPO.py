@@ -109,6 +109,7 @@ class PPO:
         self.last_loss = None
         self._ops = prl_native              # HIP entry points (tests may substitute a fake)
         self.use_fused = True               # whole update loop in one persistent HIP kernel
+        self.use_fused_dp = True            # world > 1: stepped engine + all-reduce per step
         self.use_graphs = True              # else: replay one captured optimizer step per minibatch
         self.graph_min_steps = 16           # below this many graphable steps, stay eager
         self._flat_grad = None
@@ -217,7 +218,9 @@ class PPO:
         return ret
 
     def _fused_path(self, world):
-        return world == 1 and self.use_fused and self.device.type == "cuda"
+        """The fused engine runs the update (one persistent launch on one GPU; stepped, with an
+        all-reduce per optimizer step, on several)."""
+        return self.use_fused and self.device.type == "cuda" and (world == 1 or self.use_fused_dp)
 
     @torch.no_grad()
     def _evaluate_old(self, S, A, world=1):
@@ -294,9 +297,14 @@ class PPO:
         if self._fused_path(world) and S.is_cuda:
             eng = self._fused_engine()
             if eng is not None:
-                self.last_loss = eng.run(S, A, old_logp, adv, returns, self.k_epochs).clone()
+                if world == 1:
+                    self.last_loss = eng.run(S, A, old_logp, adv, returns, self.k_epochs).clone()
+                    self.last_update_path = "fused"
+                else:
+                    self.last_loss = eng.run_stepped(S, A, old_logp, adv, returns, self.k_epochs,
+                                                     n_ranks, self.all_reduce).clone()
+                    self.last_update_path = "fused-dp"
                 self.last_graph_replays = 0
-                self.last_update_path = "fused"
                 return
         self.last_update_path = "graph" if self.use_graphs else "eager"
         nb = max(-(-n // mb) for n in n_ranks)

@@ -125,8 +125,68 @@ class FusedUpdate:
             self.ppo.value_coef, self.ppo.entropy_coef, group["lr"], beta1, beta2, group["eps"],
             group["weight_decay"], 2.0, self.loss, self.ws)
         self._sync_optimizer_state()
-        status = int(prl_native.ppo_update_status(self.ws).item())
+        status = max(prl_native.ppo_update_status(self.ws).tolist())
         if status != 0:
             raise RuntimeError(f"prl_ppo_update: in-kernel timeout (status {status}); the policy "
                                "parameters are undefined")
+        return self.loss.reshape(())
+
+    # ------------------------------------------------------------------ stepped (world_size > 1)
+    def run_stepped(self, S, A, old_logp, adv, ret, k_epochs: int, n_ranks, all_reduce):
+        """The same update loop for data-parallel ranks: per optimizer step, prl_ppo_grad_step
+        (this rank's slice of the union minibatch j, scaled by 1 / union rows) -> all_reduce of
+        the flat gradient (RCCL over xGMI on the GPU node) -> prl_ppo_adam_step.  Parameters and
+        moments stay in the engine's image layout in HBM for the whole loop."""
+        import ctypes
+        if not self.bound():
+            self._bind()
+        group = self.ppo.optimizer.param_groups[0]
+        beta1, beta2 = group["betas"]
+        dev = S.device
+        L = prl_native.ppo_image_floats(self.D, self.A, self.discrete)
+        if getattr(self, "img", None) is None or self.img[0].numel() != L:
+            self.img = [torch.zeros(L, dtype=torch.float32, device=dev) for _ in range(3)]
+            self.grad = torch.zeros(L, dtype=torch.float32, device=dev)
+        img_p, img_m, img_v = self.img
+        prl_native.ppo_image(self.D, self.A, self.discrete, self.flat, self.m, self.v,
+                             img_p, img_m, img_v, True)
+        mb = self.mini_batch
+        nb = max(-(-n // mb) for n in n_ranks)
+        counts = [sum(min(mb, max(0, n - j * mb)) for n in n_ranks) for j in range(nb)]
+        A2 = (A if A.dim() == 2 else A.reshape(-1, 1)).contiguous()
+        tens = [S.contiguous(), A2, old_logp.contiguous(), adv.contiguous(), ret.contiguous()]
+        for x in tens:
+            prl_native._dev(x, torch.float32, "update input")
+        P = ctypes.c_void_p
+        lib = prl_native.lib()
+        stream = P(torch.cuda.current_stream().cuda_stream)
+        grad_fixed = (P(img_p.data_ptr()), self.D, self.A, int(self.discrete)) + tuple(
+            P(x.data_ptr()) for x in tens) + (int(S.shape[0]), mb)
+        grad_tail = (ctypes.c_float(self.ppo.policy_clip), ctypes.c_float(self.ppo.value_coef),
+                     P(self.grad.data_ptr()), P(self.ws.data_ptr()), self.ws.numel(), stream)
+        adam_head = (P(img_p.data_ptr()), P(img_m.data_ptr()), P(img_v.data_ptr()), self.D, self.A,
+                     int(self.discrete), P(self.grad.data_ptr()))
+        adam_mid = tuple(ctypes.c_float(x) for x in (group["lr"], beta1, beta2, group["eps"],
+                                                     group["weight_decay"], 2.0))
+        adam_tail = (ctypes.c_float(self.ppo.value_coef), ctypes.c_float(self.ppo.entropy_coef),
+                     P(self.loss.data_ptr()), stream)
+        step = int(round(float(self.step.item())))
+        for _ in range(k_epochs):
+            for j in range(nb):
+                inv = ctypes.c_float(1.0 / counts[j])
+                rc = lib.prl_ppo_grad_step(*grad_fixed, j, inv, *grad_tail)
+                if rc != 0:
+                    prl_native._check(rc, "prl_ppo_grad_step")
+                all_reduce(self.grad)
+                step += 1
+                rc = lib.prl_ppo_adam_step(*adam_head, step, *adam_mid, inv, *adam_tail)
+                if rc != 0:
+                    prl_native._check(rc, "prl_ppo_adam_step")
+        prl_native.ppo_image(self.D, self.A, self.discrete, self.flat, self.m, self.v,
+                             img_p, img_m, img_v, False)
+        self.step.fill_(float(step))
+        self._sync_optimizer_state()
+        status = max(prl_native.ppo_update_status(self.ws).tolist())
+        if status != 0:
+            raise RuntimeError(f"prl_ppo_grad_step: in-kernel timeout (status {status})")
         return self.loss.reshape(())

@@ -83,7 +83,8 @@ struct UpdArgs {
   float* part;      // [G][Qtot * 4]
   float* red;       // [Qtot * 4]
   float* sq;        // [G]
-  unsigned* ctr;    // [0] arrivals A, [1] arrivals B, [2] abort, [3] status
+  unsigned* ctr;    // [0] arrivals A, [1] arrivals B, [2] abort, [3] status (zeroed per launch),
+                    // [4] sticky timeout flag (never zeroed by a launch)
   unsigned long long* prof;  // [8] workgroup 0's time per phase (100 MHz ticks, summed over steps)
 };
 
@@ -128,6 +129,7 @@ __device__ inline bool upd_wait(unsigned* ctr, int which, unsigned target) {
     if (spins > UPD_SPIN_LIMIT) {
       __hip_atomic_store(ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_or(ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -1038,6 +1040,168 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_evaluate_kernel(UpdArgs ar
   }
 }
 
+// ---- stepped mode (world_size > 1): one optimizer step = grad kernel -> RCCL all-reduce of the
+// flat gradient (caller) -> AdamW kernel.  Parameters and moments live in HBM in the LDS-image
+// layout between launches ("images"); prl_ppo_image converts to / from torch's flat vectors.
+
+// Phase A + B of one step for this rank's rows [row0, row0 + B_local) of global minibatch j:
+// partial gradients per workgroup, then the in-GPU reduction into grad_out[Lp + 4] (the last
+// quad: loss partials {sum -min(s1,s2), sum SmoothL1, sum H}).  inv_count = 1 / (rows of the
+// union minibatch over all ranks), so the all-reduced sum is the union's gradient.
+template <int KD, int KA>
+__global__ __launch_bounds__(UPD_THREADS, 1) void ppo_grad_kernel(UpdArgs args, const float* img,
+                                                                float* grad_out, int64_t row0,
+                                                                int B_local, float inv_count) {
+  extern __shared__ __align__(16) float upd_lds[];
+  const UpdNet& n = args.net;
+  const int t = threadIdx.x, g = blockIdx.x, G = args.G;
+  const int Lp = n.Lp, Qp = Lp / 4, Qtot = Qp + 1;
+  float* hdr = upd_lds;
+  float* W = upd_lds + 64;
+  float* Ga = W + Lp;
+  float* scratch = Ga + Lp + 4;
+  const UpdAct a = upd_carve(scratch, n);
+  float* s_ssq = hdr + 4;
+  int* s_abort = reinterpret_cast<int*>(hdr + 8);
+  unsigned long long* tm = reinterpret_cast<unsigned long long*>(hdr + 16);
+  for (int q = t; q < Qp; q += UPD_THREADS)   // written by the previous launch: plain loads
+    *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(img + 4 * q);
+  for (int k = t; k < Lp + 4; k += UPD_THREADS) Ga[k] = 0.0f;
+  if (t < 24) tm[t] = 0ull;
+  __syncthreads();
+  const int R = args.R;
+  const int myrows = std::max(0, std::min(R, B_local - g * R));
+  for (int c0 = 0; c0 < myrows; c0 += UPD_RC)
+    upd_chunk<KD, KA>(args, W, Ga, a, row0 + (int64_t)g * R + c0, std::min(UPD_RC, myrows - c0),
+                      inv_count, tm);
+  const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(grad_out);
+  for (int q = t; q < Qtot; q += UPD_THREADS)
+    st4_sc1(rs_part, ((size_t)g * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __hip_atomic_fetch_add(args.ctr + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_abort = upd_wait(args.ctr, 0, (unsigned)G) ? 0 : 1;
+  }
+  __syncthreads();
+  if (*s_abort) return;
+  const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
+  const int nq = qhi - qlo;
+  if (nq > UPD_THREADS / 2) {
+    for (int qi = t; qi < nq; qi += UPD_THREADS) {
+      float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int gg = 0; gg < G; ++gg) {
+        const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      st4_sc1(rs_red, (size_t)(qlo + qi) * 4, acc);
+    }
+  } else if (nq > 0) {
+    int spl = 1;
+    while (spl * 2 * nq <= UPD_THREADS && spl * 2 <= G) spl *= 2;
+    float4* red4 = reinterpret_cast<float4*>(scratch);
+    if (t < spl * nq) {
+      const int qi = t % nq, sub = t / nq;
+      float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int gg = sub; gg < G; gg += spl) {
+        const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      red4[sub * nq + qi] = acc;
+    }
+    __syncthreads();
+    if (t < nq) {
+      float4 acc = red4[t];
+      for (int sub = 1; sub < spl; ++sub) {
+        const float4 v = red4[sub * nq + t];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      st4_sc1(rs_red, (size_t)(qlo + t) * 4, acc);
+    }
+  }
+  (void)s_ssq;
+}
+
+// clip_grad_norm_(max_norm) + AdamW on the images, one parameter quad per thread.  Every
+// workgroup forms the same norm (same order), so no hand-off is needed.
+__global__ __launch_bounds__(UPD_THREADS) void ppo_adam_kernel(int Lp, float* img_p, float* img_m,
+                                                             float* img_v, const float* grad,
+                                                             double tstep, float lr, float beta1,
+                                                             float beta2, float eps, float wd,
+                                                             float max_norm, float inv_count,
+                                                             float vf_coef, float ent_coef,
+                                                             float* loss_out) {
+  __shared__ float s_part[UPD_THREADS / 64];
+  const int t = threadIdx.x, Qp = Lp / 4;
+  float acc = 0.f;
+  for (int q = t; q < Qp; q += UPD_THREADS) {
+    const float4 r = *reinterpret_cast<const float4*>(grad + 4 * q);
+    acc += r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w;
+  }
+  acc = wave_sum(acc);
+  if ((t & 63) == 0) s_part[t >> 6] = acc;
+  __syncthreads();
+  float tot = 0.f;
+  for (int w = 0; w < UPD_THREADS / 64; ++w) tot += s_part[w];
+  const float coef = max_norm / (sqrtf(tot) + 1e-6f);
+  const float clipc = coef < 1.0f ? coef : 1.0f;
+  const double bc1 = 1.0 - pow((double)beta1, tstep);
+  const double bc2 = 1.0 - pow((double)beta2, tstep);
+  const float step_size = (float)((double)lr / bc1);
+  const float inv_bc2_sqrt = (float)(1.0 / sqrt(bc2));
+  const float decay = (float)(1.0 - (double)lr * (double)wd);
+  const float omb1 = (float)(1.0 - (double)beta1), omb2 = (float)(1.0 - (double)beta2);
+  const int q = blockIdx.x * UPD_THREADS + t;
+  if (q < Qp) {
+    const float4 g4 = *reinterpret_cast<const float4*>(grad + 4 * q);
+    float4 m4 = *reinterpret_cast<const float4*>(img_m + 4 * q);
+    float4 v4 = *reinterpret_cast<const float4*>(img_v + 4 * q);
+    float4 pw = *reinterpret_cast<const float4*>(img_p + 4 * q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gr = f4get(g4, e) * clipc;
+      float m = f4get(m4, e), v = f4get(v4, e), p = f4get(pw, e);
+      p = p * decay;
+      m = m + omb1 * (gr - m);
+      v = v * beta2 + omb2 * gr * gr;
+      const float denom = __builtin_amdgcn_sqrtf(v) * inv_bc2_sqrt + eps;
+      float rq = __builtin_amdgcn_rcpf(denom);
+      rq = rq * (2.0f - denom * rq);
+      p = p - step_size * (m * rq);
+      f4set(m4, e, m);
+      f4set(v4, e, v);
+      f4set(pw, e, p);
+    }
+    *reinterpret_cast<float4*>(img_m + 4 * q) = m4;
+    *reinterpret_cast<float4*>(img_v + 4 * q) = v4;
+    *reinterpret_cast<float4*>(img_p + 4 * q) = pw;
+  }
+  if (blockIdx.x == 0 && t == 0 && loss_out) {
+    const float4 lp = *reinterpret_cast<const float4*>(grad + Lp);
+    loss_out[0] = lp.x * inv_count + vf_coef * (lp.y * inv_count) - ent_coef * (lp.z * inv_count);
+  }
+}
+
+// torch flat vectors <-> images (to_image: flat -> image, else image -> flat)
+__global__ __launch_bounds__(UPD_THREADS) void ppo_image_kernel(UpdNet n, float* fp, float* fm,
+                                                              float* fv, float* ip, float* im,
+                                                              float* iv, int to_image) {
+  const int k = blockIdx.x * UPD_THREADS + threadIdx.x;
+  if (k >= n.Lp) return;
+  const int f = upd_flat_of(n, k);
+  if (to_image) {
+    ip[k] = f >= 0 ? fp[f] : 0.0f;
+    im[k] = f >= 0 ? fm[f] : 0.0f;
+    iv[k] = f >= 0 ? fv[f] : 0.0f;
+  } else if (f >= 0) {
+    fp[f] = ip[k];
+    fm[f] = im[k];
+    fv[f] = iv[k];
+  }
+}
+
 }  // namespace prl
 
 using namespace prl;
@@ -1092,6 +1256,11 @@ const void* upd_kernel_for(const UpdNet& n) {
   if (!n.discrete && n.A == 1 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1>);
   if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0>);
   return nullptr;
+}
+const void* upd_grad_kernel_for(const UpdNet& n) {
+  if (n.discrete && n.A == 2) return reinterpret_cast<const void*>(ppo_grad_kernel<1, 2>);
+  if (!n.discrete && n.A == 1) return reinterpret_cast<const void*>(ppo_grad_kernel<0, 1>);
+  return reinterpret_cast<const void*>(ppo_grad_kernel<-1, 0>);
 }
 const void* upd_eval_kernel_for(const UpdNet& n) {
   if (n.discrete && n.A == 2) return reinterpret_cast<const void*>(ppo_evaluate_kernel<1, 2>);
@@ -1235,6 +1404,87 @@ extern "C" int prl_ppo_evaluate(const float* params, int32_t D, int32_t A, int32
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   void* kargs[] = {&args, &logp, &V, &entropy};
   PRL_HIP_TRY(hipLaunchKernel(kern, dim3(grid), dim3(UPD_THREADS), kargs, lds, as_stream(stream)));
+  return PRL_OK;
+}
+
+extern "C" int64_t prl_ppo_image_floats(int32_t D, int32_t A, int32_t discrete) {
+  UpdNet n;
+  if (!upd_layout(D, A, discrete, n)) return -1;
+  return (int64_t)n.Lp + 4;
+}
+
+extern "C" int prl_ppo_image(int32_t D, int32_t A, int32_t discrete, float* params, float* exp_avg,
+                             float* exp_avg_sq, float* img_params, float* img_m, float* img_v,
+                             int32_t to_image, void* stream) {
+  UpdNet n;
+  PRL_REQUIRE(upd_layout(D, A, discrete, n), "prl_ppo_image: D=%d A=%d not supported", D, A);
+  PRL_REQUIRE(params && exp_avg && exp_avg_sq && img_params && img_m && img_v,
+              "prl_ppo_image: null pointer");
+  hipLaunchKernelGGL(ppo_image_kernel, dim3((unsigned)cdiv(n.Lp, UPD_THREADS)), dim3(UPD_THREADS),
+                     0, as_stream(stream), n, params, exp_avg, exp_avg_sq, img_params, img_m, img_v,
+                     to_image ? 1 : 0);
+  PRL_LAUNCH_CHECK("ppo_image");
+  return PRL_OK;
+}
+
+extern "C" int prl_ppo_grad_step(const float* img_params, int32_t D, int32_t A, int32_t discrete,
+                                 const float* S, const float* actions, const float* old_logp,
+                                 const float* adv, const float* ret, int64_t N, int32_t mini_batch,
+                                 int64_t minibatch_index, float inv_count, float clip,
+                                 float vf_coef, float* grad_out, void* workspace,
+                                 int64_t workspace_bytes, void* stream) {
+  UpdArgs args{};
+  PRL_REQUIRE(upd_layout(D, A, discrete, args.net), "prl_ppo_grad_step: D=%d A=%d not supported", D, A);
+  PRL_REQUIRE(N >= 0 && mini_batch > 0 && minibatch_index >= 0, "prl_ppo_grad_step: bad sizes");
+  PRL_REQUIRE(img_params && grad_out && workspace, "prl_ppo_grad_step: null pointer");
+  const int G = upd_grid(mini_batch);
+  UpdWs ws;
+  const size_t need = upd_ws_carve(args.net, G, reinterpret_cast<char*>(workspace), &ws);
+  PRL_REQUIRE((size_t)workspace_bytes >= need, "prl_ppo_grad_step: workspace too small");
+  const int64_t row0 = minibatch_index * (int64_t)mini_batch;
+  const int B_local = (int)std::max<int64_t>(0, std::min<int64_t>(mini_batch, N - row0));
+  PRL_REQUIRE(B_local == 0 || (S && actions && old_logp && adv && ret), "prl_ppo_grad_step: null input");
+  args.S = S;
+  args.act = actions;
+  args.old_logp = old_logp;
+  args.adv = adv;
+  args.ret = ret;
+  args.N = N;
+  args.mb = mini_batch;
+  args.G = G;
+  args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RC) * UPD_RC;
+  args.clip = clip;
+  args.vf_coef = vf_coef;
+  args.part = ws.part;
+  args.ctr = ws.ctr;
+  const size_t lds = upd_lds_bytes(args.net);
+  hipStream_t st = as_stream(stream);
+  const void* kern = upd_grad_kernel_for(args.net);
+  PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
+  float inv = inv_count;
+  int64_t r0 = row0;
+  int bl = B_local;
+  const float* img = img_params;
+  void* kargs[] = {&args, &img, &grad_out, &r0, &bl, &inv};
+  // plain launch: G <= 256 workgroups of 1 per CU are co-resident in practice; the in-kernel
+  // wait is bounded and reports a timeout through the status word like the persistent kernel
+  PRL_HIP_TRY(hipLaunchKernel(kern, dim3(G), dim3(UPD_THREADS), kargs, lds, st));
+  return PRL_OK;
+}
+
+extern "C" int prl_ppo_adam_step(float* img_params, float* img_m, float* img_v, int32_t D,
+                                 int32_t A, int32_t discrete, const float* grad, int64_t step,
+                                 float lr, float beta1, float beta2, float eps, float weight_decay,
+                                 float max_norm, float inv_count, float vf_coef, float ent_coef,
+                                 float* loss_out, void* stream) {
+  UpdNet n;
+  PRL_REQUIRE(upd_layout(D, A, discrete, n), "prl_ppo_adam_step: D=%d A=%d not supported", D, A);
+  PRL_REQUIRE(img_params && img_m && img_v && grad && step >= 1, "prl_ppo_adam_step: bad arguments");
+  hipLaunchKernelGGL(ppo_adam_kernel, dim3((unsigned)cdiv(n.Lp / 4, UPD_THREADS)), dim3(UPD_THREADS),
+                     0, as_stream(stream), n.Lp, img_params, img_m, img_v, grad, (double)step, lr,
+                     beta1, beta2, eps, weight_decay, max_norm, inv_count, vf_coef, ent_coef, loss_out);
+  PRL_LAUNCH_CHECK("ppo_adam_step");
   return PRL_OK;
 }
 

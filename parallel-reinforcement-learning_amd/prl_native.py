@@ -55,8 +55,14 @@ SIGNATURES = {
                       + [_F32] * 9 + [_P, _P, _I64, _P],
     "prl_ppo_update_status_ptr": [_P, _P],
     "prl_ppo_evaluate": [_P, _I32, _I32, _I32, _P, _P, _I64, _P, _P, _P, _P],
+    "prl_ppo_image_floats": [_I32, _I32, _I32],
+    "prl_ppo_image": [_I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32, _P],
+    "prl_ppo_grad_step": [_P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I64, _F32, _F32,
+                          _F32, _P, _P, _I64, _P],
+    "prl_ppo_adam_step": [_P, _P, _P, _I32, _I32, _I32, _P, _I64] + [_F32] * 9 + [_P, _P],
 }
-_RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64}
+_RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64,
+             "prl_ppo_image_floats": _I64}
 
 _lib = None
 _lock = threading.Lock()
@@ -399,11 +405,26 @@ def ppo_update(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, action
 
 
 def ppo_update_status(workspace) -> torch.Tensor:
-    """Device u32 view of the engine's status word (0 ok, 1 in-kernel timeout)."""
+    """Device i32 view of the engine's status words: [0] last launch (0 ok, 1 in-kernel timeout),
+    [1] sticky timeout flag over all launches on this workspace."""
     ptr = ctypes.c_void_p()
     _check(lib().prl_ppo_update_status_ptr(_dev(workspace, torch.uint8, "workspace"),
                                            ctypes.byref(ptr)), "prl_ppo_update_status_ptr")
-    return workspace[12:16].view(torch.int32)
+    return workspace[12:20].view(torch.int32)
+
+
+def ppo_image_floats(D, A, discrete) -> int:
+    return int(lib().prl_ppo_image_floats(int(D), int(A), int(bool(discrete))))
+
+
+def ppo_image(D, A, discrete, params, exp_avg, exp_avg_sq, img_p, img_m, img_v, to_image):
+    _check(lib().prl_ppo_image(int(D), int(A), int(bool(discrete)),
+                               _dev(params, torch.float32, "params"),
+                               _dev(exp_avg, torch.float32, "exp_avg"),
+                               _dev(exp_avg_sq, torch.float32, "exp_avg_sq"),
+                               _dev(img_p, torch.float32, "img_p"), _dev(img_m, torch.float32, "img_m"),
+                               _dev(img_v, torch.float32, "img_v"), int(bool(to_image)), _stream()),
+           "prl_ppo_image")
 
 
 def ppo_evaluate(params, D, A, discrete, S, actions, logp, V, entropy=None):

@@ -28,7 +28,7 @@ def _make_ppo(mb, k):
     return p
 
 
-def _worker(rank, world, port, mb, nb, k, out_dir):
+def _worker(rank, world, port, mb, nb, k, out_dir, fused):
     sys.path[:0] = PATHS
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
@@ -36,32 +36,54 @@ def _worker(rank, world, port, mb, nb, k, out_dir):
         torch.cuda.set_device(0)
         torch.manual_seed(1234 + rank)
         p = _make_ppo(mb, k)
+        p.use_fused = fused
         S, A, R, D = _shard(rank, mb, nb)
         p.memory.push_device(*(torch.from_numpy(x).cuda() for x in (S, A, R, D)))
         p.learn()
         torch.cuda.synchronize()
         sd = {kk: v.cpu().numpy() for kk, v in p.policy.state_dict().items()}
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **sd,
-                 _replays=np.int64(p.last_graph_replays))
+                 _replays=np.int64(p.last_graph_replays),
+                 _path=np.array(p.last_update_path))
     finally:
         torch.distributed.destroy_process_group()
 
 
-def test_two_ranks_graphed_equal_one_process_on_the_union(tmp_path):
+@pytest.mark.parametrize("fused", [True, False])
+def test_two_ranks_graphed_equal_one_process_on_the_union(tmp_path, fused):
+    """fused: the stepped engine (grad kernel -> all-reduce -> AdamW kernel per step) on both
+    ranks vs one process running the persistent engine on the union (function space, since the
+    gradient sums differ in order); graph: per-step graphs on both sides (weights, 2e-5)."""
     mb, nb, k = 64, 5, 4
-    mp.spawn(_worker, args=(2, 29547, mb, nb, k, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, 29547 + int(fused), mb, nb, k, str(tmp_path), fused), nprocs=2,
+             join=True)
     outs = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(2)]
-    assert int(outs[0]["_replays"]) == k * nb - 2       # all but the 2 warm-up steps
+    assert str(outs[0]["_path"]) == ("fused-dp" if fused else "graph")
+    if not fused:
+        assert int(outs[0]["_replays"]) == k * nb - 2       # all but the 2 warm-up steps
     shards = [_shard(r, mb, nb) for r in range(2)]
     cols = [np.concatenate([shards[r][c][j * mb:(j + 1) * mb] for j in range(nb) for r in range(2)])
             for c in range(4)]
     torch.manual_seed(1234)
     p = _make_ppo(2 * mb, k)
-    p.use_fused = False        # world 1 would take the fused engine; compare graph with graph
+    p.use_fused = fused
     p.memory.push_device(*(torch.from_numpy(x).cuda() for x in cols))
     p.learn()
-    assert p.last_graph_replays == k * nb - 2
     ref = {kk: v.cpu().numpy() for kk, v in p.policy.state_dict().items()}
     for key in ref:
-        np.testing.assert_array_equal(outs[0][key], outs[1][key])
+        if not key.startswith("_"):
+            np.testing.assert_array_equal(outs[0][key], outs[1][key])
+    if fused:
+        import copy
+        import types
+        q = types.SimpleNamespace(policy=copy.deepcopy(p.policy))
+        q.policy.load_state_dict({kk: torch.from_numpy(outs[0][kk]) for kk in ref})
+        S = torch.from_numpy(np.concatenate([cols[0][:256]])).cuda()
+        A = torch.from_numpy(np.concatenate([cols[1][:256]])).cuda()
+        from test_engine_gpu import _outputs
+        (l1, v1), (l2, v2) = _outputs(q, S, A), _outputs(p, S, A)
+        assert float((l1 - l2).abs().max()) <= 1e-4 and float((v1 - v2).abs().max()) <= 1e-4
+        return
+    assert p.last_graph_replays == k * nb - 2
+    for key in ref:
         np.testing.assert_allclose(outs[0][key], ref[key], rtol=0, atol=2e-5, err_msg=key)

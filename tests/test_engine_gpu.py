@@ -267,3 +267,37 @@ def test_engine_evaluate_matches_get_evaluate(cont):
     l64, v64 = _outputs(p, S, Aa)
     torch.testing.assert_close(logp.double().cpu(), l64, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(V.double().cpu(), v64, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("cont", [False, True])
+def test_stepped_engine_matches_persistent(cont):
+    """The stepped engine (world_size > 1 path: grad kernel -> all-reduce -> AdamW kernel per
+    step) with an identity all-reduce equals the persistent kernel up to float32 summation
+    order (the gradient norm is summed in a different order)."""
+    N = 4000 + 11
+    data = _data(N, 3 if cont else 4, cont, seed=17)
+    kw = dict(clip=1e3, lr=3e-4) if cont else dict(clip=10.0)
+    pf = _run(True, cont, data, 512, 2, **kw)
+    from PPO import PPO
+    torch.manual_seed(0)
+    D, A = (3, 1) if cont else (4, 2)
+    ps = PPO(cont, D, A, action_scaling=2.0 if cont else None, lr=kw.get("lr", 1e-3), k_epochs=2,
+             batch_size=64, mini_batch_size=512, policy_clip=kw["clip"])
+    ps.show_progress = False
+    ps.memory.push_device(*data)
+    # drive learn()'s stepped branch with a one-rank "all-reduce"
+    ps._world = staticmethod(lambda: 1)
+    orig = ps._update
+
+    def stepped_update(S, A_, old, adv, ret, n_ranks):
+        eng = ps._fused_engine()
+        ps._last_update_inputs = (S, A_, old, adv, ret)
+        ps.last_loss = eng.run_stepped(S, A_, old, adv, ret, ps.k_epochs, n_ranks, lambda t: t)
+        ps.last_update_path = "fused-dp"
+    ps._update = stepped_update
+    ps.learn()
+    ps._update = orig
+    _compare_function(pf, ps, data, rtol=1e-3 if cont else 1e-4)
+    assert float(ps.optimizer.state[next(ps.policy.parameters())]["step"]) == 2 * 8
+    if not cont:
+        _compare(pf, ps)

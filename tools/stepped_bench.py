@@ -1,0 +1,43 @@
+"""Per-step cost of the data-parallel (stepped) engine on one GPU: grad kernel -> all-reduce ->
+AdamW kernel per optimizer step on the C2 learn workload (2^20 synthetic CartPole transitions),
+with (a) no collective, (b) a one-rank RCCL all_reduce through torch.distributed — the host
+and launch overhead the N > 1 runs pay on top of the collective's own latency."""
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "parallel-reinforcement-learning_amd"), os.path.join(ROOT, "tools")]
+from learn_bench import synthetic_batch  # noqa: E402
+from PPO import PPO  # noqa: E402
+
+os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+os.environ.setdefault("MASTER_PORT", "29611")
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+N, mb, k = 1 << 20, 512, 11
+batch = synthetic_batch(N)
+for label, ar in (("identity", lambda t: t), ("rccl-1rank", dist.all_reduce)):
+    torch.manual_seed(0)
+    p = PPO(False, 4, 2, lr=1e-3, k_epochs=k, batch_size=1, mini_batch_size=mb)
+    p.show_progress = False
+    p.memory.push_device(*batch)
+    S, A, R, Dn = p.memory.device_tensors(p.device)
+    old, V = p._evaluate_old(S, A)
+    adv = torch.randn_like(V)
+    ret = torch.randn_like(V)
+    eng = p._fused_engine()
+    eng.run_stepped(S[:8192], A[:8192], old[:8192], adv[:8192], ret[:8192], 1, [8192], ar)  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.run_stepped(S, A, old, adv, ret, k, [N], ar)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    steps = k * -(-N // mb)
+    print(json.dumps({"all_reduce": label, "learn_update_ms_per_1M": round(dt * 1e3, 1),
+                      "us_per_step": round(dt / steps * 1e6, 2)}), flush=True)
+dist.destroy_process_group()
