@@ -61,15 +61,17 @@ class LastCall:
 
 def time_kernel(launch, reps=10, cold=True):
     """Average device time of one launch, with HIP events on the launching stream.  The GPU is
-    kept busy (a 512 MiB cache-flushing fill when cold, else a spin kernel) while the host
-    enqueues start-event / launch / end-event, so no host overhead lands between the events;
-    cold=True also evicts the 256 MiB Infinity Cache, so inputs come from HBM."""
-    flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda") if cold else None
+    kept busy (a spin kernel) while the host enqueues start-event / launch / end-event, so no
+    host overhead lands between the events.  cold=True first READS a 512 MiB buffer, which evicts
+    the 256 MiB Infinity Cache and the L2s so inputs come from HBM; a read leaves the caches
+    clean (a write-based flush leaves them full of dirty lines whose write-back would then
+    compete with the timed kernel)."""
+    flush = torch.ones(128 << 20, dtype=torch.float32, device="cuda") if cold else None
     launch()
     ms = []
     for _ in range(reps):
         if cold:
-            flush.fill_(1)
+            flush.sum()
         torch.cuda._sleep(2_000_000)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
@@ -106,6 +108,9 @@ def main():
     ap.add_argument("--k-epochs", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-envs", type=int, default=8192)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL on ROCm, the measured configuration) or gloo (rehearsal of "
+                         "the multi-rank path with several ranks on one GPU)")
     ap.add_argument("--dump-gae", default=None,
                     help="save the roofline GAE launch's inputs (torch.save) for PMC passes")
     args = ap.parse_args()
@@ -113,9 +118,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    dev_index = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from AsyncTools.AsyncPPO import AsyncPPO
     from AsyncTools.envs import make
@@ -174,7 +183,8 @@ def main():
     learn_t = float(sum(r[2] for r in recs))
     vec_steps = float(np.mean([r[3] for r in recs]))
     stats = torch.tensor([elapsed, n_local, roll_t, learn_t, learn_t / max(n_local, 1)],
-                         dtype=torch.float64, device="cuda")
+                         dtype=torch.float64,
+                         device="cuda" if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -201,7 +211,7 @@ def main():
                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "traffic_source": traffic_src,
-                    "avg_launch_us": round(cold_med * 1e3, 2), "cache": "cold (512 MiB flush)",
+                    "avg_launch_us": round(cold_med * 1e3, 2), "cache": "cold (512 MiB read-only flush)",
                     "warm_launch_us": round(warm_med * 1e3, 2),
                     "warm_achieved": round(GAE_BYTES_PER_TRANSITION * n_gae / (warm_med * 1e-3)
                                            / 1e9, 1),

@@ -274,6 +274,24 @@ __device__ inline int64_t block_inclusive_scan_256(int64_t v, int64_t* lds_wave_
   return v + prefix;
 }
 
+// Sum of a double over the 64 lanes of a wave by DPP (no LDS round trips), result in lane 63:
+// xor-1 / xor-2 quad perms, half-row and row mirrors, then row_bcast:15 / row_bcast:31 (GFX9 DPP).
+template <int CTRL, int ROWS>
+__device__ inline double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWS, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ inline double wave_sum_f64_to63(double v) {
+  v += dpp_f64<0xB1, 0xF>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E, 0xF>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141, 0xF>(v);   // row_half_mirror
+  v += dpp_f64<0x140, 0xF>(v);   // row_mirror: every lane holds its row's sum
+  v += dpp_f64<0x142, 0xA>(v);   // row_bcast:15 -> rows 1, 3
+  v += dpp_f64<0x143, 0xC>(v);   // row_bcast:31 -> rows 2, 3
+  return v;                      // lane 63: the wave's sum
+}
+
 template <typename T>
 __device__ inline T wave_sum(T v) {
 #pragma unroll

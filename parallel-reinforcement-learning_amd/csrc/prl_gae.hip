@@ -45,6 +45,12 @@
 
 namespace prl {
 
+// Phase marks for tools/exp/gae_phases.hip (which defines PRL_GAE_MARK before including this
+// file); empty in the product build.
+#ifndef PRL_GAE_MARK
+#define PRL_GAE_MARK(i)
+#endif
+
 constexpr int GAE_THREADS = 256;
 constexpr int GAE_EPT = 8;
 constexpr int GAE_TILE = GAE_THREADS * GAE_EPT;
@@ -119,14 +125,26 @@ __device__ inline float gae_delta(float r, float d, float v, float nv, float gf)
   return s - v;
 }
 
-__device__ inline float chunk_chain(const float* s_delta, const float* s_c, int chunk, float carry) {
-  const float* dl = s_delta + chunk * GAE_EPT;
-  const float* cc = s_c + chunk * GAE_EPT;
-#pragma unroll
-  for (int k = GAE_EPT - 1; k >= 0; --k) carry = dl[k] + cc[k] * carry;
+struct ChunkDC {
+  float4 da, db, ca, cb;
+};
+__device__ inline ChunkDC chunk_load(const float* s_delta, const float* s_c, int chunk) {
+  const float4* d4 = reinterpret_cast<const float4*>(s_delta + chunk * GAE_EPT);
+  const float4* c4 = reinterpret_cast<const float4*>(s_c + chunk * GAE_EPT);
+  return ChunkDC{d4[0], d4[1], c4[0], c4[1]};
+}
+// the reference's recurrence over one 8-element chunk, last element first
+__device__ inline float chunk_apply(const ChunkDC& x, float carry) {
+  carry = x.db.w + x.cb.w * carry;
+  carry = x.db.z + x.cb.z * carry;
+  carry = x.db.y + x.cb.y * carry;
+  carry = x.db.x + x.cb.x * carry;
+  carry = x.da.w + x.ca.w * carry;
+  carry = x.da.z + x.ca.z * carry;
+  carry = x.da.y + x.ca.y * carry;
+  carry = x.da.x + x.ca.x * carry;
   return carry;
 }
-
 // g at index `start` computed from global memory: walk forward to the first break (c == 0) or
 // the end, then run the chain backward in the reference's order.  Used only when a successor's
 // granule did not show up in time; bit-identical to the granule path.
@@ -220,15 +238,14 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
   __shared__ __attribute__((aligned(16))) float s_delta[GAE_TILE];
   __shared__ __attribute__((aligned(16))) float s_c[GAE_TILE];
   __shared__ float s_out[GAE_THREADS];
-  __shared__ unsigned char s_hb[GAE_THREADS];
+  __shared__ unsigned long long s_mask[GAE_THREADS / 64];
+  __shared__ float s_cin[GAE_THREADS];
   __shared__ unsigned s_tag;
-  __shared__ int s_need;
-  __shared__ float s_carry;
 
   const int tid = threadIdx.x;
+  PRL_GAE_MARK(0);
   if (tid == 0) {
     s_tag = gae_tag(ws);
-    s_need = 0;
   }
   const int64_t tile = ntiles - 1 - (int64_t)blockIdx.x;
   const int64_t i0 = tile * GAE_TILE + (int64_t)tid * GAE_EPT;
@@ -253,6 +270,7 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
       vv[k] = in ? V[i] : 0.f;
     }
   }
+  PRL_GAE_MARK(1);
   // nv for the final element (PPO.py:188: next_value = V[-1]) and for this chunk's last element
   const float nv_end = next_value ? *next_value : V[n - 1];
   const int64_t inext = i0 + GAE_EPT;
@@ -291,76 +309,100 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
       }
     }
   }
-  s_hb[tid] = (pb >= 0) ? 1 : 0;
   s_out[tid] = (pb >= 0) ? g[0] : 0.0f;
-  __syncthreads();
-  const unsigned tag = s_tag;
-
-  // tail: resolve from the nearest chunk to the right that has a break
-  bool resolved = (pb == GAE_EPT - 1);
-  bool need_tile = false;
-  if (!resolved) {
-    int kk = tid + 1;
-    while (kk < GAE_THREADS && !s_hb[kk]) ++kk;
-    if (kk < GAE_THREADS) {
-      float carry = s_out[kk];
-      for (int m = kk - 1; m > tid; --m) carry = chunk_chain(s_delta, s_c, m, carry);
-#pragma unroll
-      for (int k = GAE_EPT - 1; k >= 0; --k) {
-        if (k > pb) {
-          carry = dl[k] + cc[k] * carry;
-          g[k] = carry;
-        }
-      }
-      resolved = true;
-    } else {
-      need_tile = true;
-      s_need = 1;
-    }
+  {
+    const unsigned long long bal = __ballot(pb >= 0);   // chunks of this wave with a break
+    if ((tid & 63) == 0) s_mask[tid >> 6] = bal;
   }
-  if (tid == 0 && resolved)
-    st_sc1(&ws.gran[tile], ((unsigned long long)tag << 32) | __float_as_uint(g[0]));
   __syncthreads();
+  PRL_GAE_MARK(2);
+  const unsigned tag = s_tag;
+  const bool hb = pb >= 0;
+  auto publish = [&](float carry_out) {   // g at the tile's first element -> predecessor tile
+    st_sc1(&ws.gran[tile], ((unsigned long long)tag << 32) | __float_as_uint(carry_out));
+  };
+  // chunk 0 with a break: the tile's carry-out is local — publish before anything else
+  if (tid == 0 && hb) publish(g[0]);
 
-  if (s_need) {
-    if (tid == 0) {
-      float cin = 0.0f;  // beyond the last element: gae = 0 (PPO.py:110)
-      if (tile + 1 < ntiles) {
-        unsigned spins = 0;
-        bool got = false;
-        for (;;) {
-          const unsigned long long w = ld_sc1(&ws.gran[tile + 1]);
-          if ((unsigned)(w >> 32) == tag) {
-            cin = __uint_as_float((unsigned)(w & 0xffffffffull));
-            got = true;
+  // Carries between chunks, each chained ONCE: the thread of every chunk with a break owns the
+  // run of break-free chunks to its left (down to, and including as a carry target, the previous
+  // chunk with a break) and walks it right to left, writing each chunk's carry-in (g at the
+  // first element of the chunk to its right).  Thread 255 owns the run at the tile's end, which
+  // starts from the successor tile's carry.  Same recurrence order as the reference throughout.
+  const int lane = tid & 63, wv = tid >> 6;
+  if (hb) {
+    int p = -1;   // previous chunk with a break
+    {
+      const unsigned long long below = lane == 0 ? 0ull : (s_mask[wv] << (64 - lane));
+      if (below) {
+        p = tid - 1 - __builtin_clzll(below);
+      } else {
+        for (int w2 = wv - 1; w2 >= 0; --w2) {
+          const unsigned long long mk = s_mask[w2];
+          if (mk) {
+            p = w2 * 64 + 63 - __builtin_clzll(mk);
             break;
           }
-          if (++spins >= GAE_SPIN_LIMIT) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (!got) {
-          cin = gae_lookahead(r, d, V, nv_end, n, gf, glf, (tile + 1) * (int64_t)GAE_TILE);
-          __hip_atomic_fetch_add(&ws.ctrs[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-      s_carry = cin;
     }
-    __syncthreads();
-    if (need_tile) {
-      float carry = s_carry;
-      for (int m = GAE_THREADS - 1; m > tid; --m) carry = chunk_chain(s_delta, s_c, m, carry);
-#pragma unroll
-      for (int k = GAE_EPT - 1; k >= 0; --k) {
-        if (k > pb) {
-          carry = dl[k] + cc[k] * carry;
-          g[k] = carry;
+    float carry = g[0];
+    for (int k = tid - 1; k >= (p < 0 ? 0 : p); --k) {
+      s_cin[k] = carry;
+      if (k > p) carry = chunk_apply(chunk_load(s_delta, s_c, k), carry);
+    }
+    if (p < 0 && tid > 0) publish(carry);   // walked to chunk 0: carry = g(tile start)
+  }
+  if (tid == GAE_THREADS - 1 && pb != GAE_EPT - 1) {
+    float cin = 0.0f;  // beyond the last element: gae = 0 (PPO.py:110)
+    if (tile + 1 < ntiles) {
+      unsigned spins = 0;
+      bool got = false;
+      for (;;) {
+        const unsigned long long w = ld_sc1(&ws.gran[tile + 1]);
+        if ((unsigned)(w >> 32) == tag) {
+          cin = __uint_as_float((unsigned)(w & 0xffffffffull));
+          got = true;
+          break;
         }
+        if (++spins >= GAE_SPIN_LIMIT) break;
+        __builtin_amdgcn_s_sleep(1);
       }
-      if (tid == 0)
-        st_sc1(&ws.gran[tile], ((unsigned long long)tag << 32) | __float_as_uint(g[0]));
+      if (!got) {
+        cin = gae_lookahead(r, d, V, nv_end, n, gf, glf, (tile + 1) * (int64_t)GAE_TILE);
+        __hip_atomic_fetch_add(&ws.ctrs[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    int L = -1;   // last chunk with a break
+    for (int w2 = GAE_THREADS / 64 - 1; w2 >= 0; --w2) {
+      const unsigned long long mk = s_mask[w2];
+      if (mk) {
+        L = w2 * 64 + 63 - __builtin_clzll(mk);
+        break;
+      }
+    }
+    float carry = cin;
+    for (int k = GAE_THREADS - 1; k >= (L < 0 ? 0 : L); --k) {
+      s_cin[k] = carry;
+      if (k > L) carry = chunk_apply(chunk_load(s_delta, s_c, k), carry);
+    }
+    if (L < 0) publish(carry);               // no break in the tile
+  }
+  __syncthreads();
+  PRL_GAE_MARK(3);
+  // every chunk's elements after its last break, from its carry-in
+  if (pb != GAE_EPT - 1) {
+    float carry = s_cin[tid];
+#pragma unroll
+    for (int k = GAE_EPT - 1; k >= 0; --k) {
+      if (k > pb) {
+        carry = dl[k] + cc[k] * carry;
+        g[k] = carry;
+      }
     }
   }
 
+  PRL_GAE_MARK(4);
   // outputs: ret = gae + V (PPO.py:116), adv = ret - V (PPO.py:198)
   float rt[GAE_EPT], av[GAE_EPT];
 #pragma unroll
@@ -386,6 +428,7 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
       }
     }
   }
+  PRL_GAE_MARK(5);
   double2 mine{0.0, 0.0};
   if (adv) {
     double s1 = 0.0, s2 = 0.0;
@@ -407,6 +450,7 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
       for (int w = 0; w < GAE_THREADS / 64; ++w) { mine.x += s_red[0][w]; mine.y += s_red[1][w]; }
   }
   gae_arrive(ws, ntiles, tile, tag, adv != nullptr, mine, sums_out);
+  PRL_GAE_MARK(6);
 }
 
 // Plain statistics pass (prl_adv_stats): per-tile sums + grouped ordered fold.

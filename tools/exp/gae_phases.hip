@@ -1,0 +1,12 @@
+// Experiment (tools/, not product): where a GAE tile's lifetime goes.  Builds the product GAE
+// kernel with PRL_GAE_MARK recording s_memrealtime (100 MHz) per workgroup and phase.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+__device__ unsigned long long* g_gae_prof;
+#define PRL_GAE_MARK(i) \
+  do { if (threadIdx.x == 0) g_gae_prof[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#include "../../parallel-reinforcement-learning_amd/csrc/prl_gae.hip"
+
+extern "C" int gae_prof_set(unsigned long long* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_gae_prof), &buf, sizeof(buf));
+}
