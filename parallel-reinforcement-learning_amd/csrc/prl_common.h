@@ -292,6 +292,21 @@ __device__ inline double wave_sum_f64_to63(double v) {
   return v;                      // lane 63: the wave's sum
 }
 
+// the same DPP tree for a float (result in lane 63)
+template <int CTRL, int ROWS>
+__device__ inline float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xF, false));
+}
+__device__ inline float wave_sum_f32_to63(float v) {
+  v += dpp_f32<0xB1, 0xF>(v);
+  v += dpp_f32<0x4E, 0xF>(v);
+  v += dpp_f32<0x141, 0xF>(v);
+  v += dpp_f32<0x140, 0xF>(v);
+  v += dpp_f32<0x142, 0xA>(v);
+  v += dpp_f32<0x143, 0xC>(v);
+  return v;
+}
+
 template <typename T>
 __device__ inline T wave_sum(T v) {
 #pragma unroll

@@ -859,7 +859,7 @@ ppo_update_kernel(UpdArgs args) {
         if (t < spl * nq) {
           const int qi = t % nq, sub = t / nq;
           float4 acc = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
+#pragma unroll 16
           for (int gg = sub; gg < G; gg += spl) {
             const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
             acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
@@ -878,8 +878,8 @@ ppo_update_kernel(UpdArgs args) {
         }
       }
       // block sum of ssq (threads < nq hold the pieces; fixed order)
-      ssq = wave_sum(ssq);
-      if ((t & 63) == 0) s_ssq[t >> 6] = ssq;
+      ssq = wave_sum_f32_to63(ssq);
+      if ((t & 63) == 63) s_ssq[t >> 6] = ssq;
       __syncthreads();
       if (t == 0) {
         float tot = 0.f;
@@ -898,10 +898,16 @@ ppo_update_kernel(UpdArgs args) {
       mark(4);   // wait B
     }
     // ---- phase C: clip_grad_norm_(2.0) + AdamW on every workgroup's own copy ------------------
+    float4 gq[NQ];   // this thread's gradient quads: loads issued first, in flight under the norm
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int q = t + i * UPD_THREADS;
+      if (q < Qp) gq[i] = ld4_sc1(rs_red, (size_t)q * 4);
+    }
     {
       float piece = t < G ? ld_sc1f(args.sq + t) : 0.f;     // every workgroup: same tree
-      piece = wave_sum(piece);
-      if ((t & 63) == 0) s_ssq[t >> 6] = piece;
+      piece = wave_sum_f32_to63(piece);
+      if ((t & 63) == 63) s_ssq[t >> 6] = piece;
       __syncthreads();
       if (t == 0) {
         float tot = 0.f;
@@ -926,15 +932,9 @@ ppo_update_kernel(UpdArgs args) {
       const float decay = (float)(1.0 - (double)args.lr * (double)args.wd);
       const float b2 = args.beta2;
       const float omb1 = (float)(1.0 - (double)args.beta1), omb2 = (float)(1.0 - (double)args.beta2);
-      constexpr int BATCH = NQ;  // every gradient load issued ahead of the arithmetic
+      constexpr int BATCH = NQ;
 #pragma unroll
       for (int i0 = 0; i0 < NQ; i0 += BATCH) {
-        float4 gq[BATCH];
-#pragma unroll
-        for (int b = 0; b < BATCH; ++b) {
-          const int q = t + (i0 + b) * UPD_THREADS;
-          if (i0 + b < NQ && q < Qp) gq[b] = ld4_sc1(rs_red, (size_t)q * 4);
-        }
 #pragma unroll
         for (int b = 0; b < BATCH; ++b) {
           const int i = i0 + b;
@@ -944,7 +944,7 @@ ppo_update_kernel(UpdArgs args) {
             float4 m4 = mreg[i], v4 = vreg[i];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float gr = f4get(gq[b], e) * clipc;
+              const float gr = f4get(gq[i], e) * clipc;
               float m = f4get(m4, e), v = f4get(v4, e), p = f4get(pw, e);
               p = p * decay;
               m = m + omb1 * (gr - m);
