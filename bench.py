@@ -5,12 +5,18 @@
 
 A STEP is one full AsyncPPO iteration on synthetic (freshly simulated) data: the device-resident
 worker() rolls one episode per env to termination (fused HIP env/sampling/mask kernel per vector
-step, PyTorch policy MLP), then ppo.learn() runs on that rollout (HIP GAE scan, advantage
-normalisation, surrogate; PyTorch MLP backward + AdamW; k_epochs x sequential minibatches).
+step, PyTorch policy MLP), then ppo.learn() runs on that rollout (HIP policy_old evaluation, HIP
+GAE scan + advantage normalisation, then the whole k_epochs x sequential-minibatch update loop in
+one persistent HIP kernel: forward, surrogate, backward, clip_grad_norm_, AdamW).
 `value` = transitions collected by ALL ranks / wall time of the K timed steps (max over ranks):
 whole-job env-steps/s including learn().  Also reported: rollout-only env-steps/s and learn()
 wall-ms normalised to a 2^20-transition batch.  Multi-GPU (torchrun): one process per GPU over
-RCCL, num_envs per rank fixed (weak scaling), gradients all-reduced every optimizer step.
+RCCL, num_envs per rank fixed (weak scaling), the flat gradient all-reduced every optimizer step
+(stepped engine: gradient kernel -> all-reduce -> AdamW kernel).
+
+Roofline objects: `roofline` = the dominant kernel (the update engine; f32 FLOPs of its Linear
+layers, HIP events around each launch in the timed region), `roofline_gae` = the GAE scan and
+`roofline_env` = the rollout step kernel (algorithmic bytes, re-timed cold after the run).
 """
 import argparse
 import json
@@ -27,6 +33,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "env-steps/sec + PPO.learn() wall-ms per 1M-step batch, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+F32_PEAK_TFLOPS = 157.3  # MI355X FP32 peak, vector = f32-input MFMA (MI355X_MICROARCH.md)
 
 CONFIGS = {
     # BASELINE.json configs[1] (per GPU; configs[3] is the same per-GPU shape on 8 GPUs)
@@ -42,9 +49,10 @@ CONFIGS = {
 
 # algorithmic HBM bytes per unit: GAE = r, d, V in + ret, adv out (f32)
 GAE_BYTES_PER_TRANSITION = 20
-# fused CartPole rollout step per env-step: phys f64 r/w 64, probs 8, t r/w 8, terminal r/w 2,
-# next obs 16, action 4, reward 4, done 1, ep_len 4
-CARTPOLE_STEP_BYTES = 111
+# fused rollout step per active env (prl_envs.hip rollout_step_kernel): terminal r/w 2, t r/w 8,
+# phys f64 r/w, dist row 8 (probs / mu, std), next obs f32 w, action 4, reward 4, done 1, ep_len 4
+ENV_STEP_BYTES = {"CartPole-v1": 2 + 8 + 64 + 8 + 16 + 4 + 4 + 1 + 4,     # 111
+                  "Pendulum-v1": 2 + 8 + 32 + 8 + 12 + 4 + 4 + 1 + 4}     # 75
 
 
 class LastCall:
@@ -59,7 +67,7 @@ class LastCall:
         return self.fn(*a, **k)
 
 
-def time_kernel(launch, reps=10, cold=True):
+def time_kernel(launch, reps=10, cold=True, prep=None):
     """Average device time of one launch, with HIP events on the launching stream.  The GPU is
     kept busy (a spin kernel) while the host enqueues start-event / launch / end-event, so no
     host overhead lands between the events.  cold=True first READS a 512 MiB buffer, which evicts
@@ -70,6 +78,8 @@ def time_kernel(launch, reps=10, cold=True):
     launch()
     ms = []
     for _ in range(reps):
+        if prep is not None:
+            prep()
         if cold:
             flush.sum()
         torch.cuda._sleep(2_000_000)
@@ -167,6 +177,10 @@ def main():
 
     for _ in range(args.warmup):
         iteration()
+    # the update engine's launches inside the timed region, timed with HIP events on its stream
+    eng = ppo._fused_engine() if getattr(ppo, "use_fused", False) else None
+    if eng is not None:
+        eng.events = []
 
     if world > 1:
         dist.barrier()
@@ -196,6 +210,31 @@ def main():
         total_n, roll_max, learn_per_tr = n_local, roll_t, learn_t / max(n_local, 1)
 
     roofline = None
+    if eng is not None and eng.events:
+        torch.cuda.synchronize()
+        kern = eng.events[0][0]
+        ms = [a.elapsed_time(b) for _, a, b, _, _ in eng.events]
+        rows = float(np.mean([r for _, _, _, r, _ in eng.events]))
+        steps_per_launch = float(np.mean([st for _, _, _, _, st in eng.events]))
+        fpr = eng.flops_per_row()
+        avg_ms = float(np.mean(ms))
+        flops = fpr * rows
+        achieved = flops / (avg_ms * 1e-3) / 1e12
+        what = ("persistent fused PPO update: the whole k_epochs x minibatch loop in one launch"
+                if kern == "ppo_update_kernel" else
+                "stepped engine: one minibatch's gradient on this rank per launch")
+        roofline = {"kernel": f"{kern} ({what})",
+                    "bound": "mfma", "achieved": round(achieved, 3), "peak": F32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved / F32_PEAK_TFLOPS, 5),
+                    "traffic": None,
+                    "limiter": "latency: dependent optimizer steps (k_epochs x ceil(N/mb)), "
+                               "each = forward+backward of mb rows + two grid-wide hand-offs",
+                    "avg_launch_ms": round(avg_ms, 4), "launches": len(ms),
+                    "flops_per_launch": flops, "flops_per_row": fpr, "rows_per_launch": rows,
+                    "optimizer_steps_per_launch": steps_per_launch,
+                    "us_per_optimizer_step": round(avg_ms * 1e3 / steps_per_launch, 2),
+                    "dtype": "f32"}
+    roofline_gae = None
     if gae_call.args is not None:
         a, k = gae_call.args
         n_gae = a[2].numel()
@@ -207,7 +246,7 @@ def main():
                         "next_value": None if a[3] is None else a[3].cpu(),
                         "gamma": a[4], "lam": a[5]}, args.dump_gae)
         traffic, traffic_src = pmc_traffic(n_gae)
-        roofline = {"kernel": "prl_gae: gae_kernel<true> (single-pass segmented GAE scan)",
+        roofline_gae = {"kernel": "prl_gae: gae_kernel<true> (single-pass segmented GAE scan)",
                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "traffic_source": traffic_src,
@@ -217,6 +256,33 @@ def main():
                                            / 1e9, 1),
                     "transitions_per_launch": int(n_gae),
                     "bytes_per_transition": GAE_BYTES_PER_TRANSITION}
+
+    roofline_env = None
+    if cfg["env"] in ENV_STEP_BYTES and runner._traj is not None:
+        env, tr, spec_ = runner.env, runner._traj, runner.env.spec
+        E = runner.num_envs
+        env.reset_device(tr.obs[0])
+        dist0 = ppo.dist_params(tr.obs[0]).float().contiguous()
+        scaling = float(getattr(ppo, "action_scaling", None) or 1.0)
+
+        def env_launch():
+            prl_native.rollout_step(spec_.kind, 0, env.phys, env.t_elapsed, env.terminal, dist0,
+                                    scaling, 12345, tr.T, tr.obs, tr.act, tr.rew, tr.done,
+                                    tr.ep_len, tr.active_after, tr.reward_sum)
+
+        # every timed launch steps all E envs from a fresh reset (reset outside the events)
+        env_cold, _ = time_kernel(env_launch, cold=True, prep=lambda: env.reset_device(tr.obs[0]))
+        env_warm, _ = time_kernel(env_launch, cold=False, prep=lambda: env.reset_device(tr.obs[0]))
+        bpe = ENV_STEP_BYTES[cfg["env"]]
+        ach = bpe * E / (env_cold * 1e-3) / 1e9
+        roofline_env = {"kernel": "prl_rollout_step: rollout_step_kernel (fused env step + "
+                                  "action sampling + trajectory append, thread per env)",
+                        "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "avg_launch_us": round(env_cold * 1e3, 2),
+                        "cache": "cold (512 MiB read-only flush)",
+                        "warm_launch_us": round(env_warm * 1e3, 2),
+                        "envs_per_launch": E, "bytes_per_env_step": bpe}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["env"] == "CartPole-v1":
@@ -252,9 +318,13 @@ def main():
             "transitions_per_step": round(total_n / args.steps, 1),
             "vector_steps_per_rollout": vec_steps,
             "roofline": roofline,
+            "roofline_gae": roofline_gae,
+            "roofline_env": roofline_env,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    if eng is not None:
+        eng.events = None     # release the HIP events before interpreter teardown
     if world > 1:
         dist.destroy_process_group()
 

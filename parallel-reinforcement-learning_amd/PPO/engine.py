@@ -36,6 +36,7 @@ class FusedUpdate:
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self.ws = torch.zeros(ws_bytes, dtype=torch.uint8, device=dev)
         self.mini_batch = int(mini_batch)
+        self.events = None       # a list: (kernel, start, end, rows, optimizer steps) per launch
         self._bind()
 
     def _views(self, buf):
@@ -93,6 +94,16 @@ class FusedUpdate:
                                 A2.contiguous(), logp, V)
         return logp, V
 
+    def flops_per_row(self) -> int:
+        """Algorithmic FLOPs of one row through the Linear layers: forward (2 MAC), weight
+        gradients (2 MAC) and input gradients of every layer but the first (2 MAC); GroupNorm,
+        SiLU, the loss and AdamW are not counted."""
+        H = 64
+        nh = 3 if not self.discrete else 2
+        nout = self.A + 1 if self.discrete else 2 * self.A + 1
+        trunk, heads, outs = self.D * H, nh * H * H, nout * H
+        return 2 * (trunk + heads + outs) * 2 + 2 * (heads + outs)
+
     PHASES = ("forward+backward", "publish", "wait A", "slice reduce", "wait B", "norm",
               "AdamW")
 
@@ -118,12 +129,20 @@ class FusedUpdate:
         group = self.ppo.optimizer.param_groups[0]
         beta1, beta2 = group["betas"]
         A2 = A if A.dim() == 2 else A.reshape(-1, 1)
+        if self.events is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         prl_native.ppo_update(
             self.flat, self.m, self.v, self.step, self.D, self.A, self.discrete,
             S.contiguous(), A2.contiguous(), old_logp.contiguous(), adv.contiguous(),
             ret.contiguous(), self.mini_batch, k_epochs, self.ppo.policy_clip,
             self.ppo.value_coef, self.ppo.entropy_coef, group["lr"], beta1, beta2, group["eps"],
             group["weight_decay"], 2.0, self.loss, self.ws)
+        if self.events is not None:
+            ev[1].record()
+            nb = -(-int(S.shape[0]) // self.mini_batch)
+            self.events.append(("ppo_update_kernel", ev[0], ev[1], int(S.shape[0]) * int(k_epochs),
+                                int(k_epochs) * nb))
         self._sync_optimizer_state()
         status = max(prl_native.ppo_update_status(self.ws).tolist())
         if status != 0:
@@ -171,12 +190,20 @@ class FusedUpdate:
         adam_tail = (ctypes.c_float(self.ppo.value_coef), ctypes.c_float(self.ppo.entropy_coef),
                      P(self.loss.data_ptr()), stream)
         step = int(round(float(self.step.item())))
+        n_local = int(S.shape[0])
         for _ in range(k_epochs):
             for j in range(nb):
                 inv = ctypes.c_float(1.0 / counts[j])
+                if self.events is not None:
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record()
                 rc = lib.prl_ppo_grad_step(*grad_fixed, j, inv, *grad_tail)
                 if rc != 0:
                     prl_native._check(rc, "prl_ppo_grad_step")
+                if self.events is not None:
+                    ev[1].record()
+                    self.events.append(("ppo_grad_kernel", ev[0], ev[1],
+                                        min(mb, max(0, n_local - j * mb)), 1))
                 all_reduce(self.grad)
                 step += 1
                 rc = lib.prl_ppo_adam_step(*adam_head, step, *adam_mid, inv, *adam_tail)

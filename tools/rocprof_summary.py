@@ -82,17 +82,26 @@ def pmc(paths, match, n=0):
     print(json.dumps(out[0] if n and len(out) == 1 else out, indent=1))
 
 
-def trace(path, match):
-    """Durations of the matching kernel's dispatches, grouped by grid size."""
+def trace(path, match, last=0):
+    """Durations of the matching kernel's dispatches, grouped by grid size; last > 0 keeps only
+    the last `last` dispatches of each group in time order (e.g. bench.py's timed steps after
+    its warm-up launch)."""
     acc = defaultdict(list)
     for r in csv.DictReader(open(path)):
         if match in r["Kernel_Name"]:
             acc[(short(r["Kernel_Name"]), int(r["Grid_Size_X"]))].append(
-                (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+                (int(r["Start_Timestamp"]),
+                 (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
     out = []
-    for (k, grid), us in sorted(acc.items()):
-        us.sort()
-        out.append({"kernel": k, "grid_size": grid, "dispatches": len(us),
+    for (k, grid), ev in sorted(acc.items()):
+        ev.sort()
+        n_all = len(ev)
+        if last > 0:
+            ev = ev[-last:]
+        us = sorted(d for _, d in ev)
+        out.append({"kernel": k, "grid_size": grid, "dispatches": n_all,
+                    "averaged_over": ("all" if last <= 0 or last >= n_all
+                                      else f"last {len(us)} in time order"),
                     "avg_us": round(sum(us) / len(us), 2), "median_us": us[len(us) // 2],
                     "min_us": us[0], "max_us": us[-1]})
     print(json.dumps(out, indent=1))
@@ -105,10 +114,11 @@ if __name__ == "__main__":
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--match", default="")
     ap.add_argument("--n", type=int, default=0, help="pmc: transitions per launch (recorded)")
+    ap.add_argument("--last", type=int, default=0, help="trace: average the last N dispatches")
     a = ap.parse_args()
     if a.mode == "stats":
         stats(a.paths[0], a.top)
     elif a.mode == "pmc":
         pmc(a.paths, a.match, a.n)
     else:
-        trace(a.paths[0], a.match)
+        trace(a.paths[0], a.match, a.last)
