@@ -107,12 +107,12 @@ class FusedUpdate:
     PHASES = ("forward+backward", "publish", "wait A", "slice reduce", "wait B", "norm",
               "AdamW")
 
-    CHUNK_STAGES = ("inputs", "trunk fwd", "heads fwd", "outputs+loss", "heads bwd",
-                    "weight grads+dF", "trunk bwd", "dW0")
+    CHUNK_STAGES = ("forward", "barrier 1", "loss", "heads bwd + dW2", "barrier 2", "dW1",
+                    "dF + trunk bwd", "dW0 + biases")
 
     def profile(self):
         """Workgroup 0's time per phase of the last launch, us per step (s_memrealtime, 100 MHz);
-        'chunk' splits forward+backward by stage (summed over the step's row chunks)."""
+        'chunk' splits forward+backward by stage (summed over the step's 16-row tiles)."""
         p = self.ws[256:512].view(torch.int64).tolist()
         steps = max(p[7], 1)
         out = {name: round(p[i] * 0.01 / steps, 2) for i, name in enumerate(self.PHASES)}

@@ -42,7 +42,6 @@
 namespace prl {
 
 constexpr int UPD_THREADS = 256;
-constexpr int UPD_RC = 8;         // rows per chunk
 constexpr int UPD_H = 64;         // hidden width
 constexpr int UPD_HS = 68;        // LDS row stride of [*][64] arrays
 constexpr int UPD_MAXH = 3;       // heads
@@ -148,126 +147,52 @@ __device__ inline bool upd_in(const UpdTensor& t, int k, int& f) {
 __device__ inline int upd_flat_of(const UpdNet& n, int k) {
   int f = -1;
   if (upd_in(n.w0, k, f) || upd_in(n.g0, k, f) || upd_in(n.b0, k, f)) return f;
-  for (int h = 0; h < n.nh; ++h)
-    if (upd_in(n.w1[h], k, f) || upd_in(n.g1[h], k, f) || upd_in(n.b1[h], k, f) ||
-        upd_in(n.w2[h], k, f) || upd_in(n.b2[h], k, f))
+#pragma unroll
+  for (int h = 0; h < UPD_MAXH; ++h)   // compile-time h: no dynamic indexing of the kernarg
+    if (h < n.nh && (upd_in(n.w1[h], k, f) || upd_in(n.g1[h], k, f) || upd_in(n.b1[h], k, f) ||
+                     upd_in(n.w2[h], k, f) || upd_in(n.b2[h], k, f)))
       return f;
   return -1;
 }
 
-// ---- per-chunk activation buffers (floats, offsets into the dynamic LDS) ---------------------
-constexpr int UPD_HEAD_FLOATS = 4 * UPD_RC * UPD_HS + UPD_RC * 8;
-struct UpdAct {
-  float* X;       // [RC][DX]
-  float* Ar;      // [RC][AX] actions
-  float* oldlp;   // [RC]
-  float* adv;     // [RC]
-  float* ret;     // [RC]
-  float* lossp;   // [RC][4]
-  float* T0;      // [RC][HS]  dH0
-  float* XH0;     // [RC][HS]
-  float* F;       // [RC][HS]
-  float* DU0;     // [RC][HS]
-  float* rstd0;   // [RC][8]
-  float* heads;   // per head h at heads + h * UPD_HEAD_FLOATS:
-                  //   ZB [RC][HS] (dZ), XH, Gh, DU [RC][HS], rstd [RC][8]
-  __device__ float* ZB(int h) const { return heads + h * UPD_HEAD_FLOATS; }
-  __device__ float* XH(int h) const { return heads + h * UPD_HEAD_FLOATS + UPD_RC * UPD_HS; }
-  __device__ float* Gh(int h) const { return heads + h * UPD_HEAD_FLOATS + 2 * UPD_RC * UPD_HS; }
-  __device__ float* DU(int h) const { return heads + h * UPD_HEAD_FLOATS + 3 * UPD_RC * UPD_HS; }
-  __device__ float* rstd(int h) const { return heads + h * UPD_HEAD_FLOATS + 4 * UPD_RC * UPD_HS; }
-  float* dFh;     // [MAXH][RC][HS] per-head parts of dF
-  __device__ float* dF(int h) const { return dFh + h * UPD_RC * UPD_HS; }
-  float* O;       // [RC][OX]
-  float* dO;      // [RC][OX]
-  int DX, AX, OX;
+// ---- per-tile LDS scratch (floats, carved after the parameter / gradient images) -------------
+// One tile = 16 rows.  Wave w (of 4) owns channel block w (channels 16w .. 16w+15) of every
+// 64-wide layer; activations stay in MFMA C fragments (lane (x = l & 15, q = l >> 4), register i
+// holds [row x][channel 16 b + 4 q + i]), and the only LDS traffic is the transposes the weight
+// gradients need (they contract over rows) plus the output-layer partials.
+constexpr int UPD_RT = 16;        // rows per tile
+constexpr int UPD_ZS = 80;        // row stride of the [16 rows][64 ch] tiles (80 = 16 mod 64)
+constexpr int UPD_RIN = 12;       // row-input record: act[8], old_logp, adv, ret, pad
+constexpr int UPD_MAXO = 16;      // outputs of all heads together (one 16-row MFMA tile)
+
+__host__ __device__ inline int upd_xs(int D) { return D <= 16 ? 16 : UPD_ZS; }
+__host__ __device__ inline int upd_scratch_floats(int D) {
+  return UPD_RT * upd_xs(D)          // Xs  [16][XS]      tile inputs (rows x features)
+         + 4 * UPD_RT * 16           // Op  [4][16][16]   output-layer partial per wave
+         + 4 * UPD_RT * 16           // Os  [4][16][16]   assembled outputs per wave
+         + 4 * UPD_RT * 16           // dOs [4][16][16]   d loss / d outputs per wave
+         + UPD_RT * UPD_RIN          // Rin [16][12]      row inputs
+         + UPD_RT * UPD_ZS           // Fs  [16][80]      trunk output
+         + UPD_MAXH * UPD_RT * UPD_ZS  // Zs [h][16][80]  head dZ
+         + 4 * UPD_RT * 16           // Ts  [4][16][16]   per-wave transpose slot (G_h, dH0)
+         + 16;
+}
+struct UpdScr {
+  float *Xs, *Op, *Os, *dOs, *Rin, *Fs, *Zs, *Ts;
+  int XS;
 };
-
-__host__ __device__ inline int upd_act_floats(int D, int A, int nout, int& DX, int& AX, int& OX) {
-  DX = (D + 3) & ~3;
-  AX = (A + 3) & ~3;
-  OX = (nout + 3) & ~3;
-  return UPD_RC * (DX + AX + 4 + 4 + 4 * UPD_HS + 8 + UPD_MAXH * (5 * UPD_HS + 8) + 2 * OX) + 16;
-}
-
-__device__ inline UpdAct upd_carve(float* base, const UpdNet& n) {
-  UpdAct a;
-  upd_act_floats(n.D, n.A, n.nout, a.DX, a.AX, a.OX);
-  float* p = base;
-  auto take = [&](int nf) { float* q = p; p += (nf + 3) & ~3; return q; };
-  a.X = take(UPD_RC * a.DX);
-  a.Ar = take(UPD_RC * a.AX);
-  a.oldlp = take(UPD_RC);
-  a.adv = take(UPD_RC);
-  a.ret = take(UPD_RC);
-  a.lossp = take(UPD_RC * 4);
-  a.T0 = take(UPD_RC * UPD_HS);
-  a.XH0 = take(UPD_RC * UPD_HS);
-  a.F = take(UPD_RC * UPD_HS);
-  a.DU0 = take(UPD_RC * UPD_HS);
-  a.rstd0 = take(UPD_RC * 8);
-  a.heads = take(UPD_MAXH * UPD_HEAD_FLOATS);
-  a.dFh = take(UPD_MAXH * UPD_RC * UPD_HS);
-  a.O = take(UPD_RC * a.OX);
-  a.dO = take(UPD_RC * a.OX);
-  return a;
-}
-
-// GroupNorm(8 groups of 8) + SiLU forward of one (row, group) held in registers: same
-// arithmetic as gn_silu_fwd.  Writes xhat and the block output (16-B aligned LDS rows).
-__device__ inline void upd_gn_fwd(const float (&v)[8], const float* gw, const float* gb,
-                                  float* xh_out, float* y_out, float* rstd_out) {
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) s += v[k];
-  const float mean = s * (1.0f / 8);
-  float q = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) q += (v[k] - mean) * (v[k] - mean);
-  const float rstd = 1.0f / sqrtf(q * (1.0f / 8) + 1e-5f);
-  float xh[8], y[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    xh[k] = (v[k] - mean) * rstd;
-    const float u = xh[k] * gw[k] + gb[k];
-    y[k] = u / (1.0f + expf(-u));
-  }
-  *reinterpret_cast<float4*>(xh_out) = float4{xh[0], xh[1], xh[2], xh[3]};
-  *reinterpret_cast<float4*>(xh_out + 4) = float4{xh[4], xh[5], xh[6], xh[7]};
-  *reinterpret_cast<float4*>(y_out) = float4{y[0], y[1], y[2], y[3]};
-  *reinterpret_cast<float4*>(y_out + 4) = float4{y[4], y[5], y[6], y[7]};
-  *rstd_out = rstd;
-}
-
-// backward of the above: go = d(block output) in registers; writes dX and du = d(pre-SiLU)
-__device__ inline void upd_gn_bwd(const float (&go)[8], const float* xh_in, const float* gw,
-                                  const float* gb, float rstd, float* dx_out, float* du_out) {
-  float xh[8];
-  {
-    const float4 c = *reinterpret_cast<const float4*>(xh_in);
-    const float4 d = *reinterpret_cast<const float4*>(xh_in + 4);
-    xh[0] = c.x; xh[1] = c.y; xh[2] = c.z; xh[3] = c.w; xh[4] = d.x; xh[5] = d.y; xh[6] = d.z; xh[7] = d.w;
-  }
-  float dy[8], dxh[8];
-  float m1 = 0.f, m2 = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const float u = xh[k] * gw[k] + gb[k];
-    const float s = upd_sigmoid(u);
-    dy[k] = go[k] * (s * (1.0f + u * (1.0f - s)));
-    dxh[k] = dy[k] * gw[k];
-    m1 += dxh[k];
-    m2 += dxh[k] * xh[k];
-  }
-  m1 *= (1.0f / 8);
-  m2 *= (1.0f / 8);
-  float dx[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) dx[k] = rstd * (dxh[k] - m1 - xh[k] * m2);
-  *reinterpret_cast<float4*>(dx_out) = float4{dx[0], dx[1], dx[2], dx[3]};
-  *reinterpret_cast<float4*>(dx_out + 4) = float4{dx[4], dx[5], dx[6], dx[7]};
-  *reinterpret_cast<float4*>(du_out) = float4{dy[0], dy[1], dy[2], dy[3]};
-  *reinterpret_cast<float4*>(du_out + 4) = float4{dy[4], dy[5], dy[6], dy[7]};
+__device__ inline UpdScr upd_scr(float* p, int D) {
+  UpdScr s;
+  s.XS = upd_xs(D);
+  s.Xs = p; p += UPD_RT * s.XS;
+  s.Op = p; p += 4 * UPD_RT * 16;
+  s.Os = p; p += 4 * UPD_RT * 16;
+  s.dOs = p; p += 4 * UPD_RT * 16;
+  s.Rin = p; p += UPD_RT * UPD_RIN;
+  s.Fs = p; p += UPD_RT * UPD_ZS;
+  s.Zs = p; p += UPD_MAXH * UPD_RT * UPD_ZS;
+  s.Ts = p;
+  return s;
 }
 
 // log_prob and entropy of one row's action under the head outputs O (ActorCritic.get_evaluate,
@@ -280,7 +205,7 @@ struct UpdDist {
   int ai;
 };
 // KD: 1 discrete / 0 continuous / -1 runtime;  KA: action dim (0 = runtime).  Specialised
-// kernels keep the per-row code (executed by 8 lanes, but fetched every step) small.
+// kernels keep the per-row code (executed by 16 lanes, but fetched every step) small.
 template <int KD, int KA>
 __device__ inline void upd_row_dist(const UpdNet& n, const float* O, const float* act, UpdDist& d) {
   const int A = KA > 0 ? KA : n.A;
@@ -340,27 +265,27 @@ __device__ inline void upd_row_dist(const UpdNet& n, const float* O, const float
   }
 }
 
-// Per-row loss (surrogate, prl_loss.hip semantics) and the gradient w.r.t. the head outputs.
-// Loops run to the compile-time UPD_MAXA with `k < A` guards so everything stays in registers.
+// Per-row loss (surrogate, prl_loss.hip semantics) and the gradient w.r.t. the head outputs
+// dO[0 .. nout) (dO[nout .. 16) = 0).  lp = {-min(s1, s2), SmoothL1, H}.
 template <int KD, int KA>
-__device__ inline void upd_row_loss(const UpdNet& n, const UpdAct& a, int r, float invB, float clip,
-                                    float vf_coef) {
-  const float* O = a.O + r * a.OX;
-  float* dO = a.dO + r * a.OX;
+__device__ inline void upd_row_loss(const UpdNet& n, const float* O, const float* rin, float invB,
+                                    float clip, float vf_coef, float* dO, float (&lp)[3]) {
   const int A = KA > 0 ? KA : n.A;
   const bool discrete = KD >= 0 ? (KD != 0) : (n.discrete != 0);
   const int vcol = discrete ? A : 2 * A;      // critic output column
+#pragma unroll
+  for (int j = 0; j < UPD_MAXO; ++j) dO[j] = 0.f;
   UpdDist dist;
-  upd_row_dist<KD, KA>(n, O, a.Ar + r * a.AX, dist);
+  upd_row_dist<KD, KA>(n, O, rin, dist);
   const float logp = dist.logp, H = dist.H, S2 = dist.S2, qa = dist.qa;
   const int ai = dist.ai;
   const float* p = dist.p;
   const float V = O[vcol];
   // surrogate
-  const float diff = logp - a.oldlp[r];
+  const float diff = logp - rin[8];
   const float cl = diff < -20.0f ? -20.0f : (diff > 20.0f ? 20.0f : diff);
   const float ratio = expf(cl);
-  const float adv = a.adv[r];
+  const float adv = rin[9];
   const float s1 = ratio * adv;
   const float lo = 1.0f - clip, hi = 1.0f + clip;
   const float rcl = ratio < lo ? lo : (ratio > hi ? hi : ratio);
@@ -373,14 +298,14 @@ __device__ inline void upd_row_loss(const UpdNet& n, const UpdAct& a, int r, flo
   const float in_clip = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
   const float in_20 = (diff >= -20.0f && diff <= 20.0f) ? 1.0f : 0.0f;
   const float dlogp = -invB * (w1 * adv + w2 * adv * in_clip) * ratio * in_20;
-  const float x = V - a.ret[r];
+  const float x = V - rin[10];
   const float ax = fabsf(x);
   const float sl = ax < 1.0f ? 0.5f * ax * ax : ax - 0.5f;
   const float gx = ax < 1.0f ? x : (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f));
   dO[vcol] = vf_coef * invB * gx;
-  a.lossp[r * 4 + 0] = -m;
-  a.lossp[r * 4 + 1] = sl;
-  a.lossp[r * 4 + 2] = H;
+  lp[0] = -m;
+  lp[1] = sl;
+  lp[2] = H;
   // d logp / d head outputs
   if (discrete) {
     const float mk = (qa >= FLT_EPSILON && qa <= 1.0f - FLT_EPSILON) ? 1.0f : 0.0f;
@@ -403,7 +328,7 @@ __device__ inline void upd_row_loss(const UpdNet& n, const UpdAct& a, int r, flo
         const float lsr = O[A + k];
         const float lsc = lsr < -2.0f ? -2.0f : (lsr > 2.0f ? 2.0f : lsr);
         const float sd = log1pf(expf(lsc));
-        const float d = a.Ar[r * a.AX + k] - mu;
+        const float d = rin[k] - mu;
         const float var = sd * sd;
         dO[k] = dlogp * (d / var);
         const float dsd = dlogp * ((d * d) / (var * sd) - 1.0f / sd);
@@ -414,170 +339,253 @@ __device__ inline void upd_row_loss(const UpdNet& n, const UpdAct& a, int r, flo
   }
 }
 
-// Cross-lane moves within 8-lane groups by DPP (no LDS round trip, unlike __shfl*, which lowers
-// to ds_bpermute): quad_perm [1,0,3,2] = xor 1, [2,3,0,1] = xor 2, row_half_mirror (lane i <->
-// 7 - i) carries the other quad's sum.  Every lane of a group ends with the same bits (IEEE add
-// is commutative).
+// Cross-lane moves by DPP (no LDS round trip, unlike __shfl*, which lowers to ds_bpermute):
+// quad_perm [1,0,3,2] = xor 1, [2,3,0,1] = xor 2, row_half_mirror (lane i <-> 7 - i), row_mirror
+// (lane i <-> 15 - i).  Butterflies of commutative adds: every lane ends with the same bits.
 template <int CTRL>
 __device__ inline float upd_dpp(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 __device__ inline float upd_xor1(float v) { return upd_dpp<0xB1>(v); }
 __device__ inline float upd_xor2(float v) { return upd_dpp<0x4E>(v); }
-// sum over the 8 consecutive lanes of a GroupNorm group (lanes = channels)
-__device__ inline float upd_gsum8(float v) {
+// sum over the 16 lanes of a DPP row (= the 16 rows of a tile, for one channel quad q)
+__device__ inline float upd_rsum16(float v) {
   v += upd_xor1(v);
   v += upd_xor2(v);
   v += upd_dpp<0x141>(v);
+  v += upd_dpp<0x140>(v);
   return v;
 }
+// the partner lane l ^ 16 (the other 4 channels of the lane's GroupNorm group)
+__device__ inline float upd_p16(float v) { return __shfl_xor(v, 16); }
 
-// GroupNorm(8, 64) + SiLU forward of one element, lanes = channels o (group = 8 lanes)
-__device__ inline void upd_gn_fwd_lane(float v, float gw, float gb, float* xh_out, float* y_out,
-                                       float* rstd_out, bool write_rstd) {
-  const float mean = upd_gsum8(v) * (1.0f / 8);
-  const float dv = v - mean;
-  const float rstd = 1.0f / sqrtf(upd_gsum8(dv * dv) * (1.0f / 8) + 1e-5f);
-  const float xh = dv * rstd;
-  const float u = xh * gw + gb;
-  *xh_out = xh;
-  *y_out = u / (1.0f + expf(-u));
-  if (write_rstd) *rstd_out = rstd;
+typedef float upd_v4 __attribute__((ext_vector_type(4)));
+__device__ inline upd_v4 upd_mma(float a, float b, upd_v4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ inline upd_v4 upd_ld4(const float* p) {
+  const float4 v = *reinterpret_cast<const float4*>(p);
+  return upd_v4{v.x, v.y, v.z, v.w};
+}
+__device__ inline void upd_st4(float* p, upd_v4 v) {
+  *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
+}
+// intra-wave LDS hand-off between lanes (LDS ops of one wave complete in order)
+__device__ inline void upd_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// backward of the above: go = d(block output); writes dX, returns du (= d pre-SiLU)
-__device__ inline float upd_gn_bwd_lane(float go, float xh, float gw, float gb, float rstd,
-                                        float* dx_out) {
-  const float u = xh * gw + gb;
-  const float sg = upd_sigmoid(u);
-  const float dy = go * (sg * (1.0f + u * (1.0f - sg)));
-  const float dxh = dy * gw;
-  const float m1 = upd_gsum8(dxh) * (1.0f / 8);
-  const float m2 = upd_gsum8(dxh * xh) * (1.0f / 8);
-  *dx_out = rstd * (dxh - m1 - xh * m2);
-  return dy;
-}
-
-__device__ inline int upd_head_of(const UpdNet& n, int j) {
-  int h = 0;
-  while (h + 1 < n.nh && j >= n.ocol[h + 1]) ++h;
-  return h;
-}
-
-// Forward of rc <= RC rows (ActorCritic.get_evaluate's network part): S0 inputs, S1 trunk,
-// S2 heads, then the head outputs O gathered to each row's leader lane (t == 32 r) — the only
-// reader of O[r] in the caller's per-row epilogue, so no barrier follows.
-__device__ inline void upd_forward(const UpdNet& n, const float* W, const UpdAct& a,
-                                   const float* Sg, const float* actg, int64_t row0, int rc,
-                                   unsigned long long* tm, bool timer, unsigned long long& tl) {
-  const int t = threadIdx.x;
-  const int D = n.D, A = n.A, nh = n.nh;
-#define UPD_CMARK(i)                                                   \
-  if (timer) {                                                         \
-    const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();  \
-    tm[i] += now_ - tl;                                                \
-    tl = now_;                                                         \
-  }
-  // S0. inputs
-  for (int i = t; i < UPD_RC * a.DX; i += UPD_THREADS) {
-    const int r = i / a.DX, d = i % a.DX;
-    a.X[i] = (r < rc && d < D) ? Sg[(row0 + r) * D + d] : 0.0f;
-  }
-  const int Aw = n.discrete ? 1 : A;
-  for (int i = t; i < UPD_RC * a.AX; i += UPD_THREADS) {
-    const int r = i / a.AX, k = i % a.AX;
-    a.Ar[i] = (r < rc && k < Aw) ? actg[(row0 + r) * Aw + k] : 0.0f;
-  }
-  __syncthreads();
-  UPD_CMARK(0)
-  // Lanes = the 64 channels o of a row; wave w takes rows w and w + 4 (wave-uniform).
-  const int o = t & 63, wv = t >> 6;
-  // S1. trunk: H0 = X W0^T -> GroupNorm -> SiLU
-  for (int r = wv; r < rc; r += 4) {
-    const float* x = a.X + r * a.DX;
-    const float* w = W + n.w0.lds + o * n.w0.stride;
-    float acc = 0.f;
-    for (int d = 0; d < D; ++d) acc += x[d] * w[d];
-    upd_gn_fwd_lane(acc, W[n.g0.lds + o], W[n.b0.lds + o], a.XH0 + r * UPD_HS + o,
-                    a.F + r * UPD_HS + o, a.rstd0 + r * 8 + (o >> 3), (o & 7) == 0);
-  }
-  __syncthreads();
-  UPD_CMARK(1)
-  // S2. heads: Z_h = F W1_h^T -> GroupNorm -> SiLU (rows w and w + 4 share each W1 read)
-  for (int h = 0; h < nh; ++h) {
-    const float* wrow = W + n.w1[h].lds + o * UPD_HS;
-    const int r0 = wv, r1 = wv + 4;
-    const bool two = r1 < rc;
-    if (r0 >= rc) break;
-    const float* f0 = a.F + r0 * UPD_HS;
-    const float* f1 = a.F + (two ? r1 : r0) * UPD_HS;
-    float z0 = 0.f, z1 = 0.f;
-#pragma unroll 4
-    for (int i = 0; i < UPD_H; i += 4) {
-      const float4 w4 = *reinterpret_cast<const float4*>(wrow + i);
-      const float4 a4 = *reinterpret_cast<const float4*>(f0 + i);
-      const float4 b4 = *reinterpret_cast<const float4*>(f1 + i);
-      z0 += a4.x * w4.x; z0 += a4.y * w4.y; z0 += a4.z * w4.z; z0 += a4.w * w4.w;
-      z1 += b4.x * w4.x; z1 += b4.y * w4.y; z1 += b4.z * w4.z; z1 += b4.w * w4.w;
-    }
-    const float gw = W[n.g1[h].lds + o], gb = W[n.b1[h].lds + o];
-    upd_gn_fwd_lane(z0, gw, gb, a.XH(h) + r0 * UPD_HS + o, a.Gh(h) + r0 * UPD_HS + o,
-                    a.rstd(h) + r0 * 8 + (o >> 3), (o & 7) == 0);
-    if (two)
-      upd_gn_fwd_lane(z1, gw, gb, a.XH(h) + r1 * UPD_HS + o, a.Gh(h) + r1 * UPD_HS + o,
-                      a.rstd(h) + r1 * 8 + (o >> 3), (o & 7) == 0);
-  }
-  __syncthreads();
-  UPD_CMARK(2)
-  // S3. head outputs + loss: one half-wave per row; lane l = (output j % 8, quarter of the 64
-  //     inputs); quarter sums combined by shuffles, gathered by the row's leader lane, which
-  //     writes O, evaluates the loss and writes d(loss)/d(outputs)
-  {
-    const int r = t >> 5, l = t & 31, jl = l >> 2, part = l & 3;
-    for (int j0 = 0; j0 < n.nout; j0 += 8) {
-      const int j = j0 + jl;
-      float acc = 0.f;
-      if (r < rc && j < n.nout) {
-        const int h = upd_head_of(n, j), k = j - n.ocol[h];
-        const float* wv = W + n.w2[h].lds + k * UPD_HS + part * 16;
-        const float* gv = a.Gh(h) + r * UPD_HS + part * 16;
+// GroupNorm(8 groups of 8) + SiLU forward on a C fragment: the lane's 4 channels + the partner
+// lane's 4 form the group.  Returns xhat, rstd and the block output.
+__device__ inline void upd_gn_fwd_frag(upd_v4 z, upd_v4 gw, upd_v4 gb, upd_v4& xh, float& rstd,
+                                       upd_v4& y) {
+  const float s4 = (z[0] + z[1]) + (z[2] + z[3]);
+  const float mean = (s4 + upd_p16(s4)) * 0.125f;
+  upd_v4 d;
 #pragma unroll
-        for (int i = 0; i < 16; i += 4) {
-          const float4 w4 = *reinterpret_cast<const float4*>(wv + i);
-          const float4 g4 = *reinterpret_cast<const float4*>(gv + i);
-          acc += g4.x * w4.x;
-          acc += g4.y * w4.y;
-          acc += g4.z * w4.z;
-          acc += g4.w * w4.w;
-        }
-      }
-      acc += upd_xor1(acc);
-      acc += upd_xor2(acc);
+  for (int i = 0; i < 4; ++i) d[i] = z[i] - mean;
+  const float q4 = (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+  rstd = 1.0f / sqrtf((q4 + upd_p16(q4)) * 0.125f + 1e-5f);
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {    // gather to the row leaders: two scalar reads per j
-        const float vlo = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), 4 * jj));
-        const float vhi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), 32 + 4 * jj));
-        const float v = (t & 32) ? vhi : vlo;
-        const int jo = j0 + jj;
-        if (l == 0 && r < rc && jo < n.nout) {
-          const int h = upd_head_of(n, jo);
-          a.O[r * a.OX + jo] = v + W[n.b2[h].lds + (jo - n.ocol[h])];
-        }
-      }
-    }
+  for (int i = 0; i < 4; ++i) {
+    xh[i] = d[i] * rstd;
+    const float u = xh[i] * gw[i] + gb[i];
+    y[i] = u / (1.0f + expf(-u));
   }
-#undef UPD_CMARK
+}
+// backward of the above: go = d(block output); returns dX, dy = d(pre-SiLU) (for dγ, dβ)
+__device__ inline upd_v4 upd_gn_bwd_frag(upd_v4 go, upd_v4 xh, upd_v4 gw, upd_v4 gb, float rstd,
+                                         upd_v4& dy) {
+  upd_v4 dxh;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float u = xh[i] * gw[i] + gb[i];
+    const float sg = upd_sigmoid(u);
+    dy[i] = go[i] * (sg * (1.0f + u * (1.0f - sg)));
+    dxh[i] = dy[i] * gw[i];
+  }
+  const float a4 = (dxh[0] + dxh[1]) + (dxh[2] + dxh[3]);
+  const float b4 = (dxh[0] * xh[0] + dxh[1] * xh[1]) + (dxh[2] * xh[2] + dxh[3] * xh[3]);
+  const float m1 = (a4 + upd_p16(a4)) * 0.125f;
+  const float m2 = (b4 + upd_p16(b4)) * 0.125f;
+  upd_v4 dx;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dx[i] = rstd * (dxh[i] - m1 - xh[i] * m2);
+  return dx;
 }
 
-// One chunk of rc <= RC rows: forward, loss, backward; gradients accumulated into Ga (LDS
-// image).  Eight barrier-separated stages; each Linear is fused with the GroupNorm that follows
-// it (one thread per (row, group) owns 8 channels end to end).
+// image offset of output j's bias (head chosen by compile-time h: no dynamic kernarg indexing)
+__device__ inline int upd_bias_of(const UpdNet& n, int j) {
+  int off = 0;
+#pragma unroll
+  for (int h = 0; h < UPD_MAXH; ++h)
+    if (h < n.nh && j >= n.ocol[h] && j < n.ocol[h] + n.out[h]) off = n.b2[h].lds + (j - n.ocol[h]);
+  return off;
+}
+
+template <int KD>
+__device__ inline int upd_nh(const UpdNet& n) { return KD > 0 ? 2 : (KD == 0 ? 3 : n.nh); }
+
+// Forward state of one tile kept for the backward (wave w's channel block, lane's row x).
+// KSM = compile-time bound on the input k-steps ceil(D / 4) (4 for the specialised kernels).
+template <int KSM>
+struct UpdFwd {
+  upd_v4 Fw;                         // trunk output, block w
+  upd_v4 xh0;                        // trunk xhat (block w)
+  float r0;                          // trunk rstd (block w)
+  upd_v4 xh[UPD_MAXH], G[UPD_MAXH];  // head xhat / output (block w)
+  float rh[UPD_MAXH];
+  float xin[KSM];                    // B fragments of the inputs: X[row x][4 s + q]
+};
+template <int KA>
+constexpr int upd_ksm() { return KA > 0 ? 4 : 16; }
+
+// Forward of one tile (rows row0 .. row0 + rc - 1, rc <= 16) up to the output-layer partials:
+// every wave runs the trunk for all 64 channels (it is the B operand of every head block), then
+// its head block w; the output layer's K = 64 sum is split over the waves (partial per wave in
+// Op[w]).  Also stages the row inputs (act, old_logp, adv, ret) into Rin.  No barrier inside;
+// the caller's barrier publishes Op / Rin.
 template <int KD, int KA>
-__device__ void upd_chunk(const UpdArgs& args, const float* W, float* Ga, const UpdAct& a,
-                          int64_t row0, int rc, float invB, unsigned long long* tm) {
+__device__ inline void upd_tile_fwd(const UpdNet& n, const float* W, const UpdScr& sc,
+                                    const float* Sg, const float* actg, const float* oldg,
+                                    const float* advg, const float* retg, int64_t row0, int rc,
+                                    UpdFwd<upd_ksm<KA>()>& f) {
+  constexpr int KSM = upd_ksm<KA>();
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  const int D = n.D, KS = (D + 3) >> 2;
+  const int nh = upd_nh<KD>(n);
+  const bool rowok = x < rc;
+  // global loads first (their latency runs under the trunk's LDS reads)
+#pragma unroll
+  for (int s = 0; s < KSM; ++s) {
+    const int d = 4 * s + q;
+    f.xin[s] = (s < KS && rowok && d < D) ? Sg[(row0 + x) * D + d] : 0.0f;
+  }
+  float rin = 0.f;
+  if (t < UPD_RT * UPD_RIN) {
+    const int r = t / UPD_RIN, k = t % UPD_RIN;
+    const int Aw = n.discrete ? 1 : n.A;
+    if (r < rc) {
+      if (k < UPD_MAXA) rin = k < Aw ? actg[(row0 + r) * Aw + k] : 0.0f;
+      else if (k == 8 && oldg) rin = oldg[row0 + r];
+      else if (k == 9 && advg) rin = advg[row0 + r];
+      else if (k == 10 && retg) rin = retg[row0 + r];
+    }
+  }
+  // trunk: H0^T block b = W0[16b .. 16b+15][:] X^T  (A: W0 rows, B: inputs), then GN + SiLU
+  upd_v4 F[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* wr = W + n.w0.lds + (16 * b + x) * n.w0.stride;
+#pragma unroll
+    for (int s = 0; s < KSM; ++s) {
+      if (s < KS) {
+        const int d = 4 * s + q;
+        acc = upd_mma(d < D ? wr[d] : 0.0f, f.xin[s], acc);
+      }
+    }
+    upd_v4 xh;
+    float rs;
+    upd_gn_fwd_frag(acc, upd_ld4(W + n.g0.lds + 16 * b + 4 * q), upd_ld4(W + n.b0.lds + 16 * b + 4 * q),
+                    xh, rs, F[b]);
+    if (b == w) {
+      f.xh0 = xh;
+      f.r0 = rs;
+      f.Fw = F[b];
+    }
+  }
+  // heads: Z_h^T block w = W1_h[16w ..][:] F^T; K order per step (b, i): lane q <-> input
+  // channel 16 b + 4 q + i, so F's C fragments are the B operand as they stand
+  upd_v4 z[UPD_MAXH];
+#pragma unroll
+  for (int h = 0; h < UPD_MAXH; ++h) z[h] = upd_v4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+#pragma unroll
+    for (int h = 0; h < UPD_MAXH; ++h) {
+      if (h < nh) {
+        const upd_v4 wa = upd_ld4(W + n.w1[h].lds + (16 * w + x) * UPD_HS + 16 * b + 4 * q);
+        z[h] = upd_mma(wa[0], F[b][0], z[h]);
+        z[h] = upd_mma(wa[1], F[b][1], z[h]);
+        z[h] = upd_mma(wa[2], F[b][2], z[h]);
+        z[h] = upd_mma(wa[3], F[b][3], z[h]);
+      }
+    }
+  }
+  // head GN + SiLU, then the output layer's partial over this block's 16 channels:
+  // O^T[j][row] += W2[j][16w + 4q + i] G^T (A row m = output j, head h's rows at ocol[h])
+  upd_v4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < UPD_MAXH; ++h) {
+    if (h < nh) {
+      upd_gn_fwd_frag(z[h], upd_ld4(W + n.g1[h].lds + 16 * w + 4 * q),
+                      upd_ld4(W + n.b1[h].lds + 16 * w + 4 * q), f.xh[h], f.rh[h], f.G[h]);
+      const int oc = n.ocol[h], no = n.out[h];
+      const bool mine = x >= oc && x < oc + no;
+      const upd_v4 wv = mine ? upd_ld4(W + n.w2[h].lds + (x - oc) * UPD_HS + 16 * w + 4 * q)
+                             : upd_v4{0.f, 0.f, 0.f, 0.f};
+      o = upd_mma(wv[0], f.G[h][0], o);
+      o = upd_mma(wv[1], f.G[h][1], o);
+      o = upd_mma(wv[2], f.G[h][2], o);
+      o = upd_mma(wv[3], f.G[h][3], o);
+    }
+  }
+  upd_st4(sc.Op + (w * 16 + x) * 16 + 4 * q, o);   // [w][row x][j = 4q + i]
+  if (t < UPD_RT * UPD_RIN) sc.Rin[t] = rin;
+}
+
+// After the barrier that publishes Op: lanes q == 0 of every wave assemble row x's outputs
+// (fixed order over the 4 partials, then the bias) into Os[w][x][*]; returns the pointer.
+__device__ inline const float* upd_tile_outputs(const UpdNet& n, const float* W, const UpdScr& sc) {
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  float* Orow = sc.Os + (w * 16 + x) * 16;
+  if (q == 0) {
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const upd_v4 p0 = upd_ld4(sc.Op + (0 * 16 + x) * 16 + 4 * j4);
+      const upd_v4 p1 = upd_ld4(sc.Op + (1 * 16 + x) * 16 + 4 * j4);
+      const upd_v4 p2 = upd_ld4(sc.Op + (2 * 16 + x) * 16 + 4 * j4);
+      const upd_v4 p3 = upd_ld4(sc.Op + (3 * 16 + x) * 16 + 4 * j4);
+      upd_v4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = 4 * j4 + e;
+        float s = ((p0[e] + p1[e]) + p2[e]) + p3[e];
+        if (j < n.nout) s += W[upd_bias_of(n, j)];
+        v[e] = s;
+      }
+      upd_st4(Orow + 4 * j4, v);
+    }
+  }
+  upd_wave_sync();
+  return Orow;
+}
+
+// sum over the tile's rows (DPP row) of a per-lane channel quad; lanes x == 0 add it to g[0..3]
+__device__ inline void upd_colsum_add(upd_v4 v, float* g, bool owner) {
+  upd_v4 s;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s[i] = upd_rsum16(v[i]);
+  if (owner) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g[i] += s[i];
+  }
+}
+
+// One tile of the update: forward, loss, backward; the tile's gradient is added into the LDS
+// gradient image Ga (every image entry has exactly one owning lane, so no atomics).  Two
+// workgroup barriers per tile.
+template <int KD, int KA>
+__device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const UpdScr& sc,
+                         int64_t row0, int rc, float invB, unsigned long long* tm) {
+  constexpr int KSM = upd_ksm<KA>();
   const UpdNet& n = args.net;
-  const int t = threadIdx.x;
-  const int D = n.D, A = n.A, nh = n.nh;
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  const int D = n.D, KS = (D + 3) >> 2;
+  const int nh = upd_nh<KD>(n);
   const bool timer = blockIdx.x == 0 && t == 0;
   unsigned long long tl = timer ? __builtin_amdgcn_s_memrealtime() : 0ull;
 #define UPD_CMARK(i)                                                   \
@@ -586,157 +594,162 @@ __device__ void upd_chunk(const UpdArgs& args, const float* W, float* Ga, const 
     tm[i] += now_ - tl;                                                \
     tl = now_;                                                         \
   }
-  if (t < UPD_RC) {
-    const bool ok = t < rc;
-    a.oldlp[t] = ok ? args.old_logp[row0 + t] : 0.0f;
-    a.adv[t] = ok ? args.adv[row0 + t] : 0.0f;
-    a.ret[t] = ok ? args.ret[row0 + t] : 0.0f;
-  }
-  upd_forward(n, W, a, args.S, args.act, row0, rc, tm, timer, tl);
-  const int o = t & 63, wv = t >> 6;
-  {
-    const int r = t >> 5, l = t & 31;
-    if (l == 0 && r < rc) upd_row_loss<KD, KA>(n, a, r, invB, args.clip, args.vf_coef);
-  }
-  __syncthreads();
-  UPD_CMARK(3)
-  // S4. dG_h = dO_h W2_h -> head GroupNorm + SiLU backward (lanes = channels)
-  for (int h = 0; h < nh; ++h) {
-    const float gw = W[n.g1[h].lds + o], gb = W[n.b1[h].lds + o];
-    for (int r = wv; r < rc; r += 4) {
-      const float* dO = a.dO + r * a.OX + n.ocol[h];
-      float dg = 0.f;
-      for (int k = 0; k < n.out[h]; ++k) dg += dO[k] * W[n.w2[h].lds + k * UPD_HS + o];
-      a.DU(h)[r * UPD_HS + o] =
-          upd_gn_bwd_lane(dg, a.XH(h)[r * UPD_HS + o], gw, gb, a.rstd(h)[r * 8 + (o >> 3)],
-                          a.ZB(h) + r * UPD_HS + o);
+  UpdFwd<KSM> f;
+  upd_tile_fwd<KD, KA>(n, W, sc, args.S, args.act, args.old_logp, args.adv, args.ret, row0, rc, f);
+  UPD_CMARK(0)
+  __syncthreads();   // #1: Op, Rin
+  UPD_CMARK(1)
+  // ---- loss of row x (lanes q == 0 of every wave, redundantly: each wave needs dO)
+  const float* Orow = upd_tile_outputs(n, W, sc);
+  const float* dOw = sc.dOs + w * 16 * 16;   // [row][j] of this wave
+  float lp[3] = {0.f, 0.f, 0.f};
+  if (q == 0) {
+    float* dOrow = sc.dOs + (w * 16 + x) * 16;
+    if (x < rc) {
+      upd_row_loss<KD, KA>(n, Orow, sc.Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dOrow, lp);
+    } else {
+#pragma unroll
+      for (int j = 0; j < UPD_MAXO; ++j) dOrow[j] = 0.f;
     }
   }
-  __syncthreads();
-  UPD_CMARK(4)
-  // S5. weight gradients of the heads + per-head parts of dF
-  {
-    // dW1_h += dZ_h^T F   (thread: 4 contiguous input columns x 4 output rows, per head)
-    const int i4 = (t & 15) * 4, ob = t >> 4;
-    for (int h = 0; h < nh; ++h) {
-      float acc[4][4];
+  upd_wave_sync();
+  UPD_CMARK(2)
+  float* Tw = sc.Ts + w * UPD_RT * 16;   // this wave's [16 rows][16 ch] transpose slot
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
+  for (int h = 0; h < UPD_MAXH; ++h) {
+    if (h < nh) {
+      const int oc = n.ocol[h], no = n.out[h];
+      // dW2_h[j][16w + x] += sum_rows dO[row][oc + j] G_h[row][ch]  (G_h transposed via Tw)
+      upd_st4(Tw + x * 16 + 4 * q, f.G[h]);
+      upd_wave_sync();
+      upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[k][c] = 0.f;
-#pragma unroll 4
-      for (int r = 0; r < UPD_RC; ++r) {
-        if (r >= rc) break;
-        const float4 f = *reinterpret_cast<const float4*>(a.F + r * UPD_HS + i4);
+      for (int s = 0; s < 4; ++s) {
+        const float a = x < no ? dOw[(4 * s + q) * 16 + oc + x] : 0.0f;
+        acc = upd_mma(a, Tw[(4 * s + q) * 16 + x], acc);
+      }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float dz = a.ZB(h)[r * UPD_HS + ob + 16 * k];
-          acc[k][0] += dz * f.x;
-          acc[k][1] += dz * f.y;
-          acc[k][2] += dz * f.z;
-          acc[k][3] += dz * f.w;
+      for (int i = 0; i < 4; ++i)
+        if (4 * q + i < no) Ga[n.w2[h].lds + (4 * q + i) * UPD_HS + 16 * w + x] += acc[i];
+      // dG_h^T block w = W2_h^T dO_h^T (K = the head's outputs), GroupNorm + SiLU backward
+      upd_v4 dg = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < UPD_MAXA / 4; ++s) {
+        if (4 * s < no) {
+          const int j = 4 * s + q;
+          const float a = j < no ? W[n.w2[h].lds + j * UPD_HS + 16 * w + x] : 0.0f;
+          const float bb = j < no ? dOw[x * 16 + oc + j] : 0.0f;
+          dg = upd_mma(a, bb, dg);
         }
       }
+      const upd_v4 gw = upd_ld4(W + n.g1[h].lds + 16 * w + 4 * q);
+      upd_v4 dy;
+      const upd_v4 dz = upd_gn_bwd_frag(dg, f.xh[h], gw, upd_ld4(W + n.b1[h].lds + 16 * w + 4 * q),
+                                        f.rh[h], dy);
+      upd_st4(sc.Zs + h * UPD_RT * UPD_ZS + x * UPD_ZS + 16 * w + 4 * q, dz);
+      upd_v4 dyx;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float4* gp = reinterpret_cast<float4*>(Ga + n.w1[h].lds + (ob + 16 * k) * UPD_HS + i4);
-        float4 gv = *gp;
-        gv.x += acc[k][0];
-        gv.y += acc[k][1];
-        gv.z += acc[k][2];
-        gv.w += acc[k][3];
-        *gp = gv;
+      for (int i = 0; i < 4; ++i) dyx[i] = dy[i] * f.xh[h][i];
+      upd_colsum_add(dyx, Ga + n.g1[h].lds + 16 * w + 4 * q, x == 0);
+      upd_colsum_add(dy, Ga + n.b1[h].lds + 16 * w + 4 * q, x == 0);
+      upd_wave_sync();   // Tw reads done before the next head overwrites it
+    }
+  }
+  // trunk output and inputs, rows x channels, for the weight gradients
+  upd_st4(sc.Fs + x * UPD_ZS + 16 * w + 4 * q, f.Fw);
+#pragma unroll
+  for (int s = 0; s < KSM; ++s)
+    if (s < KS && (s & 3) == w) sc.Xs[x * sc.XS + 4 * s + q] = f.xin[s];
+  UPD_CMARK(3)
+  __syncthreads();   // #2: Zs, Fs, Xs
+  UPD_CMARK(4)
+  // ---- dW1_h[16w + 4q + i][16b + x] += sum_rows dZ_h[row][out] F[row][in]  (K = rows)
+#pragma unroll
+  for (int h = 0; h < UPD_MAXH; ++h) {
+    if (h < nh) {
+      const float* Zh = sc.Zs + h * UPD_RT * UPD_ZS;
+      upd_v4 acc[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[b] = upd_v4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const float a = Zh[(4 * s + q) * UPD_ZS + 16 * w + x];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[b] = upd_mma(a, sc.Fs[(4 * s + q) * UPD_ZS + 16 * b + x], acc[b]);
       }
+      float* gw1 = Ga + n.w1[h].lds + (16 * w + 4 * q) * UPD_HS + x;
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gw1[i * UPD_HS + 16 * b] += acc[b][i];
     }
   }
-  if (t < nh * UPD_H) {   // head GroupNorm weight / bias
-    const int h = t >> 6, c = t & 63;
-    float sw = 0.f, sb = 0.f;
-#pragma unroll
-    for (int r = 0; r < UPD_RC; ++r) {
-      if (r >= rc) break;
-      const float du = a.DU(h)[r * UPD_HS + c];
-      sw += du * a.XH(h)[r * UPD_HS + c];
-      sb += du;
-    }
-    Ga[n.g1[h].lds + c] += sw;
-    Ga[n.b1[h].lds + c] += sb;
-  }
-  for (int i = t; i < n.nout * UPD_H; i += UPD_THREADS) {   // dW2 += dO^T G
-    const int j = i >> 6, c = i & 63;
-    const int h = upd_head_of(n, j), k = j - n.ocol[h];
-    float acc = 0.f;
-#pragma unroll
-    for (int r = 0; r < UPD_RC; ++r)
-      if (r < rc) acc += a.dO[r * a.OX + j] * a.Gh(h)[r * UPD_HS + c];
-    Ga[n.w2[h].lds + k * UPD_HS + c] += acc;
-  }
-  if (t < n.nout) {   // db2
-    const int h = upd_head_of(n, t);
-    float acc = 0.f;
-    for (int r = 0; r < rc; ++r) acc += a.dO[r * a.OX + t];
-    Ga[n.b2[h].lds + (t - n.ocol[h])] += acc;
-  }
-  if (t >= 64 && t < 64 + 3) {   // loss partials
-    const int which = t - 64;
-    float acc = 0.f;
-    for (int r = 0; r < rc; ++r) acc += a.lossp[r * 4 + which];
-    Ga[n.Lp + which] += acc;
-  }
-  for (int it = t; it < nh * rc * 16; it += UPD_THREADS) {   // dF_h = dZ_h W1_h
-    const int h = it / (rc * 16), rem = it % (rc * 16), r = rem >> 4, c4 = (rem & 15) * 4;
-    const float* dz = a.ZB(h) + r * UPD_HS;
-    const float* w = W + n.w1[h].lds + c4;
-    float4 acc = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int o = 0; o < UPD_H; o += 4) {
-      const float4 z4 = *reinterpret_cast<const float4*>(dz + o);
-      const float zz[4] = {z4.x, z4.y, z4.z, z4.w};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 w4 = *reinterpret_cast<const float4*>(w + (o + u) * UPD_HS);
-        acc.x += zz[u] * w4.x;
-        acc.y += zz[u] * w4.y;
-        acc.z += zz[u] * w4.z;
-        acc.w += zz[u] * w4.w;
-      }
-    }
-    *reinterpret_cast<float4*>(a.dF(h) + r * UPD_HS + c4) = acc;
-  }
-  __syncthreads();
   UPD_CMARK(5)
-  // S6. trunk GroupNorm + SiLU backward (lanes = channels): dF = sum_h dF_h
-  for (int r = wv; r < rc; r += 4) {
-    float df = 0.f;
-    for (int h = 0; h < nh; ++h) df += a.dF(h)[r * UPD_HS + o];
-    a.DU0[r * UPD_HS + o] = upd_gn_bwd_lane(df, a.XH0[r * UPD_HS + o], W[n.g0.lds + o],
-                                            W[n.b0.lds + o], a.rstd0[r * 8 + (o >> 3)],
-                                            a.T0 + r * UPD_HS + o);
-  }
-  __syncthreads();
-  UPD_CMARK(6)
-  // S7. dW0 += dH0^T X;  trunk GroupNorm weight / bias
-  for (int i = t; i < UPD_H * D; i += UPD_THREADS) {
-    const int o = i / D, d = i % D;
-    float acc = 0.f;
+  // ---- dF^T block w = sum_h W1_h^T dZ_h^T (K = 64 head channels, permuted so that the A reads
+  //      are conflict-free: step s, lane q <-> channel 16 (s & 3) + 4 q + (s >> 2))
+  upd_v4 dF;
+  {
+    upd_v4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < UPD_RC; ++r)
-      if (r < rc) acc += a.T0[r * UPD_HS + o] * a.X[r * a.DX + d];
-    Ga[n.w0.lds + o * n.w0.stride + d] += acc;
-  }
-  if (t < UPD_H) {
-    float sw = 0.f, sb = 0.f;
+    for (int h = 0; h < UPD_MAXH; ++h) {
+      if (h < nh) {
+        const float* Zh = sc.Zs + h * UPD_RT * UPD_ZS + x * UPD_ZS;
+        const float* Wh = W + n.w1[h].lds + 16 * w + x;
 #pragma unroll
-    for (int r = 0; r < UPD_RC; ++r) {
-      if (r >= rc) break;
-      const float du = a.DU0[r * UPD_HS + t];
-      sw += du * a.XH0[r * UPD_HS + t];
-      sb += du;
+        for (int s = 0; s < 16; ++s) {
+          const int o = 16 * (s & 3) + 4 * q + (s >> 2);
+          if (s & 1) d1 = upd_mma(Wh[o * UPD_HS], Zh[o], d1);
+          else d0 = upd_mma(Wh[o * UPD_HS], Zh[o], d0);
+        }
+      }
     }
-    Ga[n.g0.lds + t] += sw;
-    Ga[n.b0.lds + t] += sb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dF[i] = d0[i] + d1[i];
   }
-  __syncthreads();
+  // trunk GroupNorm + SiLU backward -> dH0 (block w), its weight / bias gradients
+  upd_v4 dy0;
+  const upd_v4 dH0 = upd_gn_bwd_frag(dF, f.xh0, upd_ld4(W + n.g0.lds + 16 * w + 4 * q),
+                                     upd_ld4(W + n.b0.lds + 16 * w + 4 * q), f.r0, dy0);
+  {
+    upd_v4 dyx;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dyx[i] = dy0[i] * f.xh0[i];
+    upd_colsum_add(dyx, Ga + n.g0.lds + 16 * w + 4 * q, x == 0);
+    upd_colsum_add(dy0, Ga + n.b0.lds + 16 * w + 4 * q, x == 0);
+  }
+  UPD_CMARK(6)
+  // ---- dW0[16w + 4q + i][16e + x] += sum_rows dH0[row][ch] X[row][d]  (dH0 transposed via Tw)
+  upd_st4(Tw + x * 16 + 4 * q, dH0);
+  upd_wave_sync();
+#pragma unroll
+  for (int e = 0; e < (KSM + 3) / 4; ++e) {
+    if (16 * e < D) {
+      upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int d = 16 * e + x;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        acc = upd_mma(Tw[(4 * s + q) * 16 + x], d < D ? sc.Xs[(4 * s + q) * sc.XS + d] : 0.0f, acc);
+      if (d < D) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ga[n.w0.lds + (16 * w + 4 * q + i) * n.w0.stride + d] += acc[i];
+      }
+    }
+  }
+  // ---- output biases and loss partials (wave 0)
+  if (w == 0) {
+    if (t < n.nout) {   // f64 sum: the softmax outputs' dO cancel across rows
+      double acc = 0.0;
+#pragma unroll
+      for (int r = 0; r < UPD_RT; ++r) acc += (double)dOw[r * 16 + t];
+      Ga[upd_bias_of(n, t)] += (float)acc;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float s = upd_rsum16(lp[k]);
+      if (t == 0) Ga[n.Lp + k] += s;
+    }
+  }
+  upd_wave_sync();   // Tw reads done before the next tile
   UPD_CMARK(7)
 #undef UPD_CMARK
 }
@@ -746,6 +759,61 @@ __device__ inline float f4get(const float4& v, int e) {
 }
 __device__ inline void f4set(float4& v, int e, float x) {
   if (e == 0) v.x = x; else if (e == 1) v.y = x; else if (e == 2) v.z = x; else v.w = x;
+}
+
+// Phase B: workgroup g sums its slice [qlo, qhi) of the gradient quads over the G partials in
+// workgroup order (deterministic) with float64 accumulators (the partials of the output biases
+// cancel across workgroups), publishes the slice (sc1) and returns this thread's share of the
+// slice's sum of squares (parameter quads only).  Uses scratch as [spl][nq] double4.
+__device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_red,
+                                         int Qtot, int Qp, int g, int G, float* scratch) {
+  const int t = threadIdx.x;
+  const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
+  const int nq = qhi - qlo;
+  float ssq = 0.f;
+  auto fin = [&](int qi, double ax, double ay, double az, double aw) {
+    const float4 r = float4{(float)ax, (float)ay, (float)az, (float)aw};
+    st4_sc1(rs_red, (size_t)(qlo + qi) * 4, r);
+    if (qlo + qi < Qp) ssq += r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w;
+  };
+  if (nq > UPD_THREADS / 2) {
+    // wide slices (few workgroups): each thread owns whole quads, partials summed in order
+    for (int qi = t; qi < nq; qi += UPD_THREADS) {
+      double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
+#pragma unroll 8
+      for (int gg = 0; gg < G; ++gg) {
+        const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
+        ax += v.x; ay += v.y; az += v.z; aw += v.w;
+      }
+      fin(qi, ax, ay, az, aw);
+    }
+  } else if (nq > 0) {
+    // narrow slices: split the G partials of each quad over spl threads, combine in LDS
+    int spl = 1;
+    while (spl * 2 * nq <= UPD_THREADS && spl * 2 <= G) spl *= 2;
+    double* red = reinterpret_cast<double*>(scratch);   // [spl][nq][4]
+    if (t < spl * nq) {
+      const int qi = t % nq, sub = t / nq;
+      double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
+#pragma unroll 16
+      for (int gg = sub; gg < G; gg += spl) {
+        const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
+        ax += v.x; ay += v.y; az += v.z; aw += v.w;
+      }
+      double* o = red + 4 * (sub * nq + qi);
+      o[0] = ax; o[1] = ay; o[2] = az; o[3] = aw;
+    }
+    __syncthreads();
+    if (t < nq) {
+      double ax = red[4 * t], ay = red[4 * t + 1], az = red[4 * t + 2], aw = red[4 * t + 3];
+      for (int sub = 1; sub < spl; ++sub) {
+        const double* o = red + 4 * (sub * nq + t);
+        ax += o[0]; ay += o[1]; az += o[2]; aw += o[3];
+      }
+      fin(t, ax, ay, az, aw);
+    }
+  }
+  return ssq;
 }
 
 // NQ = parameter quads per thread (ceil(Lp / 4 / 256)): AdamW's moments live in registers.
@@ -761,8 +829,8 @@ ppo_update_kernel(UpdArgs args) {
   float* hdr = upd_lds;             // [64] broadcast words + chunk stage timers
   float* W = upd_lds + 64;          // [Lp]
   float* Ga = W + Lp;               // [Lp + 4]
-  float* scratch = Ga + Lp + 4;     // activations / reduction scratch
-  const UpdAct a = upd_carve(scratch, n);
+  float* scratch = Ga + Lp + 4;     // tile activations / reduction scratch
+  const UpdScr sc = upd_scr(scratch, n.D);
   float* s_bcast = hdr;             // [0] clip coefficient, [1] loss
   float* s_ssq = hdr + 4;           // [4] per-wave sums of squares
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
@@ -817,9 +885,10 @@ ppo_update_kernel(UpdArgs args) {
     // ---- phase A: partial gradient of this workgroup's rows ------------------------------------
     for (int k = t; k < Lp + 4; k += UPD_THREADS) Ga[k] = 0.0f;
     __syncthreads();
-    for (int c0 = 0; c0 < myrows; c0 += UPD_RC)
-      upd_chunk<KD, KA>(args, W, Ga, a, mb0 + (int64_t)g * R + c0, std::min(UPD_RC, myrows - c0), invB,
-                reinterpret_cast<unsigned long long*>(hdr + 16));
+    for (int c0 = 0; c0 < myrows; c0 += UPD_RT)
+      upd_tile<KD, KA>(args, W, Ga, sc, mb0 + (int64_t)g * R + c0, std::min(UPD_RT, myrows - c0), invB,
+                       reinterpret_cast<unsigned long long*>(hdr + 16));
+    __syncthreads();
     mark(0);   // phase A compute
     const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(args.red);
     for (int q = t; q < Qtot; q += UPD_THREADS)
@@ -834,49 +903,9 @@ ppo_update_kernel(UpdArgs args) {
     __syncthreads();
     if (*s_abort) return;
     mark(2);   // wait A
-    // ---- phase B: reduce slice [qlo, qhi) over the G partials (workgroup order) ---------------
+    // ---- phase B: reduce this workgroup's slice over the G partials --------------------------
     {
-      const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
-      const int nq = qhi - qlo;
-      float ssq = 0.f;
-      if (nq > UPD_THREADS / 2) {
-        // wide slices (few workgroups): each thread owns whole quads, partials summed in order
-        for (int qi = t; qi < nq; qi += UPD_THREADS) {
-          float4 acc = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-          for (int gg = 0; gg < G; ++gg) {
-            const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
-            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-          }
-          st4_sc1(rs_red, (size_t)(qlo + qi) * 4, acc);
-          if (qlo + qi < Qp) ssq += acc.x * acc.x + acc.y * acc.y + acc.z * acc.z + acc.w * acc.w;
-        }
-      } else if (nq > 0) {
-        // narrow slices: split the G partials of each quad over spl threads, combine in LDS
-        int spl = 1;
-        while (spl * 2 * nq <= UPD_THREADS && spl * 2 <= G) spl *= 2;
-        float4* red4 = reinterpret_cast<float4*>(scratch);   // [spl][nq]
-        if (t < spl * nq) {
-          const int qi = t % nq, sub = t / nq;
-          float4 acc = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 16
-          for (int gg = sub; gg < G; gg += spl) {
-            const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
-            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-          }
-          red4[sub * nq + qi] = acc;
-        }
-        __syncthreads();
-        if (t < nq) {
-          float4 acc = red4[t];
-          for (int sub = 1; sub < spl; ++sub) {
-            const float4 v = red4[sub * nq + t];
-            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-          }
-          st4_sc1(rs_red, (size_t)(qlo + t) * 4, acc);
-          if (qlo + t < Qp) ssq = acc.x * acc.x + acc.y * acc.y + acc.z * acc.z + acc.w * acc.w;
-        }
-      }
+      float ssq = upd_slice_reduce(rs_part, rs_red, Qtot, Qp, g, G, scratch);
       // block sum of ssq (threads < nq hold the pieces; fixed order)
       ssq = wave_sum_f32_to63(ssq);
       if ((t & 63) == 63) s_ssq[t >> 6] = ssq;
@@ -1014,27 +1043,30 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_evaluate_kernel(UpdArgs ar
                                                                     float* V_out, float* H_out) {
   extern __shared__ __align__(16) float upd_lds[];
   const UpdNet& n = args.net;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   float* W = upd_lds + 64;
-  const UpdAct a = upd_carve(W + n.Lp, n);
+  const UpdScr sc = upd_scr(W + n.Lp, n.D);
   for (int k = t; k < n.Lp; k += UPD_THREADS) {
     const int f = upd_flat_of(n, k);
     W[k] = f >= 0 ? args.params[f] : 0.0f;
   }
   __syncthreads();
-  unsigned long long tl = 0;
-  const int64_t nchunks = (args.N + UPD_RC - 1) / UPD_RC;
-  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    const int64_t row0 = c * UPD_RC;
-    const int rc = (int)std::min<int64_t>(UPD_RC, args.N - row0);
-    upd_forward(n, W, a, args.S, args.act, row0, rc, nullptr, false, tl);
-    const int r = t >> 5, l = t & 31;
-    if (l == 0 && r < rc) {
-      UpdDist d;
-      upd_row_dist<KD, KA>(n, a.O + r * a.OX, a.Ar + r * a.AX, d);
-      logp_out[row0 + r] = d.logp;
-      V_out[row0 + r] = a.O[r * a.OX + n.ocol[n.nh - 1]];
-      if (H_out) H_out[row0 + r] = d.H;
+  const int64_t ntiles = (args.N + UPD_RT - 1) / UPD_RT;
+  for (int64_t c = blockIdx.x; c < ntiles; c += gridDim.x) {
+    const int64_t row0 = c * UPD_RT;
+    const int rc = (int)std::min<int64_t>(UPD_RT, args.N - row0);
+    UpdFwd<upd_ksm<KA>()> f;
+    upd_tile_fwd<KD, KA>(n, W, sc, args.S, args.act, nullptr, nullptr, nullptr, row0, rc, f);
+    __syncthreads();
+    if (w == 0) {
+      const float* Orow = upd_tile_outputs(n, W, sc);
+      if (q == 0 && x < rc) {
+        UpdDist d;
+        upd_row_dist<KD, KA>(n, Orow, sc.Rin + x * UPD_RIN, d);
+        logp_out[row0 + x] = d.logp;
+        V_out[row0 + x] = Orow[n.discrete ? n.A : 2 * n.A];   // critic output column
+        if (H_out) H_out[row0 + x] = d.H;
+      }
     }
     __syncthreads();
   }
@@ -1060,7 +1092,7 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_grad_kernel(UpdArgs args, 
   float* W = upd_lds + 64;
   float* Ga = W + Lp;
   float* scratch = Ga + Lp + 4;
-  const UpdAct a = upd_carve(scratch, n);
+  const UpdScr sc = upd_scr(scratch, n.D);
   float* s_ssq = hdr + 4;
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
   unsigned long long* tm = reinterpret_cast<unsigned long long*>(hdr + 16);
@@ -1071,9 +1103,10 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_grad_kernel(UpdArgs args, 
   __syncthreads();
   const int R = args.R;
   const int myrows = std::max(0, std::min(R, B_local - g * R));
-  for (int c0 = 0; c0 < myrows; c0 += UPD_RC)
-    upd_chunk<KD, KA>(args, W, Ga, a, row0 + (int64_t)g * R + c0, std::min(UPD_RC, myrows - c0),
-                      inv_count, tm);
+  for (int c0 = 0; c0 < myrows; c0 += UPD_RT)
+    upd_tile<KD, KA>(args, W, Ga, sc, row0 + (int64_t)g * R + c0, std::min(UPD_RT, myrows - c0),
+                     inv_count, tm);
+  __syncthreads();
   const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(grad_out);
   for (int q = t; q < Qtot; q += UPD_THREADS)
     st4_sc1(rs_part, ((size_t)g * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
@@ -1085,42 +1118,7 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_grad_kernel(UpdArgs args, 
   }
   __syncthreads();
   if (*s_abort) return;
-  const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
-  const int nq = qhi - qlo;
-  if (nq > UPD_THREADS / 2) {
-    for (int qi = t; qi < nq; qi += UPD_THREADS) {
-      float4 acc = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-      for (int gg = 0; gg < G; ++gg) {
-        const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
-      st4_sc1(rs_red, (size_t)(qlo + qi) * 4, acc);
-    }
-  } else if (nq > 0) {
-    int spl = 1;
-    while (spl * 2 * nq <= UPD_THREADS && spl * 2 <= G) spl *= 2;
-    float4* red4 = reinterpret_cast<float4*>(scratch);
-    if (t < spl * nq) {
-      const int qi = t % nq, sub = t / nq;
-      float4 acc = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-      for (int gg = sub; gg < G; gg += spl) {
-        const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
-      red4[sub * nq + qi] = acc;
-    }
-    __syncthreads();
-    if (t < nq) {
-      float4 acc = red4[t];
-      for (int sub = 1; sub < spl; ++sub) {
-        const float4 v = red4[sub * nq + t];
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
-      st4_sc1(rs_red, (size_t)(qlo + t) * 4, acc);
-    }
-  }
+  upd_slice_reduce(rs_part, rs_red, Qtot, Qp, g, G, scratch);
   (void)s_ssq;
 }
 
@@ -1242,6 +1240,7 @@ bool upd_layout(int D, int A, int discrete, UpdNet& n) {
     add(n.b2[h], 1, out, out);
   }
   n.nout = col;
+  if (n.nout > UPD_MAXO) return false;   // one 16-row output tile
   n.P = flat;
   n.Lp = lds;
   return true;
@@ -1252,28 +1251,26 @@ int upd_nq(const UpdNet& n) { return (int)cdiv(n.Lp / 4, UPD_THREADS); }
 // A = 1); every other shape runs the generic (runtime head configuration) kernel.
 const void* upd_kernel_for(const UpdNet& n) {
   const int nq = upd_nq(n);
-  if (n.discrete && n.A == 2 && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2>);
-  if (!n.discrete && n.A == 1 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1>);
+  if (n.discrete && n.A == 2 && n.D <= 16 && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2>);
+  if (!n.discrete && n.A == 1 && n.D <= 16 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1>);
   if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0>);
   return nullptr;
 }
 const void* upd_grad_kernel_for(const UpdNet& n) {
-  if (n.discrete && n.A == 2) return reinterpret_cast<const void*>(ppo_grad_kernel<1, 2>);
-  if (!n.discrete && n.A == 1) return reinterpret_cast<const void*>(ppo_grad_kernel<0, 1>);
+  if (n.discrete && n.A == 2 && n.D <= 16) return reinterpret_cast<const void*>(ppo_grad_kernel<1, 2>);
+  if (!n.discrete && n.A == 1 && n.D <= 16) return reinterpret_cast<const void*>(ppo_grad_kernel<0, 1>);
   return reinterpret_cast<const void*>(ppo_grad_kernel<-1, 0>);
 }
 const void* upd_eval_kernel_for(const UpdNet& n) {
-  if (n.discrete && n.A == 2) return reinterpret_cast<const void*>(ppo_evaluate_kernel<1, 2>);
-  if (!n.discrete && n.A == 1) return reinterpret_cast<const void*>(ppo_evaluate_kernel<0, 1>);
+  if (n.discrete && n.A == 2 && n.D <= 16) return reinterpret_cast<const void*>(ppo_evaluate_kernel<1, 2>);
+  if (!n.discrete && n.A == 1 && n.D <= 16) return reinterpret_cast<const void*>(ppo_evaluate_kernel<0, 1>);
   return reinterpret_cast<const void*>(ppo_evaluate_kernel<-1, 0>);
 }
 
-int upd_grid(int64_t mb) { return (int)std::min<int64_t>(256, cdiv(mb, UPD_RC)); }
+int upd_grid(int64_t mb) { return (int)std::min<int64_t>(256, cdiv(mb, UPD_RT)); }
 
 size_t upd_lds_bytes(const UpdNet& n) {
-  int DX, AX, OX;
-  const int act = upd_act_floats(n.D, n.A, n.nout, DX, AX, OX);
-  return sizeof(float) * (size_t)(64 + 2 * n.Lp + 4 + act);
+  return sizeof(float) * (size_t)(64 + 2 * n.Lp + 4 + upd_scratch_floats(n.D));
 }
 
 struct UpdWs {
@@ -1351,7 +1348,7 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
   args.nb = (int)nb;
   args.total_steps = (int)(nb * k_epochs);
   args.G = G;
-  args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RC) * UPD_RC;
+  args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RT) * UPD_RT;
   args.clip = clip;
   args.vf_coef = vf_coef;
   args.ent_coef = ent_coef;
@@ -1395,11 +1392,9 @@ extern "C" int prl_ppo_evaluate(const float* params, int32_t D, int32_t A, int32
   args.S = S;
   args.act = actions;
   args.N = N;
-  int DX, AX, OX;
-  const size_t lds = sizeof(float) * (size_t)(64 + args.net.Lp +
-                                              upd_act_floats(D, A, args.net.nout, DX, AX, OX));
+  const size_t lds = sizeof(float) * (size_t)(64 + args.net.Lp + upd_scratch_floats(D));
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_evaluate: %zu B of LDS needed", lds);
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(N, UPD_RC), 2 * 256);
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(N, UPD_RT), 2 * 256);
   const void* kern = upd_eval_kernel_for(args.net);
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   void* kargs[] = {&args, &logp, &V, &entropy};
@@ -1452,7 +1447,7 @@ extern "C" int prl_ppo_grad_step(const float* img_params, int32_t D, int32_t A, 
   args.N = N;
   args.mb = mini_batch;
   args.G = G;
-  args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RC) * UPD_RC;
+  args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RT) * UPD_RT;
   args.clip = clip;
   args.vf_coef = vf_coef;
   args.part = ws.part;

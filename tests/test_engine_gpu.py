@@ -74,15 +74,18 @@ def _compare(pf, pg, atol=ATOL, loss_rtol=1e-4):
     return worst
 
 
-def _grad_f64(ppo, data, clip_eps=0.2, vf=0.5, ent=0.01):
+def _grad_f64(ppo, data, clip_eps=0.2, vf=0.5, ent=0.01, logp_val=None):
     """float64 CPU autograd of the reference loss (PPO.py:216-249) for ONE minibatch = all rows,
     with old_logp / adv / ret recomputed exactly as learn() does (GAE oracle on the GPU's f32
-    old values is not needed: the same device tensors are reused)."""
+    old values is not needed: the same device tensors are reused).  logp_val: use these
+    (float32) log-prob VALUES in the ratio (the gradient flows through the f64 log-probs)."""
     import copy
     from torch import nn
     S, A, old_logp, adv, ret = data
     pol = copy.deepcopy(ppo.policy).cpu().double()
     logp, V, H = pol.get_evaluate(S.cpu().double(), A.cpu().double())
+    if logp_val is not None:
+        logp = logp - logp.detach() + logp_val.cpu().double()
     ratio = torch.exp(torch.clamp(logp - old_logp.cpu().double(), -20, 20))
     a = adv.cpu().double()
     s1 = ratio * a
@@ -117,6 +120,27 @@ def test_fused_gradient_matches_autograd(cont):
     assert worst["fused"] <= 1e-4 and worst["graph"] <= 1e-4, worst
 
 
+def _away_from_kinks(ppo, S, A, old, clip=0.2, gap=1e-3):
+    """The surrogate's gradient jumps where a ratio crosses 1 +- clip (or the log-ratio crosses
+    the +-20 clamp): a row within float32 noise of a kink may take either branch in any valid
+    float32 implementation (continuous log-probs reach |logp| ~ 100, so that noise is ~1e-5 in
+    the ratio).  Nudge such rows' old log-probs off the kink (float64 ratios)."""
+    import copy
+    pol = copy.deepcopy(ppo.policy).cpu().double()
+    with torch.no_grad():
+        logp, _, _ = pol.get_evaluate(S.cpu().double(), A.cpu().double())
+    old64 = old.cpu().double()
+    for _ in range(4):
+        diff = logp - old64
+        ratio = torch.exp(torch.clamp(diff, -20, 20))
+        near = ((ratio - (1 - clip)).abs() < gap) | ((ratio - (1 + clip)).abs() < gap) | \
+               ((diff.abs() - 20).abs() < gap)
+        if not bool(near.any()):
+            break
+        old64 = torch.where(near, old64 + 10 * gap, old64)
+    return old64.to(old.dtype).to(old.device)
+
+
 @pytest.mark.parametrize("cont", [False, True])
 @pytest.mark.parametrize("spread,rows", [(0.3, 512), (3.0, 512), (30.0, 512), (3.0, 405),
                                          (3.0, 100)])
@@ -129,13 +153,25 @@ def test_fused_gradient_off_policy(cont, spread, rows):
     p = _run(True, cont, (S, Aa, R, Dn), 512, 1, lr=0.0)
     S_, A_, old, adv, ret = p._last_update_inputs
     g = torch.Generator(device="cuda").manual_seed(3)
-    old2 = old + spread * torch.randn(old.shape, device="cuda", generator=g)
+    old2 = _away_from_kinks(p, S_, A_, old + spread * torch.randn(old.shape, device="cuda", generator=g))
     eng = p._engine
     eng.m.zero_()
     eng.v.zero_()
     eng.step.zero_()
+    # Continuous log-probs reach |logp| ~ 100 (narrow sigma): their float32 rounding (~5e-5
+    # absolute, the same for CPU float32) moves every ratio by ~5e-5 relative, which the
+    # cancelling sums of the mu gradients amplify past 1e-4.  So the forward is checked on its
+    # own (log-prob error relative to max |logp|, CPU float32 reaches 4e-7 here) and the
+    # backward against float64 autograd of the loss at the engine's own log-prob values.
+    logp_eng, _ = eng.evaluate(p.policy, S_, A_)
+    import copy
+    with torch.no_grad():
+        l64, _, _ = copy.deepcopy(p.policy).cpu().double().get_evaluate(S_.cpu().double(),
+                                                                          A_.cpu().double())
+    fwd = float((logp_eng.cpu().double() - l64).abs().max()) / (1.0 + float(l64.abs().max()))
+    assert fwd <= 2e-6, fwd
     eng.run(S_, A_, old2, adv, ret, 1)
-    g64 = _grad_f64(p, (S_, A_, old2, adv, ret))
+    g64 = _grad_f64(p, (S_, A_, old2, adv, ret), logp_val=logp_eng)
     per = {}
     for (name, prm), gr in zip(p.policy.named_parameters(), g64):
         m = p.optimizer.state[prm]["exp_avg"].double().cpu() / 0.1
