@@ -135,7 +135,14 @@ __device__ inline bool upd_wait(unsigned* ctr, int which, unsigned target) {
   }
 }
 
-__device__ inline float upd_sigmoid(float y) { return 1.0f / (1.0f + expf(-y)); }
+// Hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32 / v_rsq_f32, ~1 ulp) for the
+// engine's per-row and per-channel math: the forward's log-probs stay within float32 rounding of
+// float64 (tests/test_engine_gpu.py checks them), and evaluate/update share these helpers, so the
+// first minibatch's ratio is still exactly 1.
+__device__ inline float upd_exp(float x) { return __expf(x); }
+__device__ inline float upd_log(float x) { return __logf(x); }
+__device__ inline float upd_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ inline float upd_sigmoid(float y) { return upd_rcp(1.0f + upd_exp(-y)); }
 
 // flat index of LDS-image entry k (-1 = padding)
 __device__ inline bool upd_in(const UpdTensor& t, int k, int& f) {
@@ -223,24 +230,26 @@ __device__ inline void upd_row_dist(const UpdNet& n, const float* O, const float
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < UPD_MAXA; ++k) {
-      d.p[k] = k < A ? expf(O[k] - mx) : 0.f;
+      d.p[k] = k < A ? upd_exp(O[k] - mx) : 0.f;
       s += d.p[k];
     }
+    const float rs = upd_rcp(s);
 #pragma unroll
     for (int k = 0; k < UPD_MAXA; ++k) {
-      d.p[k] = k < A ? d.p[k] / s : 0.f;
+      d.p[k] = k < A ? d.p[k] * rs : 0.f;
       d.S2 += d.p[k];
     }
+    const float rS2 = upd_rcp(d.S2);
     d.ai = (int)act[0];
     const bool bad = d.ai < 0 || d.ai >= A;   // torch's gather would raise: poison instead
     float la = 0.f;
 #pragma unroll
     for (int k = 0; k < UPD_MAXA; ++k) {
-      d.q[k] = d.p[k] / d.S2;
+      d.q[k] = d.p[k] * rS2;
       if (k < A) {
         const float c = d.q[k] < FLT_EPSILON ? FLT_EPSILON
                                              : (d.q[k] > 1.0f - FLT_EPSILON ? 1.0f - FLT_EPSILON : d.q[k]);
-        const float l = logf(c);
+        const float l = upd_log(c);
         d.H += l * d.q[k];
         if (k == d.ai) { la = l; d.qa = d.q[k]; }
       }
@@ -255,10 +264,10 @@ __device__ inline void upd_row_dist(const UpdNet& n, const float* O, const float
         const float mu = O[k];
         const float lsr = O[A + k];
         const float lsc = lsr < -2.0f ? -2.0f : (lsr > 2.0f ? 2.0f : lsr);
-        const float sd = log1pf(expf(lsc));               // softplus, beta 1 (lsc <= 2 < 20)
+        const float sd = upd_log(1.0f + upd_exp(lsc));   // softplus, beta 1 (lsc <= 2 < 20)
         const float dd = act[k] - mu;
-        const float lsd = logf(sd);
-        d.logp += -(dd * dd) / (2.0f * (sd * sd)) - lsd - half_log_2pi;
+        const float lsd = upd_log(sd);
+        d.logp += -(dd * dd) * upd_rcp(2.0f * (sd * sd)) - lsd - half_log_2pi;
         d.H += 0.5f + half_log_2pi + lsd;
       }
     }
@@ -284,7 +293,7 @@ __device__ inline void upd_row_loss(const UpdNet& n, const float* O, const float
   // surrogate
   const float diff = logp - rin[8];
   const float cl = diff < -20.0f ? -20.0f : (diff > 20.0f ? 20.0f : diff);
-  const float ratio = expf(cl);
+  const float ratio = upd_exp(cl);
   const float adv = rin[9];
   const float s1 = ratio * adv;
   const float lo = 1.0f - clip, hi = 1.0f + clip;
@@ -312,9 +321,10 @@ __device__ inline void upd_row_loss(const UpdNet& n, const float* O, const float
     const float gq = (logp != logp) ? logp : dlogp * mk;
     float dp[UPD_MAXA];
     float dot = 0.f;
+    const float rqa = upd_rcp(qa), rS2 = upd_rcp(S2);
 #pragma unroll
     for (int k = 0; k < UPD_MAXA; ++k) {
-      dp[k] = k < A ? gq * (((k == ai) ? 1.0f / qa : 0.0f) - 1.0f) / S2 : 0.f;
+      dp[k] = k < A ? gq * (((k == ai) ? rqa : 0.0f) - 1.0f) * rS2 : 0.f;
       dot += p[k] * dp[k];
     }
 #pragma unroll
@@ -327,11 +337,12 @@ __device__ inline void upd_row_loss(const UpdNet& n, const float* O, const float
         const float mu = O[k];
         const float lsr = O[A + k];
         const float lsc = lsr < -2.0f ? -2.0f : (lsr > 2.0f ? 2.0f : lsr);
-        const float sd = log1pf(expf(lsc));
+        const float sd = upd_log(1.0f + upd_exp(lsc));
         const float d = rin[k] - mu;
         const float var = sd * sd;
-        dO[k] = dlogp * (d / var);
-        const float dsd = dlogp * ((d * d) / (var * sd) - 1.0f / sd);
+        const float rvar = upd_rcp(var), rsd = upd_rcp(sd);
+        dO[k] = dlogp * (d * rvar);
+        const float dsd = dlogp * ((d * d) * (rvar * rsd) - rsd);
         const float pass = (lsr >= -2.0f && lsr <= 2.0f) ? 1.0f : 0.0f;
         dO[A + k] = dsd * upd_sigmoid(lsc) * pass;
       }
@@ -387,12 +398,12 @@ __device__ inline void upd_gn_fwd_frag(upd_v4 z, upd_v4 gw, upd_v4 gb, upd_v4& x
 #pragma unroll
   for (int i = 0; i < 4; ++i) d[i] = z[i] - mean;
   const float q4 = (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
-  rstd = 1.0f / sqrtf((q4 + upd_p16(q4)) * 0.125f + 1e-5f);
+  rstd = __builtin_amdgcn_rsqf((q4 + upd_p16(q4)) * 0.125f + 1e-5f);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     xh[i] = d[i] * rstd;
     const float u = xh[i] * gw[i] + gb[i];
-    y[i] = u / (1.0f + expf(-u));
+    y[i] = u * upd_sigmoid(u);
   }
 }
 // backward of the above: go = d(block output); returns dX, dy = d(pre-SiLU) (for dγ, dβ)
@@ -437,10 +448,43 @@ struct UpdFwd {
   float r0;                          // trunk rstd (block w)
   upd_v4 xh[UPD_MAXH], G[UPD_MAXH];  // head xhat / output (block w)
   float rh[UPD_MAXH];
-  float xin[KSM];                    // B fragments of the inputs: X[row x][4 s + q]
 };
 template <int KA>
 constexpr int upd_ksm() { return KA > 0 ? 4 : 16; }
+
+// A tile's global inputs, loaded into registers ahead of the tile (prefetch): the B fragments
+// of the observations X[row x][4 s + q] and one word of the row-input record (thread t < 192:
+// row t / 12, field t % 12 = act[0..7], old_logp, adv, ret, pad).
+template <int KSM>
+struct UpdIn {
+  float xin[KSM];
+  float rin;
+};
+template <int KD, int KA>
+__device__ inline void upd_tile_load(const UpdNet& n, const float* Sg, const float* actg,
+                                     const float* oldg, const float* advg, const float* retg,
+                                     int64_t row0, int rc, UpdIn<upd_ksm<KA>()>& in) {
+  constexpr int KSM = upd_ksm<KA>();
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4;
+  const int D = n.D, KS = (D + 3) >> 2;
+  const bool rowok = x < rc;
+#pragma unroll
+  for (int s = 0; s < KSM; ++s) {
+    const int d = 4 * s + q;
+    in.xin[s] = (s < KS && rowok && d < D) ? Sg[(row0 + x) * D + d] : 0.0f;
+  }
+  in.rin = 0.f;
+  if (t < UPD_RT * UPD_RIN) {
+    const int r = t / UPD_RIN, k = t % UPD_RIN;
+    const int Aw = n.discrete ? 1 : n.A;
+    if (r < rc) {
+      if (k < UPD_MAXA) in.rin = k < Aw ? actg[(row0 + r) * Aw + k] : 0.0f;
+      else if (k == 8 && oldg) in.rin = oldg[row0 + r];
+      else if (k == 9 && advg) in.rin = advg[row0 + r];
+      else if (k == 10 && retg) in.rin = retg[row0 + r];
+    }
+  }
+}
 
 // Forward of one tile (rows row0 .. row0 + rc - 1, rc <= 16) up to the output-layer partials:
 // every wave runs the trunk for all 64 channels (it is the B operand of every head block), then
@@ -449,31 +493,11 @@ constexpr int upd_ksm() { return KA > 0 ? 4 : 16; }
 // the caller's barrier publishes Op / Rin.
 template <int KD, int KA>
 __device__ inline void upd_tile_fwd(const UpdNet& n, const float* W, const UpdScr& sc,
-                                    const float* Sg, const float* actg, const float* oldg,
-                                    const float* advg, const float* retg, int64_t row0, int rc,
-                                    UpdFwd<upd_ksm<KA>()>& f) {
+                                    const UpdIn<upd_ksm<KA>()>& in, UpdFwd<upd_ksm<KA>()>& f) {
   constexpr int KSM = upd_ksm<KA>();
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   const int D = n.D, KS = (D + 3) >> 2;
   const int nh = upd_nh<KD>(n);
-  const bool rowok = x < rc;
-  // global loads first (their latency runs under the trunk's LDS reads)
-#pragma unroll
-  for (int s = 0; s < KSM; ++s) {
-    const int d = 4 * s + q;
-    f.xin[s] = (s < KS && rowok && d < D) ? Sg[(row0 + x) * D + d] : 0.0f;
-  }
-  float rin = 0.f;
-  if (t < UPD_RT * UPD_RIN) {
-    const int r = t / UPD_RIN, k = t % UPD_RIN;
-    const int Aw = n.discrete ? 1 : n.A;
-    if (r < rc) {
-      if (k < UPD_MAXA) rin = k < Aw ? actg[(row0 + r) * Aw + k] : 0.0f;
-      else if (k == 8 && oldg) rin = oldg[row0 + r];
-      else if (k == 9 && advg) rin = advg[row0 + r];
-      else if (k == 10 && retg) rin = retg[row0 + r];
-    }
-  }
   // trunk: H0^T block b = W0[16b .. 16b+15][:] X^T  (A: W0 rows, B: inputs), then GN + SiLU
   upd_v4 F[4];
 #pragma unroll
@@ -484,7 +508,7 @@ __device__ inline void upd_tile_fwd(const UpdNet& n, const float* W, const UpdSc
     for (int s = 0; s < KSM; ++s) {
       if (s < KS) {
         const int d = 4 * s + q;
-        acc = upd_mma(d < D ? wr[d] : 0.0f, f.xin[s], acc);
+        acc = upd_mma(d < D ? wr[d] : 0.0f, in.xin[s], acc);
       }
     }
     upd_v4 xh;
@@ -534,7 +558,7 @@ __device__ inline void upd_tile_fwd(const UpdNet& n, const float* W, const UpdSc
     }
   }
   upd_st4(sc.Op + (w * 16 + x) * 16 + 4 * q, o);   // [w][row x][j = 4q + i]
-  if (t < UPD_RT * UPD_RIN) sc.Rin[t] = rin;
+  if (t < UPD_RT * UPD_RIN) sc.Rin[t] = in.rin;
 }
 
 // After the barrier that publishes Op: lanes q == 0 of every wave assemble row x's outputs
@@ -580,7 +604,7 @@ __device__ inline void upd_colsum_add(upd_v4 v, float* g, bool owner) {
 // workgroup barriers per tile.
 template <int KD, int KA>
 __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const UpdScr& sc,
-                         int64_t row0, int rc, float invB, unsigned long long* tm) {
+                         const UpdIn<upd_ksm<KA>()>& in, int rc, float invB, unsigned long long* tm) {
   constexpr int KSM = upd_ksm<KA>();
   const UpdNet& n = args.net;
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
@@ -595,7 +619,7 @@ __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const U
     tl = now_;                                                         \
   }
   UpdFwd<KSM> f;
-  upd_tile_fwd<KD, KA>(n, W, sc, args.S, args.act, args.old_logp, args.adv, args.ret, row0, rc, f);
+  upd_tile_fwd<KD, KA>(n, W, sc, in, f);
   UPD_CMARK(0)
   __syncthreads();   // #1: Op, Rin
   UPD_CMARK(1)
@@ -659,7 +683,7 @@ __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const U
   upd_st4(sc.Fs + x * UPD_ZS + 16 * w + 4 * q, f.Fw);
 #pragma unroll
   for (int s = 0; s < KSM; ++s)
-    if (s < KS && (s & 3) == w) sc.Xs[x * sc.XS + 4 * s + q] = f.xin[s];
+    if (s < KS && (s & 3) == w) sc.Xs[x * sc.XS + 4 * s + q] = in.xin[s];
   UPD_CMARK(3)
   __syncthreads();   // #2: Zs, Fs, Xs
   UPD_CMARK(4)
@@ -761,6 +785,27 @@ __device__ inline void f4set(float4& v, int e, float x) {
   if (e == 0) v.x = x; else if (e == 1) v.y = x; else if (e == 2) v.z = x; else v.w = x;
 }
 
+// sum of quad q over partials gg = first, first + stride, ... < G (in that order), loads issued
+// in batches of 8 so their latencies overlap
+__device__ inline void upd_sum_partials(__amdgpu_buffer_rsrc_t rs_part, int Qtot, int q, int first,
+                                        int stride, int G, double& ax, double& ay, double& az,
+                                        double& aw) {
+  for (int g0 = first; g0 < G; g0 += 8 * stride) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int gg = g0 + u * stride;
+      if (gg < G) v[u] = ld4_sc1(rs_part, ((size_t)gg * Qtot + q) * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (g0 + u * stride < G) {
+        ax += v[u].x; ay += v[u].y; az += v[u].z; aw += v[u].w;
+      }
+    }
+  }
+}
+
 // Phase B: workgroup g sums its slice [qlo, qhi) of the gradient quads over the G partials in
 // workgroup order (deterministic) with float64 accumulators (the partials of the output biases
 // cancel across workgroups), publishes the slice (sc1) and returns this thread's share of the
@@ -780,11 +825,7 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
     // wide slices (few workgroups): each thread owns whole quads, partials summed in order
     for (int qi = t; qi < nq; qi += UPD_THREADS) {
       double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
-#pragma unroll 8
-      for (int gg = 0; gg < G; ++gg) {
-        const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
-        ax += v.x; ay += v.y; az += v.z; aw += v.w;
-      }
+      upd_sum_partials(rs_part, Qtot, qlo + qi, 0, 1, G, ax, ay, az, aw);
       fin(qi, ax, ay, az, aw);
     }
   } else if (nq > 0) {
@@ -795,11 +836,7 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
     if (t < spl * nq) {
       const int qi = t % nq, sub = t / nq;
       double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
-#pragma unroll 16
-      for (int gg = sub; gg < G; gg += spl) {
-        const float4 v = ld4_sc1(rs_part, ((size_t)gg * Qtot + qlo + qi) * 4);
-        ax += v.x; ay += v.y; az += v.z; aw += v.w;
-      }
+      upd_sum_partials(rs_part, Qtot, qlo + qi, sub, spl, G, ax, ay, az, aw);
       double* o = red + 4 * (sub * nq + qi);
       o[0] = ax; o[1] = ay; o[2] = az; o[3] = aw;
     }
@@ -834,6 +871,7 @@ ppo_update_kernel(UpdArgs args) {
   float* s_bcast = hdr;             // [0] clip coefficient, [1] loss
   float* s_ssq = hdr + 4;           // [4] per-wave sums of squares
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
+  float* s_adam = hdr + 10;         // [2] this step's AdamW step size, 1 / sqrt(bc2)
 
   // ---- load parameters (LDS image) and this thread's moments (quad q = t + 256 i, registers);
   //      the moments are scattered into the LDS image layout through Ga (free until phase A) ---
@@ -876,18 +914,28 @@ ppo_update_kernel(UpdArgs args) {
       tp = now;
     }
   };
+  UpdIn<upd_ksm<KA>()> nin;   // inputs of the next tile to run (prefetched)
   for (int s = 0; s < args.total_steps; ++s) {
     const int j = s % args.nb;
     const int64_t mb0 = (int64_t)j * args.mb;
     const int B = (int)std::min<int64_t>(args.mb, args.N - mb0);
     const float invB = 1.0f / (float)B;
     const int myrows = std::max(0, std::min(R, B - g * R));
+    const int64_t myrow0 = mb0 + (int64_t)g * R;
     // ---- phase A: partial gradient of this workgroup's rows ------------------------------------
+    if (s == 0 && myrows > 0)
+      upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret, myrow0,
+                            std::min(UPD_RT, myrows), nin);
     for (int k = t; k < Lp + 4; k += UPD_THREADS) Ga[k] = 0.0f;
     __syncthreads();
-    for (int c0 = 0; c0 < myrows; c0 += UPD_RT)
-      upd_tile<KD, KA>(args, W, Ga, sc, mb0 + (int64_t)g * R + c0, std::min(UPD_RT, myrows - c0), invB,
+    for (int c0 = 0; c0 < myrows; c0 += UPD_RT) {
+      const UpdIn<upd_ksm<KA>()> cur = nin;
+      if (c0 + UPD_RT < myrows)   // prefetch the next tile of this step
+        upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
+                              myrow0 + c0 + UPD_RT, std::min(UPD_RT, myrows - c0 - UPD_RT), nin);
+      upd_tile<KD, KA>(args, W, Ga, sc, cur, std::min(UPD_RT, myrows - c0), invB,
                        reinterpret_cast<unsigned long long*>(hdr + 16));
+    }
     __syncthreads();
     mark(0);   // phase A compute
     const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(args.red);
@@ -896,8 +944,22 @@ ppo_update_kernel(UpdArgs args) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     mark(1);   // publish partials
+    if (s + 1 < args.total_steps) {   // prefetch the next step's first tile (runs under the waits)
+      const int64_t nmb0 = (int64_t)((s + 1) % args.nb) * args.mb;
+      const int nB = (int)std::min<int64_t>(args.mb, args.N - nmb0);
+      const int nrows = std::max(0, std::min(R, nB - g * R));
+      if (nrows > 0)
+        upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
+                              nmb0 + (int64_t)g * R, std::min(UPD_RT, nrows), nin);
+    }
     if (t == 0) {
       __hip_atomic_fetch_add(args.ctr + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // this step's AdamW bias corrections (float64 pow, as torch's AdamW), off the critical path
+      const double tstep = (double)step0 + (double)(s + 1);
+      const double bc1 = 1.0 - pow((double)args.beta1, tstep);
+      const double bc2 = 1.0 - pow((double)args.beta2, tstep);
+      s_adam[0] = (float)((double)args.lr / bc1);   // step size
+      s_adam[1] = (float)(1.0 / sqrt(bc2));         // 1 / sqrt(bias correction 2)
       *s_abort = upd_wait(args.ctr, 0, (unsigned)G * (unsigned)(s + 1)) ? 0 : 1;
     }
     __syncthreads();
@@ -953,11 +1015,8 @@ ppo_update_kernel(UpdArgs args) {
     const float clipc = s_bcast[0];
     loss_last = s_bcast[1];
     {
-      const double tstep = (double)step0 + (double)(s + 1);
-      const double bc1 = 1.0 - pow((double)args.beta1, tstep);
-      const double bc2 = 1.0 - pow((double)args.beta2, tstep);
-      const float step_size = (float)((double)args.lr / bc1);
-      const float inv_bc2_sqrt = (float)(1.0 / sqrt(bc2));   // scalar divide -> one multiply
+      const float step_size = s_adam[0];
+      const float inv_bc2_sqrt = s_adam[1];   // scalar divide -> one multiply
       const float decay = (float)(1.0 - (double)args.lr * (double)args.wd);
       const float b2 = args.beta2;
       const float omb1 = (float)(1.0 - (double)args.beta1), omb2 = (float)(1.0 - (double)args.beta2);
@@ -1055,8 +1114,10 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_evaluate_kernel(UpdArgs ar
   for (int64_t c = blockIdx.x; c < ntiles; c += gridDim.x) {
     const int64_t row0 = c * UPD_RT;
     const int rc = (int)std::min<int64_t>(UPD_RT, args.N - row0);
+    UpdIn<upd_ksm<KA>()> in;
+    upd_tile_load<KD, KA>(n, args.S, args.act, nullptr, nullptr, nullptr, row0, rc, in);
     UpdFwd<upd_ksm<KA>()> f;
-    upd_tile_fwd<KD, KA>(n, W, sc, args.S, args.act, nullptr, nullptr, nullptr, row0, rc, f);
+    upd_tile_fwd<KD, KA>(n, W, sc, in, f);
     __syncthreads();
     if (w == 0) {
       const float* Orow = upd_tile_outputs(n, W, sc);
@@ -1103,9 +1164,13 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_grad_kernel(UpdArgs args, 
   __syncthreads();
   const int R = args.R;
   const int myrows = std::max(0, std::min(R, B_local - g * R));
-  for (int c0 = 0; c0 < myrows; c0 += UPD_RT)
-    upd_tile<KD, KA>(args, W, Ga, sc, row0 + (int64_t)g * R + c0, std::min(UPD_RT, myrows - c0),
-                     inv_count, tm);
+  for (int c0 = 0; c0 < myrows; c0 += UPD_RT) {
+    const int rc = std::min(UPD_RT, myrows - c0);
+    UpdIn<upd_ksm<KA>()> in;
+    upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
+                          row0 + (int64_t)g * R + c0, rc, in);
+    upd_tile<KD, KA>(args, W, Ga, sc, in, rc, inv_count, tm);
+  }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(grad_out);
   for (int q = t; q < Qtot; q += UPD_THREADS)

@@ -108,7 +108,12 @@ def test_fused_gradient_matches_autograd(cont):
     for fused in (True, False):
         p = _run(fused, cont, (S, Aa, R, Dn), 512, 1, lr=0.0)
         cap = p._last_update_inputs
-        g64 = _grad_f64(p, cap)
+        # each path's float32 log-prob values in the ratio (see test_fused_gradient_off_policy);
+        # on-policy they reproduce old_logp, i.e. ratio == 1 as in the reference
+        with torch.no_grad():
+            lv = (p._engine.evaluate(p.policy, cap[0], cap[1])[0] if fused
+                  else p.policy.get_evaluate(cap[0], cap[1])[0])
+        g64 = _grad_f64(p, cap, logp_val=lv)
         per = {}
         for (name, prm), g in zip(p.policy.named_parameters(), g64):
             m = p.optimizer.state[prm]["exp_avg"].double().cpu() / 0.1
