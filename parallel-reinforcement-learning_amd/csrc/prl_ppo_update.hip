@@ -367,8 +367,13 @@ __device__ inline float upd_rsum16(float v) {
   v += upd_dpp<0x140>(v);
   return v;
 }
-// the partner lane l ^ 16 (the other 4 channels of the lane's GroupNorm group)
-__device__ inline float upd_p16(float v) { return __shfl_xor(v, 16); }
+// v + (v of the partner lane l ^ 16: the other 4 channels of the lane's GroupNorm group), by
+// v_permlane16_swap (VALU, no LDS round trip): with both operands = v it returns {v of the even
+// row of each row pair, v of the odd row}, so r[0] + r[1] has the same bits in both rows.
+__device__ inline float upd_pair_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 typedef float upd_v4 __attribute__((ext_vector_type(4)));
 __device__ inline upd_v4 upd_mma(float a, float b, upd_v4 c) {
@@ -393,12 +398,12 @@ __device__ inline void upd_wave_sync() {
 __device__ inline void upd_gn_fwd_frag(upd_v4 z, upd_v4 gw, upd_v4 gb, upd_v4& xh, float& rstd,
                                        upd_v4& y) {
   const float s4 = (z[0] + z[1]) + (z[2] + z[3]);
-  const float mean = (s4 + upd_p16(s4)) * 0.125f;
+  const float mean = upd_pair_sum(s4) * 0.125f;
   upd_v4 d;
 #pragma unroll
   for (int i = 0; i < 4; ++i) d[i] = z[i] - mean;
   const float q4 = (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
-  rstd = __builtin_amdgcn_rsqf((q4 + upd_p16(q4)) * 0.125f + 1e-5f);
+  rstd = __builtin_amdgcn_rsqf(upd_pair_sum(q4) * 0.125f + 1e-5f);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     xh[i] = d[i] * rstd;
@@ -419,8 +424,8 @@ __device__ inline upd_v4 upd_gn_bwd_frag(upd_v4 go, upd_v4 xh, upd_v4 gw, upd_v4
   }
   const float a4 = (dxh[0] + dxh[1]) + (dxh[2] + dxh[3]);
   const float b4 = (dxh[0] * xh[0] + dxh[1] * xh[1]) + (dxh[2] * xh[2] + dxh[3] * xh[3]);
-  const float m1 = (a4 + upd_p16(a4)) * 0.125f;
-  const float m2 = (b4 + upd_p16(b4)) * 0.125f;
+  const float m1 = upd_pair_sum(a4) * 0.125f;
+  const float m2 = upd_pair_sum(b4) * 0.125f;
   upd_v4 dx;
 #pragma unroll
   for (int i = 0; i < 4; ++i) dx[i] = rstd * (dxh[i] - m1 - xh[i] * m2);
@@ -569,6 +574,7 @@ __device__ inline const float* upd_tile_outputs(const UpdNet& n, const float* W,
   if (q == 0) {
 #pragma unroll
     for (int j4 = 0; j4 < 4; ++j4) {
+      if (4 * j4 >= n.nout) break;
       const upd_v4 p0 = upd_ld4(sc.Op + (0 * 16 + x) * 16 + 4 * j4);
       const upd_v4 p1 = upd_ld4(sc.Op + (1 * 16 + x) * 16 + 4 * j4);
       const upd_v4 p2 = upd_ld4(sc.Op + (2 * 16 + x) * 16 + 4 * j4);
@@ -588,14 +594,20 @@ __device__ inline const float* upd_tile_outputs(const UpdNet& n, const float* W,
   return Orow;
 }
 
+// gradient-image update: the step's first tile stores, later tiles accumulate (first is
+// wave-uniform; every image entry has one owning lane, so the step needs no zeroing pass)
+__device__ inline void upd_gadd(float* p, float v, bool first) {
+  if (first) *p = v;
+  else *p += v;
+}
 // sum over the tile's rows (DPP row) of a per-lane channel quad; lanes x == 0 add it to g[0..3]
-__device__ inline void upd_colsum_add(upd_v4 v, float* g, bool owner) {
+__device__ inline void upd_colsum_add(upd_v4 v, float* g, bool owner, bool first) {
   upd_v4 s;
 #pragma unroll
   for (int i = 0; i < 4; ++i) s[i] = upd_rsum16(v[i]);
   if (owner) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) g[i] += s[i];
+    for (int i = 0; i < 4; ++i) upd_gadd(g + i, s[i], first);
   }
 }
 
@@ -604,7 +616,8 @@ __device__ inline void upd_colsum_add(upd_v4 v, float* g, bool owner) {
 // workgroup barriers per tile.
 template <int KD, int KA>
 __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const UpdScr& sc,
-                         const UpdIn<upd_ksm<KA>()>& in, int rc, float invB, unsigned long long* tm) {
+                         const UpdIn<upd_ksm<KA>()>& in, int rc, float invB, bool first,
+                         unsigned long long* tm) {
   constexpr int KSM = upd_ksm<KA>();
   const UpdNet& n = args.net;
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
@@ -654,7 +667,7 @@ __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const U
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (4 * q + i < no) Ga[n.w2[h].lds + (4 * q + i) * UPD_HS + 16 * w + x] += acc[i];
+        if (4 * q + i < no) upd_gadd(Ga + n.w2[h].lds + (4 * q + i) * UPD_HS + 16 * w + x, acc[i], first);
       // dG_h^T block w = W2_h^T dO_h^T (K = the head's outputs), GroupNorm + SiLU backward
       upd_v4 dg = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -674,8 +687,8 @@ __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const U
       upd_v4 dyx;
 #pragma unroll
       for (int i = 0; i < 4; ++i) dyx[i] = dy[i] * f.xh[h][i];
-      upd_colsum_add(dyx, Ga + n.g1[h].lds + 16 * w + 4 * q, x == 0);
-      upd_colsum_add(dy, Ga + n.b1[h].lds + 16 * w + 4 * q, x == 0);
+      upd_colsum_add(dyx, Ga + n.g1[h].lds + 16 * w + 4 * q, x == 0, first);
+      upd_colsum_add(dy, Ga + n.b1[h].lds + 16 * w + 4 * q, x == 0, first);
       upd_wave_sync();   // Tw reads done before the next head overwrites it
     }
   }
@@ -705,7 +718,7 @@ __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const U
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) gw1[i * UPD_HS + 16 * b] += acc[b][i];
+        for (int i = 0; i < 4; ++i) upd_gadd(gw1 + i * UPD_HS + 16 * b, acc[b][i], first);
     }
   }
   UPD_CMARK(5)
@@ -738,8 +751,8 @@ __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const U
     upd_v4 dyx;
 #pragma unroll
     for (int i = 0; i < 4; ++i) dyx[i] = dy0[i] * f.xh0[i];
-    upd_colsum_add(dyx, Ga + n.g0.lds + 16 * w + 4 * q, x == 0);
-    upd_colsum_add(dy0, Ga + n.b0.lds + 16 * w + 4 * q, x == 0);
+    upd_colsum_add(dyx, Ga + n.g0.lds + 16 * w + 4 * q, x == 0, first);
+    upd_colsum_add(dy0, Ga + n.b0.lds + 16 * w + 4 * q, x == 0, first);
   }
   UPD_CMARK(6)
   // ---- dW0[16w + 4q + i][16e + x] += sum_rows dH0[row][ch] X[row][d]  (dH0 transposed via Tw)
@@ -755,7 +768,7 @@ __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const U
         acc = upd_mma(Tw[(4 * s + q) * 16 + x], d < D ? sc.Xs[(4 * s + q) * sc.XS + d] : 0.0f, acc);
       if (d < D) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) Ga[n.w0.lds + (16 * w + 4 * q + i) * n.w0.stride + d] += acc[i];
+        for (int i = 0; i < 4; ++i) upd_gadd(Ga + n.w0.lds + (16 * w + 4 * q + i) * n.w0.stride + d, acc[i], first);
       }
     }
   }
@@ -765,12 +778,12 @@ __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const U
       double acc = 0.0;
 #pragma unroll
       for (int r = 0; r < UPD_RT; ++r) acc += (double)dOw[r * 16 + t];
-      Ga[upd_bias_of(n, t)] += (float)acc;
+      upd_gadd(Ga + upd_bias_of(n, t), (float)acc, first);
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const float s = upd_rsum16(lp[k]);
-      if (t == 0) Ga[n.Lp + k] += s;
+      if (t == 0) upd_gadd(Ga + n.Lp + k, s, first);
     }
   }
   upd_wave_sync();   // Tw reads done before the next tile
@@ -901,6 +914,8 @@ ppo_update_kernel(UpdArgs args) {
   const float step0 = args.adam_step[0];
   if (t < 24) reinterpret_cast<unsigned long long*>(hdr + 16)[t] = 0ull;
   __syncthreads();
+  for (int k = t; k < Lp + 4; k += UPD_THREADS) Ga[k] = 0.0f;   // padding stays 0 for good
+  __syncthreads();
 
   const int R = args.R;
   float loss_last = 0.f;
@@ -926,14 +941,15 @@ ppo_update_kernel(UpdArgs args) {
     if (s == 0 && myrows > 0)
       upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret, myrow0,
                             std::min(UPD_RT, myrows), nin);
-    for (int k = t; k < Lp + 4; k += UPD_THREADS) Ga[k] = 0.0f;
-    __syncthreads();
+    if (myrows == 0) {   // no rows this step: publish zeros
+      for (int k = t; k < Lp + 4; k += UPD_THREADS) Ga[k] = 0.0f;
+    }
     for (int c0 = 0; c0 < myrows; c0 += UPD_RT) {
       const UpdIn<upd_ksm<KA>()> cur = nin;
       if (c0 + UPD_RT < myrows)   // prefetch the next tile of this step
         upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
                               myrow0 + c0 + UPD_RT, std::min(UPD_RT, myrows - c0 - UPD_RT), nin);
-      upd_tile<KD, KA>(args, W, Ga, sc, cur, std::min(UPD_RT, myrows - c0), invB,
+      upd_tile<KD, KA>(args, W, Ga, sc, cur, std::min(UPD_RT, myrows - c0), invB, c0 == 0,
                        reinterpret_cast<unsigned long long*>(hdr + 16));
     }
     __syncthreads();
@@ -1169,7 +1185,7 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_grad_kernel(UpdArgs args, 
     UpdIn<upd_ksm<KA>()> in;
     upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
                           row0 + (int64_t)g * R + c0, rc, in);
-    upd_tile<KD, KA>(args, W, Ga, sc, in, rc, inv_count, tm);
+    upd_tile<KD, KA>(args, W, Ga, sc, in, rc, inv_count, c0 == 0, tm);
   }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(grad_out);
