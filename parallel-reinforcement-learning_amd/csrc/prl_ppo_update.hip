@@ -64,6 +64,53 @@ struct UpdNet {
   int P;                        // flat parameter count
 };
 
+// LDS image + flat offsets of the reference's parameter tensors, torch parameters() order.
+// constexpr: the specialised kernels fold the whole layout into immediates.
+__host__ __device__ constexpr void upd_add(UpdTensor& t, int& flat, int& lds, int rows, int cols,
+                                           int stride) {
+  t.flat = flat;
+  t.lds = lds;
+  t.rows = rows;
+  t.cols = cols;
+  t.stride = stride;
+  flat += rows * cols;
+  lds += (rows * stride + 3) & ~3;
+}
+__host__ __device__ constexpr bool upd_layout(int D, int A, int discrete, UpdNet& n) {
+  if (D < 1 || D > UPD_MAXD || A < 1 || A > UPD_MAXA) return false;
+  n = UpdNet{};
+  n.D = D;
+  n.A = A;
+  n.discrete = discrete ? 1 : 0;
+  n.nh = discrete ? 2 : 3;
+  int flat = 0, lds = 0;
+  upd_add(n.w0, flat, lds, UPD_H, D, D | 1);
+  upd_add(n.g0, flat, lds, 1, UPD_H, UPD_H);
+  upd_add(n.b0, flat, lds, 1, UPD_H, UPD_H);
+  int col = 0;
+  for (int h = 0; h < n.nh; ++h) {
+    const int out = (h == n.nh - 1) ? 1 : A;
+    n.out[h] = out;
+    n.ocol[h] = col;
+    col += out;
+    upd_add(n.w1[h], flat, lds, UPD_H, UPD_H, UPD_HS);
+    upd_add(n.g1[h], flat, lds, 1, UPD_H, UPD_H);
+    upd_add(n.b1[h], flat, lds, 1, UPD_H, UPD_H);
+    upd_add(n.w2[h], flat, lds, out, UPD_H, UPD_HS);
+    upd_add(n.b2[h], flat, lds, 1, out, out);
+  }
+  n.nout = col;
+  if (n.nout > 16) return false;   // one 16-row output tile (UPD_MAXO)
+  n.P = flat;
+  n.Lp = lds;
+  return true;
+}
+__host__ __device__ constexpr UpdNet upd_make(int D, int A, int discrete) {
+  UpdNet n{};
+  upd_layout(D, A, discrete, n);
+  return n;
+}
+
 struct UpdArgs {
   UpdNet net;
   const float* S;
@@ -81,7 +128,7 @@ struct UpdArgs {
   float* loss_out;
   float* part;      // [G][Qtot * 4]
   float* red;       // [Qtot * 4]
-  float* sq;        // [G]
+  float* sq;        // [NW G] per-wave squared-norm pieces of the slices
   unsigned* ctr;    // [0] arrivals A, [1] arrivals B, [2] abort, [3] status (zeroed per launch),
                     // [4] sticky timeout flag (never zeroed by a launch)
   unsigned long long* prof;  // [8] workgroup 0's time per phase (100 MHz ticks, summed over steps)
@@ -173,28 +220,28 @@ constexpr int UPD_RIN = 12;       // row-input record: act[8], old_logp, adv, re
 constexpr int UPD_MAXO = 16;      // outputs of all heads together (one 16-row MFMA tile)
 
 __host__ __device__ inline int upd_xs(int D) { return D <= 16 ? 16 : UPD_ZS; }
-__host__ __device__ inline int upd_scratch_floats(int D) {
-  return UPD_RT * upd_xs(D)          // Xs  [16][XS]      tile inputs (rows x features)
-         + 4 * UPD_RT * 16           // Op  [4][16][16]   output-layer partial per wave
-         + 4 * UPD_RT * 16           // Os  [4][16][16]   assembled outputs per wave
-         + 4 * UPD_RT * 16           // dOs [4][16][16]   d loss / d outputs per wave
-         + UPD_RT * UPD_RIN          // Rin [16][12]      row inputs
-         + UPD_RT * UPD_ZS           // Fs  [16][80]      trunk output
-         + UPD_MAXH * UPD_RT * UPD_ZS  // Zs [h][16][80]  head dZ
-         + 4 * UPD_RT * 16           // Ts  [4][16][16]   per-wave transpose slot (G_h, dH0)
+__host__ __device__ inline int upd_scratch_floats(int D, int NW) {
+  return UPD_RT * upd_xs(D)          // Xs  [16][XS]       tile inputs (rows x features)
+         + NW * UPD_RT * 16          // Op  [NW][16][16]   output-layer partial per wave
+         + NW * UPD_RT * 16          // Os  [NW][16][16]   assembled outputs per wave
+         + NW * UPD_RT * 16          // dOs [NW][16][16]   d loss / d outputs per wave
+         + UPD_RT * UPD_RIN          // Rin [16][12]       row inputs
+         + UPD_RT * UPD_ZS           // Fs  [16][80]       trunk output
+         + UPD_MAXH * UPD_RT * UPD_ZS  // Zs [h][16][80]   head dZ
+         + NW * UPD_RT * 16          // Ts  [NW][16][16]   per-wave transpose slot (G_h, dH0)
          + 16;
 }
 struct UpdScr {
   float *Xs, *Op, *Os, *dOs, *Rin, *Fs, *Zs, *Ts;
   int XS;
 };
-__device__ inline UpdScr upd_scr(float* p, int D) {
+__device__ inline UpdScr upd_scr(float* p, int D, int NW) {
   UpdScr s;
   s.XS = upd_xs(D);
   s.Xs = p; p += UPD_RT * s.XS;
-  s.Op = p; p += 4 * UPD_RT * 16;
-  s.Os = p; p += 4 * UPD_RT * 16;
-  s.dOs = p; p += 4 * UPD_RT * 16;
+  s.Op = p; p += NW * UPD_RT * 16;
+  s.Os = p; p += NW * UPD_RT * 16;
+  s.dOs = p; p += NW * UPD_RT * 16;
   s.Rin = p; p += UPD_RT * UPD_RIN;
   s.Fs = p; p += UPD_RT * UPD_ZS;
   s.Zs = p; p += UPD_MAXH * UPD_RT * UPD_ZS;
@@ -445,17 +492,42 @@ template <int KD>
 __device__ inline int upd_nh(const UpdNet& n) { return KD > 0 ? 2 : (KD == 0 ? 3 : n.nh); }
 
 // Forward state of one tile kept for the backward (wave w's channel block, lane's row x).
-// KSM = compile-time bound on the input k-steps ceil(D / 4) (4 for the specialised kernels).
-template <int KSM>
+// KSM = compile-time bound on the input k-steps ceil(D / 4) (4 for the specialised kernels);
+// HPW = heads per wave (all heads with 4 waves; one head per wave group with 8 waves).
+template <int KSM, int HPW>
 struct UpdFwd {
-  upd_v4 Fw;                         // trunk output, block w
-  upd_v4 xh0;                        // trunk xhat (block w)
-  float r0;                          // trunk rstd (block w)
-  upd_v4 xh[UPD_MAXH], G[UPD_MAXH];  // head xhat / output (block w)
-  float rh[UPD_MAXH];
+  upd_v4 Fw;                     // trunk output, block b
+  upd_v4 xh0;                    // trunk xhat (block b)
+  float r0;                      // trunk rstd (block b)
+  upd_v4 xh[HPW], G[HPW];        // head xhat / output (block b) of the wave's heads
+  float rh[HPW];
 };
 template <int KA>
 constexpr int upd_ksm() { return KA > 0 ? 4 : 16; }
+// Waves per workgroup: the two-head discrete specialisation (CartPole) runs 8 waves, wave
+// w = (head group w >> 2, channel block w & 3): twice the waves per SIMD to hide latency and
+// half of every per-wave MFMA chain.  Three heads (Pendulum) and the generic kernel run 4 waves
+// (wave w = channel block w, all heads) to stay inside the LDS.
+template <int KD, int KA>
+constexpr int upd_nw() { return (KD == 1 && KA == 2 && false) ? 8 : 4; }   // 8 waves measured slower: off
+template <int NW>
+constexpr int upd_hpw() { return NW == 8 ? 1 : UPD_MAXH; }
+// global head of the wave's local head slot hs
+template <int NW>
+__device__ inline int upd_head(int hs, int hg) { return NW == 8 ? hg + 2 * hs : hs; }
+// image offsets / output columns of head h (h wave-uniform, possibly runtime): selected over
+// compile-time indices, so the kernarg struct is never indexed dynamically (that would copy it
+// to scratch)
+struct UpdHead {
+  int w1, g1, b1, w2, oc, no;
+};
+__device__ inline UpdHead upd_head_info(const UpdNet& n, int h) {
+  UpdHead r{n.w1[0].lds, n.g1[0].lds, n.b1[0].lds, n.w2[0].lds, n.ocol[0], n.out[0]};
+#pragma unroll
+  for (int k = 1; k < UPD_MAXH; ++k)
+    if (h == k) r = UpdHead{n.w1[k].lds, n.g1[k].lds, n.b1[k].lds, n.w2[k].lds, n.ocol[k], n.out[k]};
+  return r;
+}
 
 // A tile's global inputs, loaded into registers ahead of the tile (prefetch): the B fragments
 // of the observations X[row x][4 s + q] and one word of the row-input record (thread t < 192:
@@ -493,22 +565,24 @@ __device__ inline void upd_tile_load(const UpdNet& n, const float* Sg, const flo
 
 // Forward of one tile (rows row0 .. row0 + rc - 1, rc <= 16) up to the output-layer partials:
 // every wave runs the trunk for all 64 channels (it is the B operand of every head block), then
-// its head block w; the output layer's K = 64 sum is split over the waves (partial per wave in
-// Op[w]).  Also stages the row inputs (act, old_logp, adv, ret) into Rin.  No barrier inside;
-// the caller's barrier publishes Op / Rin.
+// its heads' block b; the output layer's K = 64 sum is split over the waves (partial per wave
+// in Op[w]).  Also stages the row inputs into Rin.  No barrier inside; the caller's barrier
+// publishes Op / Rin.
 template <int KD, int KA>
 __device__ inline void upd_tile_fwd(const UpdNet& n, const float* W, const UpdScr& sc,
-                                    const UpdIn<upd_ksm<KA>()>& in, UpdFwd<upd_ksm<KA>()>& f) {
-  constexpr int KSM = upd_ksm<KA>();
+                                    const UpdIn<upd_ksm<KA>()>& in,
+                                    UpdFwd<upd_ksm<KA>(), upd_hpw<upd_nw<KD, KA>()>()>& f) {
+  constexpr int KSM = upd_ksm<KA>(), NW = upd_nw<KD, KA>(), HPW = upd_hpw<NW>();
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  const int b = w & 3, hg = w >> 2;
   const int D = n.D, KS = (D + 3) >> 2;
   const int nh = upd_nh<KD>(n);
-  // trunk: H0^T block b = W0[16b .. 16b+15][:] X^T  (A: W0 rows, B: inputs), then GN + SiLU
+  // trunk: H0^T block bb = W0[16bb .. 16bb+15][:] X^T  (A: W0 rows, B: inputs), then GN + SiLU
   upd_v4 F[4];
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
+  for (int bb = 0; bb < 4; ++bb) {
     upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* wr = W + n.w0.lds + (16 * b + x) * n.w0.stride;
+    const float* wr = W + n.w0.lds + (16 * bb + x) * n.w0.stride;
 #pragma unroll
     for (int s = 0; s < KSM; ++s) {
       if (s < KS) {
@@ -518,48 +592,52 @@ __device__ inline void upd_tile_fwd(const UpdNet& n, const float* W, const UpdSc
     }
     upd_v4 xh;
     float rs;
-    upd_gn_fwd_frag(acc, upd_ld4(W + n.g0.lds + 16 * b + 4 * q), upd_ld4(W + n.b0.lds + 16 * b + 4 * q),
-                    xh, rs, F[b]);
-    if (b == w) {
+    upd_gn_fwd_frag(acc, upd_ld4(W + n.g0.lds + 16 * bb + 4 * q), upd_ld4(W + n.b0.lds + 16 * bb + 4 * q),
+                    xh, rs, F[bb]);
+    if (bb == b) {
       f.xh0 = xh;
       f.r0 = rs;
-      f.Fw = F[b];
+      f.Fw = F[bb];
     }
   }
-  // heads: Z_h^T block w = W1_h[16w ..][:] F^T; K order per step (b, i): lane q <-> input
-  // channel 16 b + 4 q + i, so F's C fragments are the B operand as they stand
-  upd_v4 z[UPD_MAXH];
+  // heads: Z_h^T block b = W1_h[16b ..][:] F^T; K order per step (bb, i): lane q <-> input
+  // channel 16 bb + 4 q + i, so F's C fragments are the B operand as they stand
+  upd_v4 z[HPW];
 #pragma unroll
-  for (int h = 0; h < UPD_MAXH; ++h) z[h] = upd_v4{0.f, 0.f, 0.f, 0.f};
+  for (int hs = 0; hs < HPW; ++hs) z[hs] = upd_v4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
+  for (int bb = 0; bb < 4; ++bb) {
 #pragma unroll
-    for (int h = 0; h < UPD_MAXH; ++h) {
+    for (int hs = 0; hs < HPW; ++hs) {
+      const int h = upd_head<NW>(hs, hg);
       if (h < nh) {
-        const upd_v4 wa = upd_ld4(W + n.w1[h].lds + (16 * w + x) * UPD_HS + 16 * b + 4 * q);
-        z[h] = upd_mma(wa[0], F[b][0], z[h]);
-        z[h] = upd_mma(wa[1], F[b][1], z[h]);
-        z[h] = upd_mma(wa[2], F[b][2], z[h]);
-        z[h] = upd_mma(wa[3], F[b][3], z[h]);
+        const UpdHead hi = upd_head_info(n, h);
+        const upd_v4 wa = upd_ld4(W + hi.w1 + (16 * b + x) * UPD_HS + 16 * bb + 4 * q);
+        z[hs] = upd_mma(wa[0], F[bb][0], z[hs]);
+        z[hs] = upd_mma(wa[1], F[bb][1], z[hs]);
+        z[hs] = upd_mma(wa[2], F[bb][2], z[hs]);
+        z[hs] = upd_mma(wa[3], F[bb][3], z[hs]);
       }
     }
   }
   // head GN + SiLU, then the output layer's partial over this block's 16 channels:
-  // O^T[j][row] += W2[j][16w + 4q + i] G^T (A row m = output j, head h's rows at ocol[h])
+  // O^T[j][row] += W2[j][16b + 4q + i] G^T (A row m = output j, head h's rows at ocol[h])
   upd_v4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int h = 0; h < UPD_MAXH; ++h) {
+  for (int hs = 0; hs < HPW; ++hs) {
+    const int h = upd_head<NW>(hs, hg);
     if (h < nh) {
-      upd_gn_fwd_frag(z[h], upd_ld4(W + n.g1[h].lds + 16 * w + 4 * q),
-                      upd_ld4(W + n.b1[h].lds + 16 * w + 4 * q), f.xh[h], f.rh[h], f.G[h]);
-      const int oc = n.ocol[h], no = n.out[h];
+      const UpdHead hi = upd_head_info(n, h);
+      upd_gn_fwd_frag(z[hs], upd_ld4(W + hi.g1 + 16 * b + 4 * q),
+                      upd_ld4(W + hi.b1 + 16 * b + 4 * q), f.xh[hs], f.rh[hs], f.G[hs]);
+      const int oc = hi.oc, no = hi.no;
       const bool mine = x >= oc && x < oc + no;
-      const upd_v4 wv = mine ? upd_ld4(W + n.w2[h].lds + (x - oc) * UPD_HS + 16 * w + 4 * q)
+      const upd_v4 wv = mine ? upd_ld4(W + hi.w2 + (x - oc) * UPD_HS + 16 * b + 4 * q)
                              : upd_v4{0.f, 0.f, 0.f, 0.f};
-      o = upd_mma(wv[0], f.G[h][0], o);
-      o = upd_mma(wv[1], f.G[h][1], o);
-      o = upd_mma(wv[2], f.G[h][2], o);
-      o = upd_mma(wv[3], f.G[h][3], o);
+      o = upd_mma(wv[0], f.G[hs][0], o);
+      o = upd_mma(wv[1], f.G[hs][1], o);
+      o = upd_mma(wv[2], f.G[hs][2], o);
+      o = upd_mma(wv[3], f.G[hs][3], o);
     }
   }
   upd_st4(sc.Op + (w * 16 + x) * 16 + 4 * q, o);   // [w][row x][j = 4q + i]
@@ -567,7 +645,9 @@ __device__ inline void upd_tile_fwd(const UpdNet& n, const float* W, const UpdSc
 }
 
 // After the barrier that publishes Op: lanes q == 0 of every wave assemble row x's outputs
-// (fixed order over the 4 partials, then the bias) into Os[w][x][*]; returns the pointer.
+// (the NW partials in wave order, then the bias) into Os[w][x][*]; returns the pointer.  A head's
+// output gets exact zeros from the other head group's waves, so 4 and 8 waves give equal bits.
+template <int NW>
 __device__ inline const float* upd_tile_outputs(const UpdNet& n, const float* W, const UpdScr& sc) {
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   float* Orow = sc.Os + (w * 16 + x) * 16;
@@ -575,17 +655,17 @@ __device__ inline const float* upd_tile_outputs(const UpdNet& n, const float* W,
 #pragma unroll
     for (int j4 = 0; j4 < 4; ++j4) {
       if (4 * j4 >= n.nout) break;
-      const upd_v4 p0 = upd_ld4(sc.Op + (0 * 16 + x) * 16 + 4 * j4);
-      const upd_v4 p1 = upd_ld4(sc.Op + (1 * 16 + x) * 16 + 4 * j4);
-      const upd_v4 p2 = upd_ld4(sc.Op + (2 * 16 + x) * 16 + 4 * j4);
-      const upd_v4 p3 = upd_ld4(sc.Op + (3 * 16 + x) * 16 + 4 * j4);
-      upd_v4 v;
+      upd_v4 v = upd_ld4(sc.Op + (0 * 16 + x) * 16 + 4 * j4);
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) {
+        const upd_v4 p = upd_ld4(sc.Op + (ww * 16 + x) * 16 + 4 * j4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += p[e];
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int j = 4 * j4 + e;
-        float s = ((p0[e] + p1[e]) + p2[e]) + p3[e];
-        if (j < n.nout) s += W[upd_bias_of(n, j)];
-        v[e] = s;
+        if (j < n.nout) v[e] += W[upd_bias_of(n, j)];
       }
       upd_st4(Orow + 4 * j4, v);
     }
@@ -597,7 +677,7 @@ __device__ inline const float* upd_tile_outputs(const UpdNet& n, const float* W,
 // gradient-image update: the step's first tile stores, later tiles accumulate (first is
 // wave-uniform; every image entry has one owning lane, so the step needs no zeroing pass)
 __device__ inline void upd_gadd(float* p, float v, bool first) {
-  if (first) *p = v;
+  if (first) *p = v;   // first is a compile-time constant at every call site (upd_tile<.., FIRST>)
   else *p += v;
 }
 // sum over the tile's rows (DPP row) of a per-lane channel quad; lanes x == 0 add it to g[0..3]
@@ -614,13 +694,14 @@ __device__ inline void upd_colsum_add(upd_v4 v, float* g, bool owner, bool first
 // One tile of the update: forward, loss, backward; the tile's gradient is added into the LDS
 // gradient image Ga (every image entry has exactly one owning lane, so no atomics).  Two
 // workgroup barriers per tile.
-template <int KD, int KA>
-__device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const UpdScr& sc,
-                         const UpdIn<upd_ksm<KA>()>& in, int rc, float invB, bool first,
+template <int KD, int KA, bool FIRST>
+__device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, float* Ga,
+                         const UpdScr& sc, const UpdIn<upd_ksm<KA>()>& in, int rc, float invB,
                          unsigned long long* tm) {
-  constexpr int KSM = upd_ksm<KA>();
-  const UpdNet& n = args.net;
+  constexpr int KSM = upd_ksm<KA>(), NW = upd_nw<KD, KA>(), HPW = upd_hpw<NW>();
+  constexpr bool first = FIRST;
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  const int b = w & 3, hg = w >> 2;
   const int D = n.D, KS = (D + 3) >> 2;
   const int nh = upd_nh<KD>(n);
   const bool timer = blockIdx.x == 0 && t == 0;
@@ -631,13 +712,13 @@ __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const U
     tm[i] += now_ - tl;                                                \
     tl = now_;                                                         \
   }
-  UpdFwd<KSM> f;
+  UpdFwd<KSM, HPW> f;
   upd_tile_fwd<KD, KA>(n, W, sc, in, f);
   UPD_CMARK(0)
   __syncthreads();   // #1: Op, Rin
   UPD_CMARK(1)
   // ---- loss of row x (lanes q == 0 of every wave, redundantly: each wave needs dO)
-  const float* Orow = upd_tile_outputs(n, W, sc);
+  const float* Orow = upd_tile_outputs<NW>(n, W, sc);
   const float* dOw = sc.dOs + w * 16 * 16;   // [row][j] of this wave
   float lp[3] = {0.f, 0.f, 0.f};
   if (q == 0) {
@@ -653,11 +734,13 @@ __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const U
   UPD_CMARK(2)
   float* Tw = sc.Ts + w * UPD_RT * 16;   // this wave's [16 rows][16 ch] transpose slot
 #pragma unroll
-  for (int h = 0; h < UPD_MAXH; ++h) {
+  for (int hs = 0; hs < HPW; ++hs) {
+    const int h = upd_head<NW>(hs, hg);
     if (h < nh) {
-      const int oc = n.ocol[h], no = n.out[h];
-      // dW2_h[j][16w + x] += sum_rows dO[row][oc + j] G_h[row][ch]  (G_h transposed via Tw)
-      upd_st4(Tw + x * 16 + 4 * q, f.G[h]);
+      const UpdHead hi = upd_head_info(n, h);
+      const int oc = hi.oc, no = hi.no;
+      // dW2_h[j][16b + x] += sum_rows dO[row][oc + j] G_h[row][ch]  (G_h transposed via Tw)
+      upd_st4(Tw + x * 16 + 4 * q, f.G[hs]);
       upd_wave_sync();
       upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -667,123 +750,132 @@ __device__ void upd_tile(const UpdArgs& args, const float* W, float* Ga, const U
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (4 * q + i < no) upd_gadd(Ga + n.w2[h].lds + (4 * q + i) * UPD_HS + 16 * w + x, acc[i], first);
-      // dG_h^T block w = W2_h^T dO_h^T (K = the head's outputs), GroupNorm + SiLU backward
+        if (4 * q + i < no) upd_gadd(Ga + hi.w2 + (4 * q + i) * UPD_HS + 16 * b + x, acc[i], first);
+      // dG_h^T block b = W2_h^T dO_h^T (K = the head's outputs), GroupNorm + SiLU backward
       upd_v4 dg = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < UPD_MAXA / 4; ++s) {
         if (4 * s < no) {
           const int j = 4 * s + q;
-          const float a = j < no ? W[n.w2[h].lds + j * UPD_HS + 16 * w + x] : 0.0f;
+          const float a = j < no ? W[hi.w2 + j * UPD_HS + 16 * b + x] : 0.0f;
           const float bb = j < no ? dOw[x * 16 + oc + j] : 0.0f;
           dg = upd_mma(a, bb, dg);
         }
       }
-      const upd_v4 gw = upd_ld4(W + n.g1[h].lds + 16 * w + 4 * q);
+      const upd_v4 gw = upd_ld4(W + hi.g1 + 16 * b + 4 * q);
       upd_v4 dy;
-      const upd_v4 dz = upd_gn_bwd_frag(dg, f.xh[h], gw, upd_ld4(W + n.b1[h].lds + 16 * w + 4 * q),
-                                        f.rh[h], dy);
-      upd_st4(sc.Zs + h * UPD_RT * UPD_ZS + x * UPD_ZS + 16 * w + 4 * q, dz);
+      const upd_v4 dz = upd_gn_bwd_frag(dg, f.xh[hs], gw, upd_ld4(W + hi.b1 + 16 * b + 4 * q),
+                                        f.rh[hs], dy);
+      upd_st4(sc.Zs + h * UPD_RT * UPD_ZS + x * UPD_ZS + 16 * b + 4 * q, dz);
       upd_v4 dyx;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dyx[i] = dy[i] * f.xh[h][i];
-      upd_colsum_add(dyx, Ga + n.g1[h].lds + 16 * w + 4 * q, x == 0, first);
-      upd_colsum_add(dy, Ga + n.b1[h].lds + 16 * w + 4 * q, x == 0, first);
+      for (int i = 0; i < 4; ++i) dyx[i] = dy[i] * f.xh[hs][i];
+      upd_colsum_add(dyx, Ga + hi.g1 + 16 * b + 4 * q, x == 0, first);
+      upd_colsum_add(dy, Ga + hi.b1 + 16 * b + 4 * q, x == 0, first);
       upd_wave_sync();   // Tw reads done before the next head overwrites it
     }
   }
   // trunk output and inputs, rows x channels, for the weight gradients
-  upd_st4(sc.Fs + x * UPD_ZS + 16 * w + 4 * q, f.Fw);
+  if (hg == 0) upd_st4(sc.Fs + x * UPD_ZS + 16 * b + 4 * q, f.Fw);
 #pragma unroll
   for (int s = 0; s < KSM; ++s)
-    if (s < KS && (s & 3) == w) sc.Xs[x * sc.XS + 4 * s + q] = in.xin[s];
+    if (s < KS && (s % NW) == w) sc.Xs[x * sc.XS + 4 * s + q] = in.xin[s];
   UPD_CMARK(3)
   __syncthreads();   // #2: Zs, Fs, Xs
   UPD_CMARK(4)
-  // ---- dW1_h[16w + 4q + i][16b + x] += sum_rows dZ_h[row][out] F[row][in]  (K = rows)
-#pragma unroll
-  for (int h = 0; h < UPD_MAXH; ++h) {
-    if (h < nh) {
-      const float* Zh = sc.Zs + h * UPD_RT * UPD_ZS;
-      upd_v4 acc[4];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[b] = upd_v4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const float a = Zh[(4 * s + q) * UPD_ZS + 16 * w + x];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[b] = upd_mma(a, sc.Fs[(4 * s + q) * UPD_ZS + 16 * b + x], acc[b]);
-      }
-      float* gw1 = Ga + n.w1[h].lds + (16 * w + 4 * q) * UPD_HS + x;
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) upd_gadd(gw1 + i * UPD_HS + 16 * b, acc[b][i], first);
-    }
-  }
-  UPD_CMARK(5)
-  // ---- dF^T block w = sum_h W1_h^T dZ_h^T (K = 64 head channels, permuted so that the A reads
-  //      are conflict-free: step s, lane q <-> channel 16 (s & 3) + 4 q + (s >> 2))
-  upd_v4 dF;
-  {
-    upd_v4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+  // After the barrier, with 8 waves: group 1 takes the head weight gradients (dW1), group 0 the
+  // trunk (dF, GroupNorm backward, dW0); with 4 waves each wave does both for its block.
+  if (NW == 4 || hg == 1) {
+    // ---- dW1_h[16b + 4q + i][16bb + x] += sum_rows dZ_h[row][out] F[row][in]  (K = rows)
 #pragma unroll
     for (int h = 0; h < UPD_MAXH; ++h) {
       if (h < nh) {
-        const float* Zh = sc.Zs + h * UPD_RT * UPD_ZS + x * UPD_ZS;
-        const float* Wh = W + n.w1[h].lds + 16 * w + x;
+        const float* Zh = sc.Zs + h * UPD_RT * UPD_ZS;
+        upd_v4 acc[4];
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const int o = 16 * (s & 3) + 4 * q + (s >> 2);
-          if (s & 1) d1 = upd_mma(Wh[o * UPD_HS], Zh[o], d1);
-          else d0 = upd_mma(Wh[o * UPD_HS], Zh[o], d0);
+        for (int bb = 0; bb < 4; ++bb) acc[bb] = upd_v4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float a = Zh[(4 * s + q) * UPD_ZS + 16 * b + x];
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb)
+            acc[bb] = upd_mma(a, sc.Fs[(4 * s + q) * UPD_ZS + 16 * bb + x], acc[bb]);
+        }
+        float* gw1 = Ga + n.w1[h].lds + (16 * b + 4 * q) * UPD_HS + x;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) upd_gadd(gw1 + i * UPD_HS + 16 * bb, acc[bb][i], first);
+      }
+    }
+  }
+  UPD_CMARK(5)
+  if (NW == 4 || hg == 0) {
+    // ---- dF^T block b = sum_h W1_h^T dZ_h^T (K = 64 head channels, permuted so that the A
+    //      reads are conflict-free: step s, lane q <-> channel 16 (s & 3) + 4 q + (s >> 2))
+    upd_v4 dF;
+    {
+      upd_v4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < UPD_MAXH; ++h) {
+        if (h < nh) {
+          const float* Zh = sc.Zs + h * UPD_RT * UPD_ZS + x * UPD_ZS;
+          const float* Wh = W + n.w1[h].lds + 16 * b + x;
+#pragma unroll
+          for (int s = 0; s < 16; ++s) {
+            const int o = 16 * (s & 3) + 4 * q + (s >> 2);
+            if (s & 1) d1 = upd_mma(Wh[o * UPD_HS], Zh[o], d1);
+            else d0 = upd_mma(Wh[o * UPD_HS], Zh[o], d0);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dF[i] = d0[i] + d1[i];
+    }
+    // trunk GroupNorm + SiLU backward -> dH0 (block b), its weight / bias gradients
+    upd_v4 dy0;
+    const upd_v4 dH0 = upd_gn_bwd_frag(dF, f.xh0, upd_ld4(W + n.g0.lds + 16 * b + 4 * q),
+                                       upd_ld4(W + n.b0.lds + 16 * b + 4 * q), f.r0, dy0);
+    {
+      upd_v4 dyx;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dyx[i] = dy0[i] * f.xh0[i];
+      upd_colsum_add(dyx, Ga + n.g0.lds + 16 * b + 4 * q, x == 0, first);
+      upd_colsum_add(dy0, Ga + n.b0.lds + 16 * b + 4 * q, x == 0, first);
+    }
+    UPD_CMARK(6)
+    // ---- dW0[16b + 4q + i][16e + x] += sum_rows dH0[row][ch] X[row][d]  (dH0 transposed via Tw)
+    upd_st4(Tw + x * 16 + 4 * q, dH0);
+    upd_wave_sync();
+#pragma unroll
+    for (int e = 0; e < (KSM + 3) / 4; ++e) {
+      if (16 * e < D) {
+        upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
+        const int d = 16 * e + x;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc = upd_mma(Tw[(4 * s + q) * 16 + x], d < D ? sc.Xs[(4 * s + q) * sc.XS + d] : 0.0f, acc);
+        if (d < D) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            upd_gadd(Ga + n.w0.lds + (16 * b + 4 * q + i) * n.w0.stride + d, acc[i], first);
         }
       }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dF[i] = d0[i] + d1[i];
   }
-  // trunk GroupNorm + SiLU backward -> dH0 (block w), its weight / bias gradients
-  upd_v4 dy0;
-  const upd_v4 dH0 = upd_gn_bwd_frag(dF, f.xh0, upd_ld4(W + n.g0.lds + 16 * w + 4 * q),
-                                     upd_ld4(W + n.b0.lds + 16 * w + 4 * q), f.r0, dy0);
-  {
-    upd_v4 dyx;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dyx[i] = dy0[i] * f.xh0[i];
-    upd_colsum_add(dyx, Ga + n.g0.lds + 16 * w + 4 * q, x == 0, first);
-    upd_colsum_add(dy0, Ga + n.b0.lds + 16 * w + 4 * q, x == 0, first);
-  }
-  UPD_CMARK(6)
-  // ---- dW0[16w + 4q + i][16e + x] += sum_rows dH0[row][ch] X[row][d]  (dH0 transposed via Tw)
-  upd_st4(Tw + x * 16 + 4 * q, dH0);
-  upd_wave_sync();
-#pragma unroll
-  for (int e = 0; e < (KSM + 3) / 4; ++e) {
-    if (16 * e < D) {
-      upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
-      const int d = 16 * e + x;
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        acc = upd_mma(Tw[(4 * s + q) * 16 + x], d < D ? sc.Xs[(4 * s + q) * sc.XS + d] : 0.0f, acc);
-      if (d < D) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) upd_gadd(Ga + n.w0.lds + (16 * w + 4 * q + i) * n.w0.stride + d, acc[i], first);
-      }
-    }
-  }
-  // ---- output biases and loss partials (wave 0)
-  if (w == 0) {
-    if (t < n.nout) {   // f64 sum: the softmax outputs' dO cancel across rows
+  // ---- output biases and loss partials (one wave: the last one)
+  if (w == NW - 1) {
+    const int tl_ = l;
+    if (tl_ < n.nout) {   // f64 sum: the softmax outputs' dO cancel across rows
       double acc = 0.0;
 #pragma unroll
-      for (int r = 0; r < UPD_RT; ++r) acc += (double)dOw[r * 16 + t];
-      upd_gadd(Ga + upd_bias_of(n, t), (float)acc, first);
+      for (int r = 0; r < UPD_RT; ++r) acc += (double)dOw[r * 16 + tl_];
+      upd_gadd(Ga + upd_bias_of(n, tl_), (float)acc, first);
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const float s = upd_rsum16(lp[k]);
-      if (t == 0) upd_gadd(Ga + n.Lp + k, s, first);
+      if (tl_ == 0) upd_gadd(Ga + n.Lp + k, s, first);
     }
   }
   upd_wave_sync();   // Tw reads done before the next tile
@@ -799,19 +891,19 @@ __device__ inline void f4set(float4& v, int e, float x) {
 }
 
 // sum of quad q over partials gg = first, first + stride, ... < G (in that order), loads issued
-// in batches of 8 so their latencies overlap
+// in batches of 16 so their latencies overlap
 __device__ inline void upd_sum_partials(__amdgpu_buffer_rsrc_t rs_part, int Qtot, int q, int first,
                                         int stride, int G, double& ax, double& ay, double& az,
                                         double& aw) {
-  for (int g0 = first; g0 < G; g0 += 8 * stride) {
-    float4 v[8];
+  for (int g0 = first; g0 < G; g0 += 16 * stride) {
+    float4 v[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int gg = g0 + u * stride;
       if (gg < G) v[u] = ld4_sc1(rs_part, ((size_t)gg * Qtot + q) * 4);
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       if (g0 + u * stride < G) {
         ax += v[u].x; ay += v[u].y; az += v[u].z; aw += v[u].w;
       }
@@ -824,7 +916,7 @@ __device__ inline void upd_sum_partials(__amdgpu_buffer_rsrc_t rs_part, int Qtot
 // cancel across workgroups), publishes the slice (sc1) and returns this thread's share of the
 // slice's sum of squares (parameter quads only).  Uses scratch as [spl][nq] double4.
 __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_red,
-                                         int Qtot, int Qp, int g, int G, float* scratch) {
+                                         int Qtot, int Qp, int g, int G, float* scratch, int NT) {
   const int t = threadIdx.x;
   const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
   const int nq = qhi - qlo;
@@ -834,9 +926,9 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
     st4_sc1(rs_red, (size_t)(qlo + qi) * 4, r);
     if (qlo + qi < Qp) ssq += r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w;
   };
-  if (nq > UPD_THREADS / 2) {
+  if (nq > NT / 2) {
     // wide slices (few workgroups): each thread owns whole quads, partials summed in order
-    for (int qi = t; qi < nq; qi += UPD_THREADS) {
+    for (int qi = t; qi < nq; qi += NT) {
       double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
       upd_sum_partials(rs_part, Qtot, qlo + qi, 0, 1, G, ax, ay, az, aw);
       fin(qi, ax, ay, az, aw);
@@ -844,7 +936,7 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
   } else if (nq > 0) {
     // narrow slices: split the G partials of each quad over spl threads, combine in LDS
     int spl = 1;
-    while (spl * 2 * nq <= UPD_THREADS && spl * 2 <= G) spl *= 2;
+    while (spl * 2 * nq <= NT && spl * 2 <= G) spl *= 2;
     double* red = reinterpret_cast<double*>(scratch);   // [spl][nq][4]
     if (t < spl * nq) {
       const int qi = t % nq, sub = t / nq;
@@ -868,10 +960,9 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
 
 // NQ = parameter quads per thread (ceil(Lp / 4 / 256)): AdamW's moments live in registers.
 template <int NQ, int KD, int KA>
-__global__ __launch_bounds__(UPD_THREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void
-ppo_update_kernel(UpdArgs args) {
+__device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& args) {
+  constexpr int NW = upd_nw<KD, KA>(), NT = 64 * NW;
   extern __shared__ __align__(16) float upd_lds[];
-  const UpdNet& n = args.net;
   const int t = threadIdx.x, g = blockIdx.x, G = args.G;
   const int Lp = n.Lp;
   const int Qp = Lp / 4;            // parameter quads
@@ -880,16 +971,14 @@ ppo_update_kernel(UpdArgs args) {
   float* W = upd_lds + 64;          // [Lp]
   float* Ga = W + Lp;               // [Lp + 4]
   float* scratch = Ga + Lp + 4;     // tile activations / reduction scratch
-  const UpdScr sc = upd_scr(scratch, n.D);
-  float* s_bcast = hdr;             // [0] clip coefficient, [1] loss
-  float* s_ssq = hdr + 4;           // [4] per-wave sums of squares
+  const UpdScr sc = upd_scr(scratch, n.D, NW);
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
   float* s_adam = hdr + 10;         // [2] this step's AdamW step size, 1 / sqrt(bc2)
 
   // ---- load parameters (LDS image) and this thread's moments (quad q = t + 256 i, registers);
   //      the moments are scattered into the LDS image layout through Ga (free until phase A) ---
   float4 mreg[NQ], vreg[NQ];
-  for (int k = t; k < Lp; k += UPD_THREADS) {
+  for (int k = t; k < Lp; k += NT) {
     const int f = upd_flat_of(n, k);
     W[k] = f >= 0 ? args.params[f] : 0.0f;
     Ga[k] = f >= 0 ? args.exp_avg[f] : 0.0f;
@@ -897,24 +986,24 @@ ppo_update_kernel(UpdArgs args) {
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < NQ; ++i) {
-    const int q = t + i * UPD_THREADS;
+    const int q = t + i * NT;
     mreg[i] = q < Qp ? *reinterpret_cast<const float4*>(Ga + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();
-  for (int k = t; k < Lp; k += UPD_THREADS) {
+  for (int k = t; k < Lp; k += NT) {
     const int f = upd_flat_of(n, k);
     Ga[k] = f >= 0 ? args.exp_avg_sq[f] : 0.0f;
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < NQ; ++i) {
-    const int q = t + i * UPD_THREADS;
+    const int q = t + i * NT;
     vreg[i] = q < Qp ? *reinterpret_cast<const float4*>(Ga + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
   }
   const float step0 = args.adam_step[0];
   if (t < 24) reinterpret_cast<unsigned long long*>(hdr + 16)[t] = 0ull;
   __syncthreads();
-  for (int k = t; k < Lp + 4; k += UPD_THREADS) Ga[k] = 0.0f;   // padding stays 0 for good
+  for (int k = t; k < Lp + 4; k += NT) Ga[k] = 0.0f;   // padding stays 0 for good
   __syncthreads();
 
   const int R = args.R;
@@ -942,20 +1031,24 @@ ppo_update_kernel(UpdArgs args) {
       upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret, myrow0,
                             std::min(UPD_RT, myrows), nin);
     if (myrows == 0) {   // no rows this step: publish zeros
-      for (int k = t; k < Lp + 4; k += UPD_THREADS) Ga[k] = 0.0f;
+      for (int k = t; k < Lp + 4; k += NT) Ga[k] = 0.0f;
     }
     for (int c0 = 0; c0 < myrows; c0 += UPD_RT) {
       const UpdIn<upd_ksm<KA>()> cur = nin;
       if (c0 + UPD_RT < myrows)   // prefetch the next tile of this step
         upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
                               myrow0 + c0 + UPD_RT, std::min(UPD_RT, myrows - c0 - UPD_RT), nin);
-      upd_tile<KD, KA>(args, W, Ga, sc, cur, std::min(UPD_RT, myrows - c0), invB, c0 == 0,
-                       reinterpret_cast<unsigned long long*>(hdr + 16));
+      if (c0 == 0)
+        upd_tile<KD, KA, true>(n, args, W, Ga, sc, cur, std::min(UPD_RT, myrows - c0), invB,
+                               reinterpret_cast<unsigned long long*>(hdr + 16));
+      else
+        upd_tile<KD, KA, false>(n, args, W, Ga, sc, cur, std::min(UPD_RT, myrows - c0), invB,
+                                reinterpret_cast<unsigned long long*>(hdr + 16));
     }
     __syncthreads();
     mark(0);   // phase A compute
     const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(args.red);
-    for (int q = t; q < Qtot; q += UPD_THREADS)
+    for (int q = t; q < Qtot; q += NT)
       st4_sc1(rs_part, ((size_t)g * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -983,16 +1076,10 @@ ppo_update_kernel(UpdArgs args) {
     mark(2);   // wait A
     // ---- phase B: reduce this workgroup's slice over the G partials --------------------------
     {
-      float ssq = upd_slice_reduce(rs_part, rs_red, Qtot, Qp, g, G, scratch);
-      // block sum of ssq (threads < nq hold the pieces; fixed order)
+      float ssq = upd_slice_reduce(rs_part, rs_red, Qtot, Qp, g, G, scratch, NT);
+      // the slice's sum of squares as NW per-wave pieces (fixed DPP tree, lane 63 publishes)
       ssq = wave_sum_f32_to63(ssq);
-      if ((t & 63) == 63) s_ssq[t >> 6] = ssq;
-      __syncthreads();
-      if (t == 0) {
-        float tot = 0.f;
-        for (int w = 0; w < UPD_THREADS / 64; ++w) tot += s_ssq[w];
-        st_sc1f(args.sq + g, tot);
-      }
+      if ((t & 63) == 63) st_sc1f(args.sq + NW * g + (t >> 6), ssq);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       mark(3);   // slice reduce
@@ -1008,28 +1095,25 @@ ppo_update_kernel(UpdArgs args) {
     float4 gq[NQ];   // this thread's gradient quads: loads issued first, in flight under the norm
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
-      const int q = t + i * UPD_THREADS;
+      const int q = t + i * NT;
       if (q < Qp) gq[i] = ld4_sc1(rs_red, (size_t)q * 4);
     }
+    float clipc;
     {
-      float piece = t < G ? ld_sc1f(args.sq + t) : 0.f;     // every workgroup: same tree
+      // every wave of every workgroup sums the NW G pieces in the same order (no LDS, no barrier)
+      const int l = t & 63;
+      float piece = 0.f;
+      for (int i = l; i < NW * G; i += 64) piece += ld_sc1f(args.sq + i);
       piece = wave_sum_f32_to63(piece);
-      if ((t & 63) == 63) s_ssq[t >> 6] = piece;
-      __syncthreads();
-      if (t == 0) {
-        float tot = 0.f;
-        for (int w = 0; w < UPD_THREADS / 64; ++w) tot += s_ssq[w];
-        const float norm = sqrtf(tot);
-        const float coef = args.max_norm / (norm + 1e-6f);
-        s_bcast[0] = coef < 1.0f ? coef : 1.0f;
+      const float tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(piece), 63));
+      const float coef = args.max_norm / (sqrtf(tot) + 1e-6f);
+      clipc = coef < 1.0f ? coef : 1.0f;
+      if (g == 0 && t == 0 && s + 1 == args.total_steps) {
         const float4 lp = ld4_sc1(rs_red, (size_t)Qp * 4);
-        s_bcast[1] = lp.x * invB + args.vf_coef * (lp.y * invB) - args.ent_coef * (lp.z * invB);
+        loss_last = lp.x * invB + args.vf_coef * (lp.y * invB) - args.ent_coef * (lp.z * invB);
       }
-      __syncthreads();
     }
     mark(5);   // norm + loss
-    const float clipc = s_bcast[0];
-    loss_last = s_bcast[1];
     {
       const float step_size = s_adam[0];
       const float inv_bc2_sqrt = s_adam[1];   // scalar divide -> one multiply
@@ -1042,7 +1126,7 @@ ppo_update_kernel(UpdArgs args) {
 #pragma unroll
         for (int b = 0; b < BATCH; ++b) {
           const int i = i0 + b;
-          const int q = t + i * UPD_THREADS;
+          const int q = t + i * NT;
           if (i < NQ && q < Qp) {
             float4 pw = *reinterpret_cast<float4*>(W + 4 * q);
             float4 m4 = mreg[i], v4 = vreg[i];
@@ -1050,13 +1134,14 @@ ppo_update_kernel(UpdArgs args) {
             for (int e = 0; e < 4; ++e) {
               const float gr = f4get(gq[i], e) * clipc;
               float m = f4get(m4, e), v = f4get(v4, e), p = f4get(pw, e);
+              // torch AdamW (decoupled decay; lerp for m; addcmul for v) with fused multiply-adds
               p = p * decay;
-              m = m + omb1 * (gr - m);
-              v = v * b2 + omb2 * gr * gr;
-              const float denom = __builtin_amdgcn_sqrtf(v) * inv_bc2_sqrt + args.eps;
+              m = fmaf(omb1, gr - m, m);
+              v = fmaf(omb2 * gr, gr, v * b2);
+              const float denom = fmaf(__builtin_amdgcn_sqrtf(v), inv_bc2_sqrt, args.eps);
               float rq = __builtin_amdgcn_rcpf(denom);
-              rq = rq * (2.0f - denom * rq);              // one Newton step: ~0.5 ulp
-              p = p - step_size * (m * rq);
+              rq = fmaf(rq, fmaf(-denom, rq, 1.0f), rq);   // one Newton step: ~0.5 ulp
+              p = fmaf(-step_size, m * rq, p);
               f4set(m4, e, m);
               f4set(v4, e, v);
               f4set(pw, e, p);
@@ -1075,11 +1160,11 @@ ppo_update_kernel(UpdArgs args) {
   if (g == 0) {
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
-      const int q = t + i * UPD_THREADS;
+      const int q = t + i * NT;
       if (q < Qp) *reinterpret_cast<float4*>(Ga + 4 * q) = mreg[i];
     }
     __syncthreads();
-    for (int k = t; k < Lp; k += UPD_THREADS) {
+    for (int k = t; k < Lp; k += NT) {
       const int f = upd_flat_of(n, k);
       if (f >= 0) {
         args.params[f] = W[k];
@@ -1089,11 +1174,11 @@ ppo_update_kernel(UpdArgs args) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
-      const int q = t + i * UPD_THREADS;
+      const int q = t + i * NT;
       if (q < Qp) *reinterpret_cast<float4*>(Ga + 4 * q) = vreg[i];
     }
     __syncthreads();
-    for (int k = t; k < Lp; k += UPD_THREADS) {
+    for (int k = t; k < Lp; k += NT) {
       const int f = upd_flat_of(n, k);
       if (f >= 0) args.exp_avg_sq[f] = Ga[k];
     }
@@ -1109,19 +1194,31 @@ ppo_update_kernel(UpdArgs args) {
   }
 }
 
+// KDIM > 0: the observation dim is a compile-time constant and the whole parameter layout folds
+// into immediates (the specialised shapes); KDIM = 0: runtime layout from the kernel argument.
+template <int NQ, int KD, int KA, int KDIM>
+__global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_update_kernel(UpdArgs args) {
+  if constexpr (KDIM > 0) {
+    constexpr UpdNet N = upd_make(KDIM, KA, KD);
+    ppo_update_body<NQ, KD, KA>(N, args);
+  } else {
+    ppo_update_body<NQ, KD, KA>(args.net, args);
+  }
+}
+
 // ActorCritic.get_evaluate over N rows (PPO.learn's policy_old pass, PPO.py:127-154):
 // log_prob, state value and (optionally) entropy per row, with exactly the update kernel's
 // forward arithmetic, so the first minibatch of learn() sees ratio == 1 exactly, as in the
 // reference.  Workgroups stride over 8-row chunks; parameters are staged once into LDS.
 template <int KD, int KA>
-__global__ __launch_bounds__(UPD_THREADS, 1) void ppo_evaluate_kernel(UpdArgs args, float* logp_out,
-                                                                    float* V_out, float* H_out) {
+__device__ __forceinline__ void ppo_evaluate_body(const UpdNet& n, const UpdArgs& args, float* logp_out,
+                                                  float* V_out, float* H_out) {
+  constexpr int NW = upd_nw<KD, KA>(), NT = 64 * NW;
   extern __shared__ __align__(16) float upd_lds[];
-  const UpdNet& n = args.net;
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   float* W = upd_lds + 64;
-  const UpdScr sc = upd_scr(W + n.Lp, n.D);
-  for (int k = t; k < n.Lp; k += UPD_THREADS) {
+  const UpdScr sc = upd_scr(W + n.Lp, n.D, NW);
+  for (int k = t; k < n.Lp; k += NT) {
     const int f = upd_flat_of(n, k);
     W[k] = f >= 0 ? args.params[f] : 0.0f;
   }
@@ -1132,11 +1229,11 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_evaluate_kernel(UpdArgs ar
     const int rc = (int)std::min<int64_t>(UPD_RT, args.N - row0);
     UpdIn<upd_ksm<KA>()> in;
     upd_tile_load<KD, KA>(n, args.S, args.act, nullptr, nullptr, nullptr, row0, rc, in);
-    UpdFwd<upd_ksm<KA>()> f;
+    UpdFwd<upd_ksm<KA>(), upd_hpw<NW>()> f;
     upd_tile_fwd<KD, KA>(n, W, sc, in, f);
     __syncthreads();
     if (w == 0) {
-      const float* Orow = upd_tile_outputs(n, W, sc);
+      const float* Orow = upd_tile_outputs<NW>(n, W, sc);
       if (q == 0 && x < rc) {
         UpdDist d;
         upd_row_dist<KD, KA>(n, Orow, sc.Rin + x * UPD_RIN, d);
@@ -1149,6 +1246,17 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_evaluate_kernel(UpdArgs ar
   }
 }
 
+template <int KD, int KA, int KDIM>
+__global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_evaluate_kernel(UpdArgs args, float* logp_out,
+                                                                              float* V_out, float* H_out) {
+  if constexpr (KDIM > 0) {
+    constexpr UpdNet N = upd_make(KDIM, KA, KD);
+    ppo_evaluate_body<KD, KA>(N, args, logp_out, V_out, H_out);
+  } else {
+    ppo_evaluate_body<KD, KA>(args.net, args, logp_out, V_out, H_out);
+  }
+}
+
 // ---- stepped mode (world_size > 1): one optimizer step = grad kernel -> RCCL all-reduce of the
 // flat gradient (caller) -> AdamW kernel.  Parameters and moments live in HBM in the LDS-image
 // layout between launches ("images"); prl_ppo_image converts to / from torch's flat vectors.
@@ -1158,24 +1266,24 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_evaluate_kernel(UpdArgs ar
 // quad: loss partials {sum -min(s1,s2), sum SmoothL1, sum H}).  inv_count = 1 / (rows of the
 // union minibatch over all ranks), so the all-reduced sum is the union's gradient.
 template <int KD, int KA>
-__global__ __launch_bounds__(UPD_THREADS, 1) void ppo_grad_kernel(UpdArgs args, const float* img,
-                                                                float* grad_out, int64_t row0,
-                                                                int B_local, float inv_count) {
+__device__ __forceinline__ void ppo_grad_body(const UpdNet& n, const UpdArgs& args, const float* img,
+                                              float* grad_out, int64_t row0, int B_local,
+                                              float inv_count) {
+  constexpr int NW = upd_nw<KD, KA>(), NT = 64 * NW;
   extern __shared__ __align__(16) float upd_lds[];
-  const UpdNet& n = args.net;
   const int t = threadIdx.x, g = blockIdx.x, G = args.G;
   const int Lp = n.Lp, Qp = Lp / 4, Qtot = Qp + 1;
   float* hdr = upd_lds;
   float* W = upd_lds + 64;
   float* Ga = W + Lp;
   float* scratch = Ga + Lp + 4;
-  const UpdScr sc = upd_scr(scratch, n.D);
+  const UpdScr sc = upd_scr(scratch, n.D, NW);
   float* s_ssq = hdr + 4;
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
   unsigned long long* tm = reinterpret_cast<unsigned long long*>(hdr + 16);
-  for (int q = t; q < Qp; q += UPD_THREADS)   // written by the previous launch: plain loads
+  for (int q = t; q < Qp; q += NT)   // written by the previous launch: plain loads
     *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(img + 4 * q);
-  for (int k = t; k < Lp + 4; k += UPD_THREADS) Ga[k] = 0.0f;
+  for (int k = t; k < Lp + 4; k += NT) Ga[k] = 0.0f;
   if (t < 24) tm[t] = 0ull;
   __syncthreads();
   const int R = args.R;
@@ -1185,11 +1293,12 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_grad_kernel(UpdArgs args, 
     UpdIn<upd_ksm<KA>()> in;
     upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
                           row0 + (int64_t)g * R + c0, rc, in);
-    upd_tile<KD, KA>(args, W, Ga, sc, in, rc, inv_count, c0 == 0, tm);
+    if (c0 == 0) upd_tile<KD, KA, true>(n, args, W, Ga, sc, in, rc, inv_count, tm);
+    else upd_tile<KD, KA, false>(n, args, W, Ga, sc, in, rc, inv_count, tm);
   }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(grad_out);
-  for (int q = t; q < Qtot; q += UPD_THREADS)
+  for (int q = t; q < Qtot; q += NT)
     st4_sc1(rs_part, ((size_t)g * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1199,8 +1308,20 @@ __global__ __launch_bounds__(UPD_THREADS, 1) void ppo_grad_kernel(UpdArgs args, 
   }
   __syncthreads();
   if (*s_abort) return;
-  upd_slice_reduce(rs_part, rs_red, Qtot, Qp, g, G, scratch);
+  upd_slice_reduce(rs_part, rs_red, Qtot, Qp, g, G, scratch, NT);
   (void)s_ssq;
+}
+
+template <int KD, int KA, int KDIM>
+__global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_grad_kernel(UpdArgs args, const float* img,
+                                                                float* grad_out, int64_t row0,
+                                                                int B_local, float inv_count) {
+  if constexpr (KDIM > 0) {
+    constexpr UpdNet N = upd_make(KDIM, KA, KD);
+    ppo_grad_body<KD, KA>(N, args, img, grad_out, row0, B_local, inv_count);
+  } else {
+    ppo_grad_body<KD, KA>(args.net, args, img, grad_out, row0, B_local, inv_count);
+  }
 }
 
 // clip_grad_norm_(max_norm) + AdamW on the images, one parameter quad per thread.  Every
@@ -1287,71 +1408,34 @@ using namespace prl;
 
 namespace {
 
-// LDS image + flat offsets of the reference's parameter tensors, torch parameters() order.
-bool upd_layout(int D, int A, int discrete, UpdNet& n) {
-  if (D < 1 || D > UPD_MAXD || A < 1 || A > UPD_MAXA) return false;
-  n = UpdNet{};
-  n.D = D;
-  n.A = A;
-  n.discrete = discrete ? 1 : 0;
-  n.nh = discrete ? 2 : 3;
-  int flat = 0, lds = 0;
-  auto add = [&](UpdTensor& t, int rows, int cols, int stride) {
-    t.flat = flat;
-    t.lds = lds;
-    t.rows = rows;
-    t.cols = cols;
-    t.stride = stride;
-    flat += rows * cols;
-    lds += (rows * stride + 3) & ~3;
-  };
-  add(n.w0, UPD_H, D, D | 1);
-  add(n.g0, 1, UPD_H, UPD_H);
-  add(n.b0, 1, UPD_H, UPD_H);
-  int col = 0;
-  for (int h = 0; h < n.nh; ++h) {
-    const int out = (h == n.nh - 1) ? 1 : A;
-    n.out[h] = out;
-    n.ocol[h] = col;
-    col += out;
-    add(n.w1[h], UPD_H, UPD_H, UPD_HS);
-    add(n.g1[h], 1, UPD_H, UPD_H);
-    add(n.b1[h], 1, UPD_H, UPD_H);
-    add(n.w2[h], out, UPD_H, UPD_HS);
-    add(n.b2[h], 1, out, out);
-  }
-  n.nout = col;
-  if (n.nout > UPD_MAXO) return false;   // one 16-row output tile
-  n.P = flat;
-  n.Lp = lds;
-  return true;
-}
-
-int upd_nq(const UpdNet& n) { return (int)cdiv(n.Lp / 4, UPD_THREADS); }
+// waves per workgroup of the kernels chosen for this shape (upd_nw<KD, KA>() on the device)
+int upd_nw_host(const UpdNet& n) { (void)n; return 4; }
+int upd_nt(const UpdNet& n) { return 64 * upd_nw_host(n); }
+int upd_nq(const UpdNet& n) { return (int)cdiv(n.Lp / 4, upd_nt(n)); }
 // Specialisations for the configs' shapes (CartPole: discrete, A = 2; Pendulum: continuous,
 // A = 1); every other shape runs the generic (runtime head configuration) kernel.
 const void* upd_kernel_for(const UpdNet& n) {
   const int nq = upd_nq(n);
-  if (n.discrete && n.A == 2 && n.D <= 16 && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2>);
-  if (!n.discrete && n.A == 1 && n.D <= 16 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1>);
-  if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0>);
+  if (n.discrete && n.A == 2 && n.D == 4 && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4>);
+  if (!n.discrete && n.A == 1 && n.D == 3 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3>);
+  if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0>);
   return nullptr;
 }
 const void* upd_grad_kernel_for(const UpdNet& n) {
-  if (n.discrete && n.A == 2 && n.D <= 16) return reinterpret_cast<const void*>(ppo_grad_kernel<1, 2>);
-  if (!n.discrete && n.A == 1 && n.D <= 16) return reinterpret_cast<const void*>(ppo_grad_kernel<0, 1>);
-  return reinterpret_cast<const void*>(ppo_grad_kernel<-1, 0>);
+  if (n.discrete && n.A == 2 && n.D == 4) return reinterpret_cast<const void*>(ppo_grad_kernel<1, 2, 4>);
+  if (!n.discrete && n.A == 1 && n.D == 3) return reinterpret_cast<const void*>(ppo_grad_kernel<0, 1, 3>);
+  return reinterpret_cast<const void*>(ppo_grad_kernel<-1, 0, 0>);
 }
 const void* upd_eval_kernel_for(const UpdNet& n) {
-  if (n.discrete && n.A == 2 && n.D <= 16) return reinterpret_cast<const void*>(ppo_evaluate_kernel<1, 2>);
-  if (!n.discrete && n.A == 1 && n.D <= 16) return reinterpret_cast<const void*>(ppo_evaluate_kernel<0, 1>);
-  return reinterpret_cast<const void*>(ppo_evaluate_kernel<-1, 0>);
+  if (n.discrete && n.A == 2 && n.D == 4) return reinterpret_cast<const void*>(ppo_evaluate_kernel<1, 2, 4>);
+  if (!n.discrete && n.A == 1 && n.D == 3) return reinterpret_cast<const void*>(ppo_evaluate_kernel<0, 1, 3>);
+  return reinterpret_cast<const void*>(ppo_evaluate_kernel<-1, 0, 0>);
 }
 
 int upd_grid(int64_t mb) { return (int)std::min<int64_t>(256, cdiv(mb, UPD_RT)); }
 
 size_t upd_lds_bytes(const UpdNet& n) {
-  return sizeof(float) * (size_t)(64 + 2 * n.Lp + 4 + upd_scratch_floats(n.D));
+  return sizeof(float) * (size_t)(64 + 2 * n.Lp + 4 + upd_scratch_floats(n.D, upd_nw_host(n)));
 }
 
 struct UpdWs {
@@ -1362,12 +1446,12 @@ struct UpdWs {
   float* part;
 };
 
-// workspace: ctr[4] (16 B, zeroed per launch) | prof[32] | sq[256] | red[Qtot*4] | part[G][Qtot*4]
+// workspace: ctr[4] (16 B, zeroed per launch) | prof[32] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4]
 size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
   const size_t Qtot = (size_t)n.Lp / 4 + 1;
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-  const size_t o_ctr = take(16), o_prof = take(256), o_sq = take(256 * 4), o_red = take(Qtot * 16),
+  const size_t o_ctr = take(16), o_prof = take(256), o_sq = take(2048 * 4), o_red = take(Qtot * 16),
                o_part = take((size_t)G * Qtot * 16);
   if (ws) {
     ws->ctr = reinterpret_cast<unsigned*>(base + o_ctr);
@@ -1457,7 +1541,7 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
   void* kargs[] = {&args};
-  PRL_HIP_TRY(hipLaunchCooperativeKernel(kern, dim3(G), dim3(UPD_THREADS), kargs, (unsigned)lds, st));
+  PRL_HIP_TRY(hipLaunchCooperativeKernel(kern, dim3(G), dim3(upd_nt(args.net)), kargs, (unsigned)lds, st));
   return PRL_OK;
 }
 
@@ -1473,13 +1557,13 @@ extern "C" int prl_ppo_evaluate(const float* params, int32_t D, int32_t A, int32
   args.S = S;
   args.act = actions;
   args.N = N;
-  const size_t lds = sizeof(float) * (size_t)(64 + args.net.Lp + upd_scratch_floats(D));
+  const size_t lds = sizeof(float) * (size_t)(64 + args.net.Lp + upd_scratch_floats(D, upd_nw_host(args.net)));
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_evaluate: %zu B of LDS needed", lds);
   const unsigned grid = (unsigned)std::min<int64_t>(cdiv(N, UPD_RT), 2 * 256);
   const void* kern = upd_eval_kernel_for(args.net);
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   void* kargs[] = {&args, &logp, &V, &entropy};
-  PRL_HIP_TRY(hipLaunchKernel(kern, dim3(grid), dim3(UPD_THREADS), kargs, lds, as_stream(stream)));
+  PRL_HIP_TRY(hipLaunchKernel(kern, dim3(grid), dim3(upd_nt(args.net)), kargs, lds, as_stream(stream)));
   return PRL_OK;
 }
 
@@ -1545,7 +1629,7 @@ extern "C" int prl_ppo_grad_step(const float* img_params, int32_t D, int32_t A, 
   void* kargs[] = {&args, &img, &grad_out, &r0, &bl, &inv};
   // plain launch: G <= 256 workgroups of 1 per CU are co-resident in practice; the in-kernel
   // wait is bounded and reports a timeout through the status word like the persistent kernel
-  PRL_HIP_TRY(hipLaunchKernel(kern, dim3(G), dim3(UPD_THREADS), kargs, lds, st));
+  PRL_HIP_TRY(hipLaunchKernel(kern, dim3(G), dim3(upd_nt(args.net)), kargs, lds, st));
   return PRL_OK;
 }
 
