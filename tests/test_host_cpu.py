@@ -205,3 +205,15 @@ def test_save_load_weights_roundtrip(tmp_path):
         assert torch.equal(v, b.policy.state_dict()[k])
         assert torch.equal(v, b.policy_old.state_dict()[k])
     b.load_weights(str(tmp_path / "missing"))  # FileNotFoundError swallowed (PPO.py:276-277)
+
+
+def test_kernel_bench_tool_imports():
+    """tools/kernel_bench.py (the PMC passes of tools/gpu_benchprof.sh) binds bench.py's
+    constants at import: keep the two in step (no GPU needed to import)."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("kernel_bench", os.path.join(root, "tools", "kernel_bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.CARTPOLE_STEP_BYTES == 111 and mod.GAE_BYTES_PER_TRANSITION == 20

@@ -15,7 +15,9 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "parallel-reinforcement-learning_amd")]
 import prl_native  # noqa: E402
-from bench import CARTPOLE_STEP_BYTES, GAE_BYTES_PER_TRANSITION, HBM_PEAK_GBS, time_kernel  # noqa
+from bench import ENV_STEP_BYTES, GAE_BYTES_PER_TRANSITION, HBM_PEAK_GBS, time_kernel  # noqa
+
+CARTPOLE_STEP_BYTES = ENV_STEP_BYTES["CartPole-v1"]
 
 
 def gae_case(n, pd=0.05, seg=None, reps=10):
