@@ -254,6 +254,10 @@ int prl_ppo_adam_step(float* img_params, float* img_m, float* img_v, int32_t D, 
 /* Host call: device address of the u32 status words inside an engine workspace ([0] last
  * launch, [1] sticky timeout flag). */
 int prl_ppo_update_status_ptr(void* workspace, uint32_t** status);
+/* The engine's timing words in `workspace` (u64[32]: workgroup 0's s_memrealtime ticks per phase
+ * and per tile stage, summed over the launch's steps; [7] = steps; [30], [31] = wall ticks and
+ * shader clocks of the launch).  Instrumentation of this build, no reference counterpart. */
+int prl_ppo_update_profile_ptr(void* workspace, uint64_t** prof);
 
 #ifdef __cplusplus
 }

@@ -113,7 +113,7 @@ class FusedUpdate:
     def profile(self):
         """Workgroup 0's time per phase of the last launch, us per step (s_memrealtime, 100 MHz);
         'chunk' splits forward+backward by stage (summed over the step's 16-row tiles)."""
-        p = self.ws[256:512].view(torch.int64).tolist()
+        p = prl_native.ppo_update_profile(self.ws).tolist()
         steps = max(p[7], 1)
         out = {name: round(p[i] * 0.01 / steps, 2) for i, name in enumerate(self.PHASES)}
         out["chunk"] = {name: round(p[8 + i] * 0.01 / steps, 2)

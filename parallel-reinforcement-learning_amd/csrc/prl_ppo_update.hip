@@ -167,6 +167,44 @@ __device__ inline unsigned ld_sc1u(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// 8-way sharded arrival counters (shard k at word 32 (1 + k) of its block, one 128-B line each):
+// an arrival adds to shard g & 7, so at most G / 8 atomics meet on one line; a whole wave polls,
+// lanes 0..7 one shard each, and the DPP sum over the 8 lanes is the arrival count.
+constexpr int UPD_SHARDS = 8;
+constexpr int UPD_CTR_A = 32;                              // first shard word of counter A
+constexpr int UPD_CTR_B = UPD_CTR_A + 32 * UPD_SHARDS;     // ... of counter B
+constexpr int UPD_CTR_WORDS = UPD_CTR_B + 32 * UPD_SHARDS;
+__device__ inline void upd_arrive(unsigned* ctr, int base, int g) {
+  __hip_atomic_fetch_add(ctr + base + 32 * (g & (UPD_SHARDS - 1)), 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline unsigned upd_isum8(unsigned v) {
+  v += (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  v += (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  v += (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+  return v;
+}
+// one whole wave: wait until the shards of counter `base` sum to >= target; false on timeout /
+// abort (same abort / status / sticky words as upd_wait)
+__device__ inline bool upd_wait_sharded(unsigned* ctr, int base, unsigned target) {
+  const int l = threadIdx.x & 63;
+  for (unsigned spins = 0;; ++spins) {
+    const unsigned v = l < UPD_SHARDS ? ld_sc1u(ctr + base + 32 * l) : 0u;
+    const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)upd_isum8(v), 0);
+    if (tot >= target) return true;
+    if (ld_sc1u(ctr + 2) != 0u) return false;
+    if (spins > UPD_SPIN_LIMIT) {
+      if (l == 0) {
+        __hip_atomic_store(ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_or(ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // one lane: wait until *c >= target (or abort); false on timeout / abort
 __device__ inline bool upd_wait(unsigned* ctr, int which, unsigned target) {
   for (unsigned spins = 0;; ++spins) {
@@ -1061,15 +1099,18 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
         upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
                               nmb0 + (int64_t)g * R, std::min(UPD_RT, nrows), nin);
     }
-    if (t == 0) {
-      __hip_atomic_fetch_add(args.ctr + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // this step's AdamW bias corrections (float64 pow, as torch's AdamW), off the critical path
-      const double tstep = (double)step0 + (double)(s + 1);
-      const double bc1 = 1.0 - pow((double)args.beta1, tstep);
-      const double bc2 = 1.0 - pow((double)args.beta2, tstep);
-      s_adam[0] = (float)((double)args.lr / bc1);   // step size
-      s_adam[1] = (float)(1.0 / sqrt(bc2));         // 1 / sqrt(bias correction 2)
-      *s_abort = upd_wait(args.ctr, 0, (unsigned)G * (unsigned)(s + 1)) ? 0 : 1;
+    if (t < 64) {
+      if (t == 0) {
+        upd_arrive(args.ctr, UPD_CTR_A, g);
+        // this step's AdamW bias corrections (float64 pow, as torch's AdamW), off the critical path
+        const double tstep = (double)step0 + (double)(s + 1);
+        const double bc1 = 1.0 - pow((double)args.beta1, tstep);
+        const double bc2 = 1.0 - pow((double)args.beta2, tstep);
+        s_adam[0] = (float)((double)args.lr / bc1);   // step size
+        s_adam[1] = (float)(1.0 / sqrt(bc2));         // 1 / sqrt(bias correction 2)
+      }
+      const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));
+      if (t == 0) *s_abort = ok ? 0 : 1;
     }
     __syncthreads();
     if (*s_abort) return;
@@ -1083,9 +1124,10 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       mark(3);   // slice reduce
-      if (t == 0) {
-        __hip_atomic_fetch_add(args.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_abort = upd_wait(args.ctr, 1, (unsigned)G * (unsigned)(s + 1)) ? 0 : 1;
+      if (t < 64) {
+        if (t == 0) upd_arrive(args.ctr, UPD_CTR_B, g);
+        const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_B, (unsigned)G * (unsigned)(s + 1));
+        if (t == 0) *s_abort = ok ? 0 : 1;
       }
       __syncthreads();
       if (*s_abort) return;
@@ -1446,12 +1488,12 @@ struct UpdWs {
   float* part;
 };
 
-// workspace: ctr[4] (16 B, zeroed per launch) | prof[32] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4]
+// workspace: ctr[UPD_CTR_WORDS] (words 0-3 and the shards zeroed per launch, word 4 sticky) | prof[32] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4]
 size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
   const size_t Qtot = (size_t)n.Lp / 4 + 1;
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-  const size_t o_ctr = take(16), o_prof = take(256), o_sq = take(2048 * 4), o_red = take(Qtot * 16),
+  const size_t o_ctr = take(4 * UPD_CTR_WORDS), o_prof = take(256), o_sq = take(2048 * 4), o_red = take(Qtot * 16),
                o_part = take((size_t)G * Qtot * 16);
   if (ws) {
     ws->ctr = reinterpret_cast<unsigned*>(base + o_ctr);
@@ -1540,6 +1582,7 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
   PRL_REQUIRE(kern, "prl_ppo_update: %d parameter quads per thread not built", upd_nq(args.net));
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
+  PRL_HIP_TRY(hipMemsetAsync(ws.ctr + UPD_CTR_A, 0, 4 * (UPD_CTR_WORDS - UPD_CTR_A), st));
   void* kargs[] = {&args};
   PRL_HIP_TRY(hipLaunchCooperativeKernel(kern, dim3(G), dim3(upd_nt(args.net)), kargs, (unsigned)lds, st));
   return PRL_OK;
@@ -1652,5 +1695,15 @@ extern "C" int prl_ppo_adam_step(float* img_params, float* img_m, float* img_v, 
 extern "C" int prl_ppo_update_status_ptr(void* workspace, uint32_t** status) {
   PRL_REQUIRE(workspace && status, "prl_ppo_update_status_ptr: null pointer");
   *status = reinterpret_cast<uint32_t*>(workspace) + 3;
+  return PRL_OK;
+}
+
+// the engine's per-phase timing words (u64 [32], workgroup 0, see PPO/engine.py FusedUpdate.profile)
+extern "C" int prl_ppo_update_profile_ptr(void* workspace, uint64_t** prof) {
+  PRL_REQUIRE(workspace && prof, "prl_ppo_update_profile_ptr: null pointer");
+  UpdWs ws;
+  UpdNet n{};
+  upd_ws_carve(n, 1, reinterpret_cast<char*>(workspace), &ws);
+  *prof = reinterpret_cast<uint64_t*>(ws.prof);
   return PRL_OK;
 }

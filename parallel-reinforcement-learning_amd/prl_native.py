@@ -54,6 +54,7 @@ SIGNATURES = {
     "prl_ppo_update": [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I32]
                       + [_F32] * 9 + [_P, _P, _I64, _P],
     "prl_ppo_update_status_ptr": [_P, _P],
+    "prl_ppo_update_profile_ptr": [_P, _P],
     "prl_ppo_evaluate": [_P, _I32, _I32, _I32, _P, _P, _I64, _P, _P, _P, _P],
     "prl_ppo_image_floats": [_I32, _I32, _I32],
     "prl_ppo_image": [_I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32, _P],
@@ -411,6 +412,15 @@ def ppo_update_status(workspace) -> torch.Tensor:
     _check(lib().prl_ppo_update_status_ptr(_dev(workspace, torch.uint8, "workspace"),
                                            ctypes.byref(ptr)), "prl_ppo_update_status_ptr")
     return workspace[12:20].view(torch.int32)
+
+
+def ppo_update_profile(workspace) -> torch.Tensor:
+    """Device i64 view of the engine's 32 timing words (engine.FusedUpdate.profile)."""
+    ptr = ctypes.c_void_p()
+    _check(lib().prl_ppo_update_profile_ptr(_dev(workspace, torch.uint8, "workspace"),
+                                            ctypes.byref(ptr)), "prl_ppo_update_profile_ptr")
+    off = int(ptr.value) - workspace.data_ptr()
+    return workspace[off:off + 256].view(torch.int64)
 
 
 def ppo_image_floats(D, A, discrete) -> int:
