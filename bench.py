@@ -220,9 +220,12 @@ def main():
         avg_ms = float(np.mean(ms))
         flops = fpr * rows
         achieved = flops / (avg_ms * 1e-3) / 1e12
-        what = ("persistent fused PPO update: the whole k_epochs x minibatch loop in one launch"
-                if kern == "ppo_update_kernel" else
-                "stepped engine: one minibatch's gradient on this rank per launch")
+        what = {"ppo_update_kernel": "persistent fused PPO update: the whole k_epochs x "
+                                     "minibatch loop in one launch",
+                "ppo_update_dp": "data-parallel engine: the whole loop enqueued natively, per "
+                                 "step gradient kernel -> RCCL all-reduce -> AdamW kernel; "
+                                 "time = events around the loop",
+                }.get(kern, "stepped engine: one minibatch's gradient on this rank per launch")
         roofline = {"kernel": f"{kern} ({what})",
                     "bound": "mfma", "achieved": round(achieved, 3), "peak": F32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / F32_PEAK_TFLOPS, 5),

@@ -259,6 +259,28 @@ int prl_ppo_update_status_ptr(void* workspace, uint32_t** status);
  * shader clocks of the launch).  Instrumentation of this build, no reference counterpart. */
 int prl_ppo_update_profile_ptr(void* workspace, uint64_t** prof);
 
+/* ---- data-parallel update loop (world > 1): PPO.py:216-255 per rank, one optimizer step =
+ * prl_ppo_grad_step -> all-reduce of the gradient image -> prl_ppo_adam_step, enqueued from C
+ * (no Python per step).  RCCL is resolved at run time from `lib_path` (the librccl torch
+ * loaded); the communicator is the engine's own, built from a unique id the caller broadcasts
+ * over torch.distributed.  No reference counterpart (the reference is single-process). */
+int prl_dp_rccl_open(const char* lib_path);
+int prl_dp_unique_id(uint8_t* id_out, int64_t id_bytes);
+int prl_dp_comm_init(const uint8_t* id, int64_t id_bytes, int32_t nranks, int32_t rank,
+                     void** comm);
+int prl_dp_comm_destroy(void* comm);
+/* counts[j] = rows of union minibatch j over all ranks (host array, nb entries); step0 = AdamW
+ * steps taken so far.  Semantics = nb x k_epochs calls of prl_ppo_grad_step(j, 1 / counts[j])
+ * + all-reduce + prl_ppo_adam_step(step0 + 1 + ...), bit for bit. */
+int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, int32_t D, int32_t A,
+                      int32_t discrete, const float* S, const float* actions,
+                      const float* old_logp, const float* adv, const float* ret, int64_t N,
+                      int32_t mini_batch, int32_t k_epochs, int64_t nb, const int64_t* counts,
+                      int64_t step0, float clip, float vf_coef, float ent_coef, float lr,
+                      float beta1, float beta2, float eps, float weight_decay, float max_norm,
+                      float* grad, float* loss_out, void* workspace, int64_t workspace_bytes,
+                      void* comm, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -301,9 +301,10 @@ class PPO:
                     self.last_loss = eng.run(S, A, old_logp, adv, returns, self.k_epochs).clone()
                     self.last_update_path = "fused"
                 else:
+                    comm = eng.dp_comm()
                     self.last_loss = eng.run_stepped(S, A, old_logp, adv, returns, self.k_epochs,
-                                                     n_ranks, self.all_reduce).clone()
-                    self.last_update_path = "fused-dp"
+                                                     n_ranks, self.all_reduce, comm=comm).clone()
+                    self.last_update_path = "fused-dp" + ("-native" if comm is not None else "")
                 self.last_graph_replays = 0
                 return
         self.last_update_path = "graph" if self.use_graphs else "eager"

@@ -10,6 +10,9 @@ shapes outside the engine) continues exactly where the engine stopped.
 """
 from __future__ import annotations
 
+import os
+import warnings
+
 import torch
 
 import prl_native
@@ -151,11 +154,46 @@ class FusedUpdate:
         return self.loss.reshape(())
 
     # ------------------------------------------------------------------ stepped (world_size > 1)
-    def run_stepped(self, S, A, old_logp, adv, ret, k_epochs: int, n_ranks, all_reduce):
+    def dp_comm(self):
+        """This engine's own RCCL communicator for the native step loop (world > 1 on the nccl
+        backend), or None: then run_stepped loops in Python with torch's all_reduce.  Every rank
+        opens RCCL and votes; the communicator is built only if all ranks could open it.
+        PRL_DP_NATIVE=0 disables it."""
+        if getattr(self, "_comm_tried", False):
+            return self._comm
+        self._comm_tried, self._comm = True, None
+        if os.environ.get("PRL_DP_NATIVE", "1") == "0":
+            return None
+        import torch.distributed as tdist
+        if not (tdist.is_available() and tdist.is_initialized() and tdist.get_backend() == "nccl"):
+            return None
+        dev = self.ws.device
+        ok = torch.ones(1, dtype=torch.int32, device=dev)
+        try:
+            prl_native.dp_rccl_open()
+        except (RuntimeError, OSError) as e:
+            warnings.warn(f"native data-parallel loop unavailable ({e}); using the Python loop")
+            ok.zero_()
+        tdist.all_reduce(ok, op=tdist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            return None
+        world, rank = tdist.get_world_size(), tdist.get_rank()
+        uid = torch.zeros(prl_native.RCCL_UNIQUE_ID_BYTES, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(prl_native.dp_unique_id()), dtype=torch.uint8))
+        tdist.broadcast(uid, src=0)
+        self._comm = prl_native.dp_comm_init(bytes(uid.cpu().numpy().tobytes()), world, rank)
+        return self._comm
+
+    def run_stepped(self, S, A, old_logp, adv, ret, k_epochs: int, n_ranks, all_reduce,
+                    comm=None):
         """The same update loop for data-parallel ranks: per optimizer step, prl_ppo_grad_step
         (this rank's slice of the union minibatch j, scaled by 1 / union rows) -> all_reduce of
         the flat gradient (RCCL over xGMI on the GPU node) -> prl_ppo_adam_step.  Parameters and
-        moments stay in the engine's image layout in HBM for the whole loop."""
+        moments stay in the engine's image layout in HBM for the whole loop.  With `comm` (an
+        RCCL communicator from dp_comm()) the loop is enqueued natively (prl_ppo_update_dp: no
+        Python per step, ncclAllReduce on torch's stream); otherwise it runs here, calling
+        `all_reduce` on the gradient image every step.  Both give the same bits."""
         import ctypes
         if not self.bound():
             self._bind()
@@ -191,6 +229,21 @@ class FusedUpdate:
                      P(self.loss.data_ptr()), stream)
         step = int(round(float(self.step.item())))
         n_local = int(S.shape[0])
+        if comm is not None:
+            if self.events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            prl_native.ppo_update_dp(img_p, img_m, img_v, self.D, self.A, self.discrete, *tens,
+                                     mb, k_epochs, counts, step, self.ppo.policy_clip,
+                                     self.ppo.value_coef, self.ppo.entropy_coef, group["lr"],
+                                     beta1, beta2, group["eps"], group["weight_decay"], 2.0,
+                                     self.grad, self.loss, self.ws, comm)
+            if self.events is not None:
+                ev[1].record()
+                self.events.append(("ppo_update_dp", ev[0], ev[1], n_local * k_epochs,
+                                    k_epochs * nb))
+            step += k_epochs * nb
+            k_epochs = 0   # the Python loop below has nothing left to do
         for _ in range(k_epochs):
             for j in range(nb):
                 inv = ctypes.c_float(1.0 / counts[j])

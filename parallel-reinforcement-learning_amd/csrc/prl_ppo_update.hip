@@ -39,6 +39,10 @@
 
 #include <algorithm>
 
+#include <dlfcn.h>
+#include <string.h>
+#include <rccl/rccl.h>
+
 namespace prl {
 
 constexpr int UPD_THREADS = 256;
@@ -132,6 +136,7 @@ struct UpdArgs {
   unsigned* ctr;    // [0] arrivals A, [1] arrivals B, [2] abort, [3] status (zeroed per launch),
                     // [4] sticky timeout flag (never zeroed by a launch)
   unsigned long long* prof;  // [8] workgroup 0's time per phase (100 MHz ticks, summed over steps)
+  unsigned grad_target;      // ppo_grad_kernel: arrivals on ctr[0] that end its hand-off
 };
 
 // ---- sc1 (write-through / L1-bypassing) accessors -------------------------------------------
@@ -1346,7 +1351,7 @@ __device__ __forceinline__ void ppo_grad_body(const UpdNet& n, const UpdArgs& ar
   __syncthreads();
   if (t == 0) {
     __hip_atomic_fetch_add(args.ctr + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *s_abort = upd_wait(args.ctr, 0, (unsigned)G) ? 0 : 1;
+    *s_abort = upd_wait(args.ctr, 0, args.grad_target) ? 0 : 1;
   }
   __syncthreads();
   if (*s_abort) return;
@@ -1660,6 +1665,7 @@ extern "C" int prl_ppo_grad_step(const float* img_params, int32_t D, int32_t A, 
   args.vf_coef = vf_coef;
   args.part = ws.part;
   args.ctr = ws.ctr;
+  args.grad_target = (unsigned)G;
   const size_t lds = upd_lds_bytes(args.net);
   hipStream_t st = as_stream(stream);
   const void* kern = upd_grad_kernel_for(args.net);
@@ -1705,5 +1711,140 @@ extern "C" int prl_ppo_update_profile_ptr(void* workspace, uint64_t** prof) {
   UpdNet n{};
   upd_ws_carve(n, 1, reinterpret_cast<char*>(workspace), &ws);
   *prof = reinterpret_cast<uint64_t*>(ws.prof);
+  return PRL_OK;
+}
+
+// ---- data-parallel step loop without Python per step (world > 1) ----------------------------
+// RCCL is resolved at run time from the library torch loaded (one RCCL per process); the
+// communicator is this engine's own (unique id broadcast by the caller over torch.distributed).
+namespace {
+struct RcclApi {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+RcclApi g_rccl;
+}  // namespace
+
+extern "C" int prl_dp_rccl_open(const char* lib_path) {
+  PRL_REQUIRE(lib_path, "prl_dp_rccl_open: null path");
+  void* h = dlopen(lib_path, RTLD_NOW | RTLD_LOCAL);
+  PRL_REQUIRE(h, "prl_dp_rccl_open: dlopen(%s) failed: %s", lib_path, dlerror());
+  RcclApi api;
+  api.get_unique_id = reinterpret_cast<decltype(api.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+  api.comm_init_rank = reinterpret_cast<decltype(api.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+  api.all_reduce = reinterpret_cast<decltype(api.all_reduce)>(dlsym(h, "ncclAllReduce"));
+  api.comm_destroy = reinterpret_cast<decltype(api.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+  api.error_string = reinterpret_cast<decltype(api.error_string)>(dlsym(h, "ncclGetErrorString"));
+  PRL_REQUIRE(api.get_unique_id && api.comm_init_rank && api.all_reduce && api.comm_destroy,
+              "prl_dp_rccl_open: %s lacks the RCCL entry points", lib_path);
+  g_rccl = api;
+  return PRL_OK;
+}
+
+#define PRL_RCCL_TRY(call, what)                                                            \
+  do {                                                                                      \
+    const ncclResult_t r_ = (call);                                                         \
+    PRL_REQUIRE(r_ == ncclSuccess, "%s: RCCL error %d (%s)", what, (int)r_,                 \
+                g_rccl.error_string ? g_rccl.error_string(r_) : "?");                       \
+  } while (0)
+
+extern "C" int prl_dp_unique_id(uint8_t* id_out, int64_t id_bytes) {
+  PRL_REQUIRE(g_rccl.get_unique_id, "prl_dp_unique_id: RCCL not opened (prl_dp_rccl_open)");
+  PRL_REQUIRE(id_out && id_bytes == (int64_t)sizeof(ncclUniqueId), "prl_dp_unique_id: need %zu bytes",
+              sizeof(ncclUniqueId));
+  ncclUniqueId id;
+  PRL_RCCL_TRY(g_rccl.get_unique_id(&id), "ncclGetUniqueId");
+  memcpy(id_out, &id, sizeof(id));
+  return PRL_OK;
+}
+
+extern "C" int prl_dp_comm_init(const uint8_t* id, int64_t id_bytes, int32_t nranks, int32_t rank,
+                                void** comm) {
+  PRL_REQUIRE(g_rccl.comm_init_rank, "prl_dp_comm_init: RCCL not opened (prl_dp_rccl_open)");
+  PRL_REQUIRE(id && comm && id_bytes == (int64_t)sizeof(ncclUniqueId) && nranks >= 1 && rank >= 0 &&
+                  rank < nranks, "prl_dp_comm_init: bad arguments");
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  ncclComm_t c = nullptr;
+  PRL_RCCL_TRY(g_rccl.comm_init_rank(&c, nranks, uid, rank), "ncclCommInitRank");
+  *comm = c;
+  return PRL_OK;
+}
+
+extern "C" int prl_dp_comm_destroy(void* comm) {
+  if (comm && g_rccl.comm_destroy) g_rccl.comm_destroy(reinterpret_cast<ncclComm_t>(comm));
+  return PRL_OK;
+}
+
+// The whole k_epochs x nb loop of the stepped engine enqueued from C: per optimizer step the
+// gradient kernel (this rank's slice of union minibatch j, scaled 1 / counts[j]), ncclAllReduce
+// of the flat gradient image on `stream`, the AdamW kernel; asynchronous, no host sync.  The
+// gradient kernel's hand-off counter is zeroed once and its target advances per launch (no
+// memset node per step).  Semantics = FusedUpdate.run_stepped's Python loop, bit for bit.
+extern "C" int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, int32_t D, int32_t A,
+                                 int32_t discrete, const float* S, const float* actions,
+                                 const float* old_logp, const float* adv, const float* ret, int64_t N,
+                                 int32_t mini_batch, int32_t k_epochs, int64_t nb,
+                                 const int64_t* counts, int64_t step0, float clip, float vf_coef,
+                                 float ent_coef, float lr, float beta1, float beta2, float eps,
+                                 float weight_decay, float max_norm, float* grad, float* loss_out,
+                                 void* workspace, int64_t workspace_bytes, void* comm, void* stream) {
+  UpdArgs args{};
+  PRL_REQUIRE(upd_layout(D, A, discrete, args.net), "prl_ppo_update_dp: D=%d A=%d not supported", D, A);
+  PRL_REQUIRE(N >= 0 && mini_batch > 0 && k_epochs >= 0 && nb >= 0 && counts, "prl_ppo_update_dp: bad sizes");
+  PRL_REQUIRE(img_params && img_m && img_v && grad && workspace && comm, "prl_ppo_update_dp: null pointer");
+  PRL_REQUIRE(g_rccl.all_reduce, "prl_ppo_update_dp: RCCL not opened (prl_dp_rccl_open)");
+  PRL_REQUIRE(N == 0 || (S && actions && old_logp && adv && ret), "prl_ppo_update_dp: null input");
+  const int G = upd_grid(mini_batch);
+  UpdWs ws;
+  const size_t need = upd_ws_carve(args.net, G, reinterpret_cast<char*>(workspace), &ws);
+  PRL_REQUIRE((size_t)workspace_bytes >= need, "prl_ppo_update_dp: workspace too small");
+  PRL_REQUIRE((int64_t)k_epochs * nb < (int64_t)(1u << 31) / 256, "prl_ppo_update_dp: too many steps");
+  for (int64_t j = 0; j < nb; ++j) PRL_REQUIRE(counts[j] > 0, "prl_ppo_update_dp: empty union minibatch %lld", (long long)j);
+  args.S = S;
+  args.act = actions;
+  args.old_logp = old_logp;
+  args.adv = adv;
+  args.ret = ret;
+  args.N = N;
+  args.mb = mini_batch;
+  args.G = G;
+  args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RT) * UPD_RT;
+  args.clip = clip;
+  args.vf_coef = vf_coef;
+  args.part = ws.part;
+  args.ctr = ws.ctr;
+  const size_t lds = upd_lds_bytes(args.net);
+  hipStream_t st = as_stream(stream);
+  const void* kern = upd_grad_kernel_for(args.net);
+  PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
+  const int nt = upd_nt(args.net);
+  const unsigned adam_grid = (unsigned)cdiv(args.net.Lp / 4, UPD_THREADS);
+  const size_t count = (size_t)args.net.Lp + 4;   // the image + its loss quad
+  const ncclComm_t c = reinterpret_cast<ncclComm_t>(comm);
+  int64_t step = step0;
+  unsigned launches = 0;
+  for (int e = 0; e < k_epochs; ++e) {
+    for (int64_t j = 0; j < nb; ++j) {
+      const int64_t row0 = j * (int64_t)mini_batch;
+      int B_local = (int)std::max<int64_t>(0, std::min<int64_t>(mini_batch, N - row0));
+      float inv = 1.0f / (float)counts[j];
+      int64_t r0 = row0;
+      const float* img = img_params;
+      args.grad_target = (unsigned)G * (++launches);
+      void* kargs[] = {&args, &img, &grad, &r0, &B_local, &inv};
+      PRL_HIP_TRY(hipLaunchKernel(kern, dim3(G), dim3(nt), kargs, lds, st));
+      PRL_RCCL_TRY(g_rccl.all_reduce(grad, grad, count, ncclFloat32, ncclSum, c, st), "ncclAllReduce");
+      ++step;
+      hipLaunchKernelGGL(ppo_adam_kernel, dim3(adam_grid), dim3(UPD_THREADS), 0, st, args.net.Lp,
+                         img_params, img_m, img_v, grad, (double)step, lr, beta1, beta2, eps,
+                         weight_decay, max_norm, inv, vf_coef, ent_coef, loss_out);
+      PRL_LAUNCH_CHECK("ppo_adam_step");
+    }
+  }
   return PRL_OK;
 }

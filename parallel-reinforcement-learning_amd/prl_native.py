@@ -55,6 +55,12 @@ SIGNATURES = {
                       + [_F32] * 9 + [_P, _P, _I64, _P],
     "prl_ppo_update_status_ptr": [_P, _P],
     "prl_ppo_update_profile_ptr": [_P, _P],
+    "prl_dp_rccl_open": [ctypes.c_char_p],
+    "prl_dp_unique_id": [_P, _I64],
+    "prl_dp_comm_init": [_P, _I64, _I32, _I32, _P],
+    "prl_dp_comm_destroy": [_P],
+    "prl_ppo_update_dp": [_P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I32,
+                          _I64, _P, _I64] + [_F32] * 9 + [_P, _P, _P, _I64, _P, _P],
     "prl_ppo_evaluate": [_P, _I32, _I32, _I32, _P, _P, _I64, _P, _P, _P, _P],
     "prl_ppo_image_floats": [_I32, _I32, _I32],
     "prl_ppo_image": [_I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32, _P],
@@ -421,6 +427,57 @@ def ppo_update_profile(workspace) -> torch.Tensor:
                                             ctypes.byref(ptr)), "prl_ppo_update_profile_ptr")
     off = int(ptr.value) - workspace.data_ptr()
     return workspace[off:off + 256].view(torch.int64)
+
+
+# ------------------------------------------------------------- data-parallel step loop (RCCL)
+RCCL_UNIQUE_ID_BYTES = 128
+
+
+def dp_rccl_open(path: str | None = None):
+    """Resolve RCCL's entry points from the library torch loaded (one RCCL per process)."""
+    if path is None:
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    _check(lib().prl_dp_rccl_open(path.encode()), "prl_dp_rccl_open")
+
+
+def dp_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(RCCL_UNIQUE_ID_BYTES)
+    _check(lib().prl_dp_unique_id(ctypes.cast(buf, ctypes.c_void_p), RCCL_UNIQUE_ID_BYTES),
+           "prl_dp_unique_id")
+    return buf.raw
+
+
+def dp_comm_init(uid: bytes, nranks: int, rank: int) -> ctypes.c_void_p:
+    buf = ctypes.create_string_buffer(bytes(uid), RCCL_UNIQUE_ID_BYTES)
+    comm = ctypes.c_void_p()
+    _check(lib().prl_dp_comm_init(ctypes.cast(buf, ctypes.c_void_p), RCCL_UNIQUE_ID_BYTES,
+                                  int(nranks), int(rank), ctypes.byref(comm)), "prl_dp_comm_init")
+    return comm
+
+
+def dp_comm_destroy(comm):
+    if comm:
+        lib().prl_dp_comm_destroy(comm)
+
+
+def ppo_update_dp(img_p, img_m, img_v, D, A, discrete, S, A_, old_logp, adv, ret, mini_batch,
+                  k_epochs, counts, step0, clip, vf_coef, ent_coef, lr, beta1, beta2, eps, wd,
+                  max_norm, grad, loss_out, workspace, comm):
+    """The stepped engine's whole loop enqueued natively (prl_ppo_update_dp): per optimizer step
+    gradient kernel -> ncclAllReduce(grad) -> AdamW kernel on torch's current stream."""
+    import numpy as np
+    cnt = np.ascontiguousarray(np.asarray(counts, dtype=np.int64))
+    N = int(S.shape[0])
+    _check(lib().prl_ppo_update_dp(
+        _dev(img_p, torch.float32, "img_p"), _dev(img_m, torch.float32, "img_m"),
+        _dev(img_v, torch.float32, "img_v"), int(D), int(A), int(bool(discrete)),
+        _dev(S, torch.float32, "S"), _dev(A_, torch.float32, "actions"),
+        _dev(old_logp, torch.float32, "old_logp"), _dev(adv, torch.float32, "adv"),
+        _dev(ret, torch.float32, "ret"), N, int(mini_batch), int(k_epochs), int(cnt.size),
+        cnt.ctypes.data_as(ctypes.c_void_p), int(step0), clip, vf_coef, ent_coef, lr, beta1,
+        beta2, eps, wd, max_norm, _dev(grad, torch.float32, "grad"),
+        _dev(loss_out, torch.float32, "loss"), _dev(workspace, torch.uint8, "workspace"),
+        workspace.numel(), comm, _stream()), "prl_ppo_update_dp")
 
 
 def ppo_image_floats(D, A, discrete) -> int:

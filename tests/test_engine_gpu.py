@@ -342,3 +342,42 @@ def test_stepped_engine_matches_persistent(cont):
     assert float(ps.optimizer.state[next(ps.policy.parameters())]["step"]) == 2 * 8
     if not cont:
         _compare(pf, ps)
+
+
+@pytest.mark.parametrize("cont", [False, True])
+def test_native_dp_loop_equals_python_loop(cont):
+    """prl_ppo_update_dp (the stepped loop enqueued from C with ncclAllReduce, here on a one-rank
+    RCCL communicator: the all-reduce is an identity) gives the same bits as the Python loop
+    with an identity all-reduce: parameters, both moments, step count and loss."""
+    import prl_native
+    from PPO import PPO
+    N = 3000 + 7
+    data = _data(N, 3 if cont else 4, cont, seed=29)
+    D, A = (3, 1) if cont else (4, 2)
+    prl_native.dp_rccl_open()
+    comm = prl_native.dp_comm_init(prl_native.dp_unique_id(), 1, 0)
+    outs = []
+    try:
+        for native in (False, True):
+            torch.manual_seed(0)
+            p = PPO(cont, D, A, action_scaling=2.0 if cont else None, k_epochs=3, batch_size=64,
+                    mini_batch_size=512)
+            p.show_progress = False
+            p.memory.push_device(*data)
+            p._world = staticmethod(lambda: 1)
+
+            def stepped_update(S, A_, old, adv, ret, n_ranks, p=p, native=native):
+                eng = p._fused_engine()
+                p.last_loss = eng.run_stepped(S, A_, old, adv, ret, p.k_epochs, n_ranks,
+                                              lambda t: t, comm=comm if native else None)
+            p._update = stepped_update
+            p.learn()
+            torch.cuda.synchronize()
+            eng = p._engine
+            outs.append((eng.flat.cpu(), eng.m.cpu(), eng.v.cpu(), float(eng.step.item()),
+                         float(p.last_loss)))
+    finally:
+        prl_native.dp_comm_destroy(comm)
+    (f0, m0, v0, s0, l0), (f1, m1, v1, s1, l1) = outs
+    assert torch.equal(f0, f1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+    assert s0 == s1 == 3 * 6 and l0 == l1

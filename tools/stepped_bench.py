@@ -1,7 +1,9 @@
 """Per-step cost of the data-parallel (stepped) engine on one GPU: grad kernel -> all-reduce ->
 AdamW kernel per optimizer step on the C2 learn workload (2^20 synthetic CartPole transitions),
 with (a) no collective, (b) a one-rank RCCL all_reduce through torch.distributed — the host
-and launch overhead the N > 1 runs pay on top of the collective's own latency."""
+and launch overhead the N > 1 runs pay on top of the collective's own latency — and (c) the
+native loop (prl_ppo_update_dp: the steps enqueued from C, ncclAllReduce on a one-rank
+communicator of the engine's own)."""
 import json
 import os
 import sys
@@ -21,7 +23,11 @@ torch.cuda.set_device(0)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
 N, mb, k = 1 << 20, 512, 11
 batch = synthetic_batch(N)
-for label, ar in (("identity", lambda t: t), ("rccl-1rank", dist.all_reduce)):
+import prl_native  # noqa: E402
+prl_native.dp_rccl_open()
+comm = prl_native.dp_comm_init(prl_native.dp_unique_id(), 1, 0)
+for label, ar, cm in (("identity", lambda t: t, None), ("rccl-1rank", dist.all_reduce, None),
+                      ("native-rccl-1rank", None, comm)):
     torch.manual_seed(0)
     p = PPO(False, 4, 2, lr=1e-3, k_epochs=k, batch_size=1, mini_batch_size=mb)
     p.show_progress = False
@@ -31,13 +37,15 @@ for label, ar in (("identity", lambda t: t), ("rccl-1rank", dist.all_reduce)):
     adv = torch.randn_like(V)
     ret = torch.randn_like(V)
     eng = p._fused_engine()
-    eng.run_stepped(S[:8192], A[:8192], old[:8192], adv[:8192], ret[:8192], 1, [8192], ar)  # warm
+    eng.run_stepped(S[:8192], A[:8192], old[:8192], adv[:8192], ret[:8192], 1, [8192], ar,
+                    comm=cm)  # warm
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    eng.run_stepped(S, A, old, adv, ret, k, [N], ar)
+    eng.run_stepped(S, A, old, adv, ret, k, [N], ar, comm=cm)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     steps = k * -(-N // mb)
     print(json.dumps({"all_reduce": label, "learn_update_ms_per_1M": round(dt * 1e3, 1),
                       "us_per_step": round(dt / steps * 1e6, 2)}), flush=True)
+prl_native.dp_comm_destroy(comm)
 dist.destroy_process_group()
