@@ -46,6 +46,7 @@
 namespace prl {
 
 constexpr int UPD_THREADS = 256;
+constexpr int UPD_HDR = 128;      // LDS header floats: broadcast words, timers (u64 at +16 / +64)
 constexpr int UPD_H = 64;         // hidden width
 constexpr int UPD_HS = 68;        // LDS row stride of [*][64] arrays
 constexpr int UPD_MAXH = 3;       // heads
@@ -1011,37 +1012,27 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
   const int Qp = Lp / 4;            // parameter quads
   const int Qtot = Qp + 1;          // + one quad of loss partials
   float* hdr = upd_lds;             // [64] broadcast words + chunk stage timers
-  float* W = upd_lds + 64;          // [Lp]
-  float* Ga = W + Lp;               // [Lp + 4]
-  float* scratch = Ga + Lp + 4;     // tile activations / reduction scratch
+  // LDS: header | tile scratch | parameter image W | gradient image Ga.  The scratch sits below
+  // 64 KB so every scratch address folds into the ds instructions' 16-bit offset field (no base
+  // registers kept live across the step loop)
+  float* scratch = upd_lds + UPD_HDR;                                   // tile activations
+  float* W = scratch + ((upd_scratch_floats(n.D, NW) + 3) & ~3);         // [Lp]
+  float* Ga = W + Lp;                                                    // [Lp + 4]
   const UpdScr sc = upd_scr(scratch, n.D, NW);
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
   float* s_adam = hdr + 10;         // [2] this step's AdamW step size, 1 / sqrt(bc2)
 
-  // ---- load parameters (LDS image) and this thread's moments (quad q = t + 256 i, registers);
-  //      the moments are scattered into the LDS image layout through Ga (free until phase A) ---
+  // ---- load the parameter image into LDS and this thread's moment quads (q = t + NT i) into
+  //      registers: args.params / exp_avg / exp_avg_sq are IMAGES here (prl_ppo_update converts
+  //      the flat torch vectors around the launch), so no layout arithmetic stays live in SGPRs
   float4 mreg[NQ], vreg[NQ];
-  for (int k = t; k < Lp; k += NT) {
-    const int f = upd_flat_of(n, k);
-    W[k] = f >= 0 ? args.params[f] : 0.0f;
-    Ga[k] = f >= 0 ? args.exp_avg[f] : 0.0f;
-  }
-  __syncthreads();
+  for (int q = t; q < Qp; q += NT)
+    *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(args.params + 4 * q);
 #pragma unroll
   for (int i = 0; i < NQ; ++i) {
     const int q = t + i * NT;
-    mreg[i] = q < Qp ? *reinterpret_cast<const float4*>(Ga + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
-  }
-  __syncthreads();
-  for (int k = t; k < Lp; k += NT) {
-    const int f = upd_flat_of(n, k);
-    Ga[k] = f >= 0 ? args.exp_avg_sq[f] : 0.0f;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < NQ; ++i) {
-    const int q = t + i * NT;
-    vreg[i] = q < Qp ? *reinterpret_cast<const float4*>(Ga + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+    mreg[i] = q < Qp ? *reinterpret_cast<const float4*>(args.exp_avg + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+    vreg[i] = q < Qp ? *reinterpret_cast<const float4*>(args.exp_avg_sq + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
   }
   const float step0 = args.adam_step[0];
   if (t < 24) reinterpret_cast<unsigned long long*>(hdr + 16)[t] = 0ull;
@@ -1051,14 +1042,20 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
 
   const int R = args.R;
   float loss_last = 0.f;
-  unsigned long long pt[7] = {0, 0, 0, 0, 0, 0, 0};
-  unsigned long long tp = __builtin_amdgcn_s_memrealtime();
-  const unsigned long long rt0 = tp, ck0 = __builtin_amdgcn_s_memtime();
+  // phase timers of workgroup 0 live in LDS (hdr + 64: pt[7], tp, rt0, ck0), not in SGPRs:
+  // the step loop is short of scalar registers
+  unsigned long long* const pts = reinterpret_cast<unsigned long long*>(hdr + 64);
+  if (g == 0 && t == 0) {
+    for (int i = 0; i < 7; ++i) pts[i] = 0ull;
+    pts[7] = __builtin_amdgcn_s_memrealtime();
+    pts[8] = pts[7];
+    pts[9] = __builtin_amdgcn_s_memtime();
+  }
   auto mark = [&](int i) {
     if (g == 0 && t == 0) {
       const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-      pt[i] += now - tp;
-      tp = now;
+      pts[i] += now - pts[7];
+      pts[7] = now;
     }
   };
   UpdIn<upd_ksm<KA>()> nin;   // inputs of the next tile to run (prefetched)
@@ -1203,37 +1200,23 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     __syncthreads();
     mark(6);   // AdamW
   }
-  // ---- write back (workgroup 0): parameters, moments, step count, last loss -------------------
+  // ---- write back (workgroup 0): parameter / moment images, step count, last loss -----------
   if (g == 0) {
+    for (int q = t; q < Qp; q += NT)
+      *reinterpret_cast<float4*>(args.params + 4 * q) = *reinterpret_cast<const float4*>(W + 4 * q);
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
       const int q = t + i * NT;
-      if (q < Qp) *reinterpret_cast<float4*>(Ga + 4 * q) = mreg[i];
-    }
-    __syncthreads();
-    for (int k = t; k < Lp; k += NT) {
-      const int f = upd_flat_of(n, k);
-      if (f >= 0) {
-        args.params[f] = W[k];
-        args.exp_avg[f] = Ga[k];
+      if (q < Qp) {
+        *reinterpret_cast<float4*>(args.exp_avg + 4 * q) = mreg[i];
+        *reinterpret_cast<float4*>(args.exp_avg_sq + 4 * q) = vreg[i];
       }
     }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      const int q = t + i * NT;
-      if (q < Qp) *reinterpret_cast<float4*>(Ga + 4 * q) = vreg[i];
-    }
-    __syncthreads();
-    for (int k = t; k < Lp; k += NT) {
-      const int f = upd_flat_of(n, k);
-      if (f >= 0) args.exp_avg_sq[f] = Ga[k];
-    }
     if (t == 0) {
-      for (int i = 0; i < 7; ++i) args.prof[i] = pt[i];
+      for (int i = 0; i < 7; ++i) args.prof[i] = pts[i];
       args.prof[7] = (unsigned long long)args.total_steps;
-      args.prof[30] = __builtin_amdgcn_s_memrealtime() - rt0;
-      args.prof[31] = __builtin_amdgcn_s_memtime() - ck0;
+      args.prof[30] = __builtin_amdgcn_s_memrealtime() - pts[8];
+      args.prof[31] = __builtin_amdgcn_s_memtime() - pts[9];
       for (int i = 0; i < 22; ++i) args.prof[8 + i] = reinterpret_cast<unsigned long long*>(hdr + 16)[i];
       args.adam_step[0] = step0 + (float)args.total_steps;
       if (args.loss_out) args.loss_out[0] = loss_last;
@@ -1263,8 +1246,9 @@ __device__ __forceinline__ void ppo_evaluate_body(const UpdNet& n, const UpdArgs
   constexpr int NW = upd_nw<KD, KA>(), NT = 64 * NW;
   extern __shared__ __align__(16) float upd_lds[];
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
-  float* W = upd_lds + 64;
-  const UpdScr sc = upd_scr(W + n.Lp, n.D, NW);
+  float* scratch = upd_lds + UPD_HDR;
+  float* W = scratch + ((upd_scratch_floats(n.D, NW) + 3) & ~3);
+  const UpdScr sc = upd_scr(scratch, n.D, NW);
   for (int k = t; k < n.Lp; k += NT) {
     const int f = upd_flat_of(n, k);
     W[k] = f >= 0 ? args.params[f] : 0.0f;
@@ -1321,9 +1305,9 @@ __device__ __forceinline__ void ppo_grad_body(const UpdNet& n, const UpdArgs& ar
   const int t = threadIdx.x, g = blockIdx.x, G = args.G;
   const int Lp = n.Lp, Qp = Lp / 4, Qtot = Qp + 1;
   float* hdr = upd_lds;
-  float* W = upd_lds + 64;
+  float* scratch = upd_lds + UPD_HDR;
+  float* W = scratch + ((upd_scratch_floats(n.D, NW) + 3) & ~3);
   float* Ga = W + Lp;
-  float* scratch = Ga + Lp + 4;
   const UpdScr sc = upd_scr(scratch, n.D, NW);
   float* s_ssq = hdr + 4;
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
@@ -1482,7 +1466,7 @@ const void* upd_eval_kernel_for(const UpdNet& n) {
 int upd_grid(int64_t mb) { return (int)std::min<int64_t>(256, cdiv(mb, UPD_RT)); }
 
 size_t upd_lds_bytes(const UpdNet& n) {
-  return sizeof(float) * (size_t)(64 + 2 * n.Lp + 4 + upd_scratch_floats(n.D, upd_nw_host(n)));
+  return sizeof(float) * (size_t)(UPD_HDR + 2 * n.Lp + 4 + ((upd_scratch_floats(n.D, upd_nw_host(n)) + 3) & ~3));
 }
 
 struct UpdWs {
@@ -1491,6 +1475,7 @@ struct UpdWs {
   float* sq;
   float* red;
   float* part;
+  float* img;   // [3][Lp + 4]: parameter, exp_avg, exp_avg_sq images of the persistent launch
 };
 
 // workspace: ctr[UPD_CTR_WORDS] (words 0-3 and the shards zeroed per launch, word 4 sticky) | prof[32] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4]
@@ -1499,13 +1484,14 @@ size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
   const size_t o_ctr = take(4 * UPD_CTR_WORDS), o_prof = take(256), o_sq = take(2048 * 4), o_red = take(Qtot * 16),
-               o_part = take((size_t)G * Qtot * 16);
+               o_part = take((size_t)G * Qtot * 16), o_img = take((size_t)3 * Qtot * 16);
   if (ws) {
     ws->ctr = reinterpret_cast<unsigned*>(base + o_ctr);
     ws->prof = reinterpret_cast<unsigned long long*>(base + o_prof);
     ws->sq = reinterpret_cast<float*>(base + o_sq);
     ws->red = reinterpret_cast<float*>(base + o_red);
     ws->part = reinterpret_cast<float*>(base + o_part);
+    ws->img = reinterpret_cast<float*>(base + o_img);
   }
   return off;
 }
@@ -1570,9 +1556,13 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
   args.eps = eps;
   args.wd = weight_decay;
   args.max_norm = max_norm;
-  args.params = params;
-  args.exp_avg = exp_avg;
-  args.exp_avg_sq = exp_avg_sq;
+  const size_t L4 = (size_t)args.net.Lp + 4;
+  float* img_p = ws.img;
+  float* img_m = ws.img + L4;
+  float* img_v = ws.img + 2 * L4;
+  args.params = img_p;
+  args.exp_avg = img_m;
+  args.exp_avg_sq = img_v;
   args.adam_step = adam_step;
   args.loss_out = loss_out;
   args.part = ws.part;
@@ -1589,7 +1579,14 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr + UPD_CTR_A, 0, 4 * (UPD_CTR_WORDS - UPD_CTR_A), st));
   void* kargs[] = {&args};
+  const unsigned img_grid = (unsigned)cdiv(args.net.Lp, UPD_THREADS);
+  hipLaunchKernelGGL(ppo_image_kernel, dim3(img_grid), dim3(UPD_THREADS), 0, st, args.net, params,
+                     exp_avg, exp_avg_sq, img_p, img_m, img_v, 1);
+  PRL_LAUNCH_CHECK("ppo_image");
   PRL_HIP_TRY(hipLaunchCooperativeKernel(kern, dim3(G), dim3(upd_nt(args.net)), kargs, (unsigned)lds, st));
+  hipLaunchKernelGGL(ppo_image_kernel, dim3(img_grid), dim3(UPD_THREADS), 0, st, args.net, params,
+                     exp_avg, exp_avg_sq, img_p, img_m, img_v, 0);
+  PRL_LAUNCH_CHECK("ppo_image");
   return PRL_OK;
 }
 
@@ -1605,7 +1602,7 @@ extern "C" int prl_ppo_evaluate(const float* params, int32_t D, int32_t A, int32
   args.S = S;
   args.act = actions;
   args.N = N;
-  const size_t lds = sizeof(float) * (size_t)(64 + args.net.Lp + upd_scratch_floats(D, upd_nw_host(args.net)));
+  const size_t lds = sizeof(float) * (size_t)(UPD_HDR + args.net.Lp + ((upd_scratch_floats(D, upd_nw_host(args.net)) + 3) & ~3));
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_evaluate: %zu B of LDS needed", lds);
   const unsigned grid = (unsigned)std::min<int64_t>(cdiv(N, UPD_RT), 2 * 256);
   const void* kern = upd_eval_kernel_for(args.net);
