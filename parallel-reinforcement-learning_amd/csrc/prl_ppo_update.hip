@@ -41,6 +41,7 @@
 
 #include <dlfcn.h>
 #include <string.h>
+#include <stdlib.h>
 #include <rccl/rccl.h>
 
 namespace prl {
@@ -1445,19 +1446,27 @@ int upd_nt(const UpdNet& n) { return 64 * upd_nw_host(n); }
 int upd_nq(const UpdNet& n) { return (int)cdiv(n.Lp / 4, upd_nt(n)); }
 // Specialisations for the configs' shapes (CartPole: discrete, A = 2; Pendulum: continuous,
 // A = 1); every other shape runs the generic (runtime head configuration) kernel.
+// PRL_UPD_GENERIC=1 routes every shape through the runtime-layout kernels (testing)
+bool upd_force_generic() {
+  const char* e = getenv("PRL_UPD_GENERIC");
+  return e && e[0] == '1';
+}
 const void* upd_kernel_for(const UpdNet& n) {
   const int nq = upd_nq(n);
+  if (upd_force_generic()) return nq <= 20 ? reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0>) : nullptr;
   if (n.discrete && n.A == 2 && n.D == 4 && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4>);
   if (!n.discrete && n.A == 1 && n.D == 3 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3>);
   if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0>);
   return nullptr;
 }
 const void* upd_grad_kernel_for(const UpdNet& n) {
+  if (upd_force_generic()) return reinterpret_cast<const void*>(ppo_grad_kernel<-1, 0, 0>);
   if (n.discrete && n.A == 2 && n.D == 4) return reinterpret_cast<const void*>(ppo_grad_kernel<1, 2, 4>);
   if (!n.discrete && n.A == 1 && n.D == 3) return reinterpret_cast<const void*>(ppo_grad_kernel<0, 1, 3>);
   return reinterpret_cast<const void*>(ppo_grad_kernel<-1, 0, 0>);
 }
 const void* upd_eval_kernel_for(const UpdNet& n) {
+  if (upd_force_generic()) return reinterpret_cast<const void*>(ppo_evaluate_kernel<-1, 0, 0>);
   if (n.discrete && n.A == 2 && n.D == 4) return reinterpret_cast<const void*>(ppo_evaluate_kernel<1, 2, 4>);
   if (!n.discrete && n.A == 1 && n.D == 3) return reinterpret_cast<const void*>(ppo_evaluate_kernel<0, 1, 3>);
   return reinterpret_cast<const void*>(ppo_evaluate_kernel<-1, 0, 0>);

@@ -381,3 +381,40 @@ def test_native_dp_loop_equals_python_loop(cont):
     (f0, m0, v0, s0, l0), (f1, m1, v1, s1, l1) = outs
     assert torch.equal(f0, f1) and torch.equal(m0, m1) and torch.equal(v0, v1)
     assert s0 == s1 == 3 * 6 and l0 == l1
+
+
+@pytest.mark.parametrize("cont,D,A", [(False, 6, 3), (True, 5, 2)])
+def test_generic_shape_engine_gradient(cont, D, A):
+    """Shapes outside the specialised kernels run the runtime-layout engine (KD = -1): one step at
+    lr = 0, its forward against float64 and its gradient against float64 autograd of the
+    reference loss at the engine's own log-prob values (as test_fused_gradient_off_policy)."""
+    import copy
+    rng = np.random.default_rng(41)
+    N = 512 - 37        # one ragged minibatch: the float64 reference is one step over all rows
+    S = torch.from_numpy((rng.normal(size=(N, D)) * 0.5).astype(np.float32)).cuda()
+    Aa = (torch.from_numpy((np.tanh(rng.normal(size=(N, A))) * 2).astype(np.float32)).cuda() if cont
+          else torch.from_numpy(rng.integers(0, A, N).astype(np.float32)).cuda())
+    R = torch.from_numpy(rng.normal(1, 0.5, N).astype(np.float32)).cuda()
+    Dn = torch.from_numpy((rng.random(N) < 0.05).astype(np.float32)).cuda()
+    Dn[-1] = 1
+    p = _run(True, cont, (S, Aa, R, Dn), 512, 1, D=D, A=A, lr=0.0)
+    S_, A_, old, adv, ret = p._last_update_inputs
+    eng = p._engine
+    logp_eng, _ = eng.evaluate(p.policy, S_, A_)
+    with torch.no_grad():
+        l64, _, _ = copy.deepcopy(p.policy).cpu().double().get_evaluate(S_.cpu().double(),
+                                                                          A_.cpu().double())
+    fwd = float((logp_eng.cpu().double() - l64).abs().max()) / (1.0 + float(l64.abs().max()))
+    assert fwd <= 2e-6, fwd
+    g = torch.Generator(device="cuda").manual_seed(5)
+    old2 = _away_from_kinks(p, S_, A_, old + 0.5 * torch.randn(old.shape, device="cuda", generator=g))
+    eng.m.zero_()
+    eng.v.zero_()
+    eng.step.zero_()
+    eng.run(S_, A_, old2, adv, ret, 1)
+    g64 = _grad_f64(p, (S_, A_, old2, adv, ret), logp_val=logp_eng)
+    per = {}
+    for (name, prm), gr in zip(p.policy.named_parameters(), g64):
+        m = p.optimizer.state[prm]["exp_avg"].double().cpu() / 0.1
+        per[name] = float((m - gr).abs().max()) / (float(gr.abs().max()) + 1e-30)
+    assert max(per.values()) <= 1e-4, per
