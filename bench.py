@@ -75,6 +75,8 @@ def time_kernel(launch, reps=10, cold=True, prep=None):
     clean (a write-based flush leaves them full of dirty lines whose write-back would then
     compete with the timed kernel)."""
     flush = torch.ones(128 << 20, dtype=torch.float32, device="cuda") if cold else None
+    if prep is not None:
+        prep()
     launch()
     ms = []
     for _ in range(reps):
@@ -90,6 +92,46 @@ def time_kernel(launch, reps=10, cold=True, prep=None):
         e.synchronize()
         ms.append(s.elapsed_time(e))
     return float(np.median(ms)), float(np.min(ms))
+
+
+def env_at_scale(env_name, spec, scaling, bpe, E=1 << 22):
+    """The rollout step kernel on E = 2^22 envs (one vector step from a fresh reset, every env
+    active; trajectory buffers of that one step only): at the bench's E = 65,536 the launch is
+    latency-bound, this is the kernel's streaming rate."""
+    import types
+
+    import prl_native
+    from AsyncTools.AsyncPPO import EnvVectorizer
+    vec = EnvVectorizer(env_name, E, seed=7)
+    D, adim = spec.obs_dim, (1 if spec.discrete else spec.act_dim)
+    dev = vec.device
+    # every launch follows a reset (time_kernel's prep), so it writes time rows 0 / 1 only;
+    # 4 rows of margin all the same
+    R = 4
+    tr = types.SimpleNamespace(
+        obs=torch.empty(R + 1, E, D, device=dev), act=torch.empty(R, E, adim, device=dev),
+        rew=torch.empty(R, E, device=dev), done=torch.empty(R, E, dtype=torch.uint8, device=dev),
+        ep_len=torch.zeros(E, dtype=torch.int32, device=dev),
+        active_after=torch.zeros(1, dtype=torch.int32, device=dev),
+        reward_sum=torch.zeros(1, dtype=torch.float64, device=dev))
+    if spec.discrete:
+        dist = torch.full((E, spec.act_dim), 1.0 / spec.act_dim, device=dev)
+    else:
+        dist = torch.cat([torch.zeros(E, spec.act_dim, device=dev),
+                          torch.ones(E, spec.act_dim, device=dev)], 1).contiguous()
+
+    def launch():
+        prl_native.rollout_step(prl_native.ENV_KINDS[env_name], 0, vec.phys, vec.t_elapsed,
+                                vec.terminal, dist, scaling, 12345, spec.max_episode_steps,
+                                tr.obs, tr.act, tr.rew, tr.done, tr.ep_len, tr.active_after,
+                                tr.reward_sum)
+
+    cold, _ = time_kernel(launch, cold=True, prep=lambda: vec.reset_device(tr.obs[0]))
+    warm, _ = time_kernel(launch, cold=False, prep=lambda: vec.reset_device(tr.obs[0]))
+    ach = bpe * E / (cold * 1e-3) / 1e9
+    return {"envs_per_launch": E, "avg_launch_us": round(cold * 1e3, 2),
+            "warm_launch_us": round(warm * 1e3, 2), "achieved": round(ach, 1),
+            "frac": round(ach / HBM_PEAK_GBS, 4), "cache": "cold (512 MiB read-only flush)"}
 
 
 def pmc_traffic(n):
@@ -118,6 +160,8 @@ def main():
     ap.add_argument("--k-epochs", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-envs", type=int, default=8192)
+    ap.add_argument("--no-env-scale", action="store_true",
+                    help="skip the rollout-step kernel's 2^22-env re-timing (roofline_env.at_scale)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm, the measured configuration) or gloo (rehearsal of "
                          "the multi-rank path with several ranks on one GPU)")
@@ -286,6 +330,8 @@ def main():
                         "cache": "cold (512 MiB read-only flush)",
                         "warm_launch_us": round(env_warm * 1e3, 2),
                         "envs_per_launch": E, "bytes_per_env_step": bpe}
+        if not args.no_env_scale:
+            roofline_env["at_scale"] = env_at_scale(cfg["env"], spec_, scaling, bpe)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["env"] == "CartPole-v1":
