@@ -261,7 +261,13 @@ class PPO:
         if self.use_RND:
             r_int = self.rnd.compute_intrinsic_reward(S)
             R = R + r_int                                   # PPO.py:171 (float32 add)
-            self.rnd.update_pred(self.batch_packer(S, self.mini_batch_size))
+            if world > 1:   # union minibatches over the ranks, predictor gradient all-reduced
+                mb = self.mini_batch_size
+                nbr = max(-(-n // mb) for n in n_ranks)
+                counts = [sum(min(mb, max(0, n - j * mb)) for n in n_ranks) for j in range(nbr)]
+                self.rnd.update_pred(self.batch_packer(S, mb), self.all_reduce, counts)
+            else:
+                self.rnd.update_pred(self.batch_packer(S, self.mini_batch_size))
         self.memory.clear()
 
         returns = torch.empty_like(old_V)

@@ -71,15 +71,33 @@ class RND(nn.Module):
         prl_native.rnd_forward(x, tp, pp, float(self.beta), out)
         return out
 
-    def update_pred(self, values) -> None:
-        """RND.py:96-115: one MSE/AdamW pass of the predictor over the minibatches (PyTorch)."""
+    def update_pred(self, values, all_reduce=None, counts=None) -> None:
+        """RND.py:96-115: one MSE/AdamW pass of the predictor over the minibatches (PyTorch).
+
+        Data-parallel ranks (all_reduce, counts given): minibatch j is the union of the ranks'
+        j-th minibatches, counts[j] its rows.  Each rank weights its MSE by its share of the union
+        (the union's MSE is the row-weighted mean of the ranks'), the predictor's gradient is
+        all-reduced (SUM) and every rank takes the same AdamW step; len(counts) steps on every
+        rank, ranks past their last minibatch contribute zero gradients (lockstep)."""
         self.pred_net.train()
-        for i in values:
-            with torch.no_grad():
-                targets = self.target_net(i)
-            preds = self.pred_net(i)
-            loss = self.loss_fn(preds, targets)
+        values = list(values)
+        steps = len(values) if counts is None else len(counts)
+        params = list(self.pred_net.parameters())
+        for j in range(steps):
             self.optimizer.zero_grad()
-            loss.backward()
+            if j < len(values):
+                i = values[j]
+                with torch.no_grad():
+                    targets = self.target_net(i)
+                preds = self.pred_net(i)
+                loss = self.loss_fn(preds, targets)
+                if counts is not None:
+                    loss = loss * (i.shape[0] / counts[j])
+                loss.backward()
+            if all_reduce is not None:
+                for p in params:
+                    if p.grad is None:
+                        p.grad = torch.zeros_like(p)
+                    all_reduce(p.grad)
             self.optimizer.step()
         self.pred_net.eval()

@@ -101,3 +101,46 @@ def test_two_ranks_unequal_shards_stay_in_lockstep(tmp_path):
             continue
         np.testing.assert_array_equal(outs[0][key], outs[1][key])
         assert np.isfinite(outs[0][key]).all()
+
+
+def _rnd_worker(rank, world, port, mb, rows, out_dir):
+    sys.path[:0] = PATHS
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from PPO import PPO
+        from PPO.RND import RND
+        torch.manual_seed(7)                       # same initial predictor / target on every rank
+        r = RND(4, 4, device="cpu")
+        x = torch.from_numpy(np.random.default_rng(100 + rank).normal(size=(rows[rank], 4))
+                             .astype(np.float32))
+        nb = max(-(-n // mb) for n in rows)
+        counts = [sum(min(mb, max(0, n - j * mb)) for n in rows) for j in range(nb)]
+        r.update_pred(list(x.split(mb)), PPO.all_reduce, counts)
+        np.savez(os.path.join(out_dir, f"rnd{rank}.npz"),
+                 **{k: v.numpy() for k, v in r.pred_net.state_dict().items()})
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_rnd_update_pred_two_ranks_equal_one_process_on_the_union(tmp_path):
+    """RND.update_pred on data-parallel ranks (the predictor half of RND.py:96-115): gradient
+    all-reduced per step, each rank's MSE weighted by its share of the union minibatch.  Equal
+    to ONE process whose minibatch j is [rank0 slice j | rank1 slice j]; unequal row counts keep
+    the ranks in lockstep (rank 1 runs out of minibatches first)."""
+    from PPO.RND import RND
+    mb, rows = 32, (100, 70)
+    mp.spawn(_rnd_worker, args=(2, 29553, mb, rows, str(tmp_path)), nprocs=2, join=True)
+    outs = [np.load(os.path.join(tmp_path, f"rnd{r}.npz")) for r in range(2)]
+    xs = [np.random.default_rng(100 + r).normal(size=(rows[r], 4)).astype(np.float32)
+          for r in range(2)]
+    nb = max(-(-n // mb) for n in rows)
+    union = [torch.from_numpy(np.concatenate([x[j * mb:(j + 1) * mb] for x in xs]))
+             for j in range(nb)]
+    torch.manual_seed(7)
+    r = RND(4, 4, device="cpu")
+    r.update_pred(union)
+    ref = r.pred_net.state_dict()
+    for key in ref:
+        np.testing.assert_array_equal(outs[0][key], outs[1][key])
+        np.testing.assert_allclose(outs[0][key], ref[key].numpy(), rtol=0, atol=2e-6, err_msg=key)
