@@ -114,7 +114,8 @@ class FusedUpdate:
                     "dF + trunk bwd", "dW0 + biases")
 
     def profile(self):
-        """Workgroup 0's time per phase of the last launch, us per step (s_memrealtime, 100 MHz);
+        """Workgroup 0's time per phase of the last launch, us per step (s_memrealtime, 100 MHz;
+        recorded only with PRL_UPD_PROFILE=1 in the environment, zeros otherwise);
         'chunk' splits forward+backward by stage (summed over the step's 16-row tiles)."""
         p = prl_native.ppo_update_profile(self.ws).tolist()
         steps = max(p[7], 1)

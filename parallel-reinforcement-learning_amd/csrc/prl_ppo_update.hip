@@ -139,6 +139,7 @@ struct UpdArgs {
                     // [4] sticky timeout flag (never zeroed by a launch)
   unsigned long long* prof;  // [8] workgroup 0's time per phase (100 MHz ticks, summed over steps)
   unsigned grad_target;      // ppo_grad_kernel: arrivals on ctr[0] that end its hand-off
+  int profile;               // 1: workgroup 0 records its phase / tile-stage times (PRL_UPD_PROFILE)
 };
 
 // ---- sc1 (write-through / L1-bypassing) accessors -------------------------------------------
@@ -749,7 +750,9 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
   const int b = w & 3, hg = w >> 2;
   const int D = n.D, KS = (D + 3) >> 2;
   const int nh = upd_nh<KD>(n);
-  const bool timer = blockIdx.x == 0 && t == 0;
+  // the marks wait for their s_memrealtime (and the LDS queue): off unless profiling, since every
+  // hand-off waits for workgroup 0 too
+  const bool timer = args.profile && blockIdx.x == 0 && t == 0;
   unsigned long long tl = timer ? __builtin_amdgcn_s_memrealtime() : 0ull;
 #define UPD_CMARK(i)                                                   \
   if (timer) {                                                         \
@@ -1053,7 +1056,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     pts[9] = __builtin_amdgcn_s_memtime();
   }
   auto mark = [&](int i) {
-    if (g == 0 && t == 0) {
+    if (args.profile && g == 0 && t == 0) {
       const unsigned long long now = __builtin_amdgcn_s_memrealtime();
       pts[i] += now - pts[7];
       pts[7] = now;
@@ -1446,6 +1449,11 @@ int upd_nt(const UpdNet& n) { return 64 * upd_nw_host(n); }
 int upd_nq(const UpdNet& n) { return (int)cdiv(n.Lp / 4, upd_nt(n)); }
 // Specialisations for the configs' shapes (CartPole: discrete, A = 2; Pendulum: continuous,
 // A = 1); every other shape runs the generic (runtime head configuration) kernel.
+// PRL_UPD_PROFILE=1: the engine records workgroup 0's per-phase times (FusedUpdate.profile)
+bool upd_profile_enabled() {
+  const char* e = getenv("PRL_UPD_PROFILE");
+  return e && e[0] == '1';
+}
 // PRL_UPD_GENERIC=1 routes every shape through the runtime-layout kernels (testing)
 bool upd_force_generic() {
   const char* e = getenv("PRL_UPD_GENERIC");
@@ -1579,6 +1587,7 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
   args.sq = ws.sq;
   args.ctr = ws.ctr;
   args.prof = ws.prof;
+  args.profile = upd_profile_enabled();
   const size_t lds = upd_lds_bytes(args.net);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_update: %zu B of LDS needed", lds);
   hipStream_t st = as_stream(stream);
@@ -1672,6 +1681,7 @@ extern "C" int prl_ppo_grad_step(const float* img_params, int32_t D, int32_t A, 
   args.part = ws.part;
   args.ctr = ws.ctr;
   args.grad_target = (unsigned)G;
+  args.profile = upd_profile_enabled();
   const size_t lds = upd_lds_bytes(args.net);
   hipStream_t st = as_stream(stream);
   const void* kern = upd_grad_kernel_for(args.net);

@@ -7,6 +7,7 @@ import time
 
 import torch
 
+os.environ.setdefault("PRL_UPD_PROFILE", "1")   # the engine's phase marks (off by default)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "parallel-reinforcement-learning_amd"), os.path.join(ROOT, "tools")]
 from learn_bench import synthetic_batch  # noqa: E402
