@@ -251,6 +251,23 @@ int prl_ppo_adam_step(float* img_params, float* img_m, float* img_v, int32_t D, 
                       int32_t discrete, const float* grad, int64_t step, float lr, float beta1,
                       float beta2, float eps, float weight_decay, float max_norm, float inv_count,
                       float vf_coef, float ent_coef, float* loss_out, void* stream);
+/* One launch per optimizer step (what the data-parallel loops use): the PREVIOUS step's
+ * clip_grad_norm_(max_norm) + AdamW (step number step_prev, its all-reduced gradient grad_prev,
+ * state in_* -> out_*, loss_out = its loss with inv_count_prev) folded in front of this step's
+ * prl_ppo_grad_step (minibatch j from the updated parameters) -> grad_out.  Bit-identical to
+ * prl_ppo_adam_step followed by prl_ppo_grad_step.  in_* != out_* and grad_prev != grad_out (the
+ * caller double-buffers: the launch's workgroups read `in` while each writes its slice of `out`).
+ * grad_prev == NULL: no AdamW, parameters from in_p (the first step).  Replaces the per-step
+ * optimizer.step() + next forward/backward of PPO.py:247-250 / :225-245. */
+int prl_ppo_grad_fold_step(const float* in_p, const float* in_m, const float* in_v, float* out_p,
+                           float* out_m, float* out_v, const float* grad_prev, int64_t step_prev,
+                           float inv_count_prev, int32_t D, int32_t A, int32_t discrete,
+                           const float* S, const float* actions, const float* old_logp,
+                           const float* adv, const float* ret, int64_t N, int32_t mini_batch,
+                           int64_t minibatch_index, float inv_count, float clip, float vf_coef,
+                           float ent_coef, float lr, float beta1, float beta2, float eps,
+                           float weight_decay, float max_norm, float* loss_out, float* grad_out,
+                           void* workspace, int64_t workspace_bytes, void* stream);
 /* Host call: device address of the u32 status words inside an engine workspace ([0] last
  * launch, [1] sticky timeout flag). */
 int prl_ppo_update_status_ptr(void* workspace, uint32_t** status);
@@ -260,7 +277,8 @@ int prl_ppo_update_status_ptr(void* workspace, uint32_t** status);
 int prl_ppo_update_profile_ptr(void* workspace, uint64_t** prof);
 
 /* ---- data-parallel update loop (world > 1): PPO.py:216-255 per rank, one optimizer step =
- * prl_ppo_grad_step -> all-reduce of the gradient image -> prl_ppo_adam_step, enqueued from C
+ * one prl_ppo_grad_fold_step launch (previous AdamW + this gradient) -> all-reduce of the
+ * gradient image (the last step's AdamW: one prl_ppo_adam_step), enqueued from C
  * (no Python per step).  RCCL is resolved at run time from `lib_path` (the librccl torch
  * loaded); the communicator is the engine's own, built from a unique id the caller broadcasts
  * over torch.distributed.  No reference counterpart (the reference is single-process). */

@@ -188,13 +188,16 @@ class FusedUpdate:
 
     def run_stepped(self, S, A, old_logp, adv, ret, k_epochs: int, n_ranks, all_reduce,
                     comm=None):
-        """The same update loop for data-parallel ranks: per optimizer step, prl_ppo_grad_step
-        (this rank's slice of the union minibatch j, scaled by 1 / union rows) -> all_reduce of
-        the flat gradient (RCCL over xGMI on the GPU node) -> prl_ppo_adam_step.  Parameters and
-        moments stay in the engine's image layout in HBM for the whole loop.  With `comm` (an
-        RCCL communicator from dp_comm()) the loop is enqueued natively (prl_ppo_update_dp: no
-        Python per step, ncclAllReduce on torch's stream); otherwise it runs here, calling
-        `all_reduce` on the gradient image every step.  Both give the same bits."""
+        """The same update loop for data-parallel ranks.  Per optimizer step ONE launch,
+        prl_ppo_grad_fold_step: the previous step's clip_grad_norm_ + AdamW (folded in front)
+        then this rank's slice of the union minibatch j (scaled by 1 / union rows) -> its
+        gradient image; then the all_reduce of that image (RCCL over xGMI on the GPU node).  The
+        last step's AdamW is one prl_ppo_adam_step.  Parameters and moments stay in the engine's
+        image layout in HBM for the whole loop, double-buffered (a launch reads one set while
+        its workgroups write their slices of the other).  With `comm` (an RCCL communicator from
+        dp_comm()) the loop is enqueued natively (prl_ppo_update_dp: no Python per step,
+        ncclAllReduce on torch's stream); otherwise it runs here, calling `all_reduce` on the
+        gradient image every step.  Both give the same bits."""
         import ctypes
         if not self.bound():
             self._bind()
@@ -205,6 +208,8 @@ class FusedUpdate:
         if getattr(self, "img", None) is None or self.img[0].numel() != L:
             self.img = [torch.zeros(L, dtype=torch.float32, device=dev) for _ in range(3)]
             self.grad = torch.zeros(L, dtype=torch.float32, device=dev)
+            self.img_b = [torch.zeros(L, dtype=torch.float32, device=dev) for _ in range(3)]
+            self.grad_b = torch.zeros(L, dtype=torch.float32, device=dev)
         img_p, img_m, img_v = self.img
         prl_native.ppo_image(self.D, self.A, self.discrete, self.flat, self.m, self.v,
                              img_p, img_m, img_v, True)
@@ -218,16 +223,9 @@ class FusedUpdate:
         P = ctypes.c_void_p
         lib = prl_native.lib()
         stream = P(torch.cuda.current_stream().cuda_stream)
-        grad_fixed = (P(img_p.data_ptr()), self.D, self.A, int(self.discrete)) + tuple(
-            P(x.data_ptr()) for x in tens) + (int(S.shape[0]), mb)
-        grad_tail = (ctypes.c_float(self.ppo.policy_clip), ctypes.c_float(self.ppo.value_coef),
-                     P(self.grad.data_ptr()), P(self.ws.data_ptr()), self.ws.numel(), stream)
-        adam_head = (P(img_p.data_ptr()), P(img_m.data_ptr()), P(img_v.data_ptr()), self.D, self.A,
-                     int(self.discrete), P(self.grad.data_ptr()))
-        adam_mid = tuple(ctypes.c_float(x) for x in (group["lr"], beta1, beta2, group["eps"],
-                                                     group["weight_decay"], 2.0))
-        adam_tail = (ctypes.c_float(self.ppo.value_coef), ctypes.c_float(self.ppo.entropy_coef),
-                     P(self.loss.data_ptr()), stream)
+        hyper = tuple(ctypes.c_float(x) for x in (
+            self.ppo.policy_clip, self.ppo.value_coef, self.ppo.entropy_coef, group["lr"], beta1,
+            beta2, group["eps"], group["weight_decay"], 2.0))
         step = int(round(float(self.step.item())))
         n_local = int(S.shape[0])
         if comm is not None:
@@ -245,24 +243,50 @@ class FusedUpdate:
                                     k_epochs * nb))
             step += k_epochs * nb
             k_epochs = 0   # the Python loop below has nothing left to do
-        for _ in range(k_epochs):
-            for j in range(nb):
-                inv = ctypes.c_float(1.0 / counts[j])
-                if self.events is not None:
-                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                    ev[0].record()
-                rc = lib.prl_ppo_grad_step(*grad_fixed, j, inv, *grad_tail)
-                if rc != 0:
-                    prl_native._check(rc, "prl_ppo_grad_step")
-                if self.events is not None:
-                    ev[1].record()
-                    self.events.append(("ppo_grad_kernel", ev[0], ev[1],
-                                        min(mb, max(0, n_local - j * mb)), 1))
-                all_reduce(self.grad)
-                step += 1
-                rc = lib.prl_ppo_adam_step(*adam_head, step, *adam_mid, inv, *adam_tail)
-                if rc != 0:
-                    prl_native._check(rc, "prl_ppo_adam_step")
+        sets = [self.img, self.img_b]
+        grads = [self.grad, self.grad_b]
+        cur, inv_prev, total = 0, 0.0, k_epochs * nb
+        null = P()
+        for s in range(total):
+            j = s % nb
+            inv = 1.0 / counts[j]
+            if s > 0:
+                fin, fout, gprev = sets[cur], sets[cur ^ 1], grads[(s - 1) & 1]
+                fold = tuple(P(x.data_ptr()) for x in fin + fout) + (P(gprev.data_ptr()), step,
+                                                                     ctypes.c_float(inv_prev))
+                cur ^= 1
+            else:
+                fold = (P(sets[0][0].data_ptr()),) + (null,) * 6 + (0, ctypes.c_float(0.0))
+            gout = grads[s & 1]
+            if self.events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            rc = lib.prl_ppo_grad_fold_step(
+                *fold, self.D, self.A, int(self.discrete), *(P(x.data_ptr()) for x in tens),
+                n_local, mb, j, ctypes.c_float(inv), *hyper, P(self.loss.data_ptr()),
+                P(gout.data_ptr()), P(self.ws.data_ptr()), self.ws.numel(), stream)
+            if rc != 0:
+                prl_native._check(rc, "prl_ppo_grad_fold_step")
+            if self.events is not None:
+                ev[1].record()
+                self.events.append(("ppo_grad_kernel", ev[0], ev[1],
+                                    min(mb, max(0, n_local - j * mb)), 1))
+            all_reduce(gout)
+            step += 1
+            inv_prev = inv
+        if total > 0:
+            p_, m_, v_ = sets[cur]
+            rc = lib.prl_ppo_adam_step(
+                P(p_.data_ptr()), P(m_.data_ptr()), P(v_.data_ptr()), self.D, self.A,
+                int(self.discrete), P(grads[(total - 1) & 1].data_ptr()), step, *hyper[3:],
+                ctypes.c_float(inv_prev), hyper[1], hyper[2], P(self.loss.data_ptr()), stream)
+            if rc != 0:
+                prl_native._check(rc, "prl_ppo_adam_step")
+            if cur != 0:
+                for dst, src in zip(self.img, self.img_b):
+                    dst.copy_(src)
+            if (total - 1) & 1:
+                self.grad.copy_(self.grad_b)
         prl_native.ppo_image(self.D, self.A, self.discrete, self.flat, self.m, self.v,
                              img_p, img_m, img_v, False)
         self.step.fill_(float(step))

@@ -1292,6 +1292,135 @@ __global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_evaluate_kerne
   }
 }
 
+// ---- AdamW pieces shared by ppo_adam_kernel and the folded prologue of ppo_grad_kernel: one
+// arithmetic, so the folded and the separate AdamW give the same bits.
+struct AdamConst {
+  float step_size, inv_bc2_sqrt, decay, omb1, omb2, beta2, eps;
+};
+__device__ __forceinline__ AdamConst adam_const(double tstep, float lr, float beta1, float beta2,
+                                                float eps, float wd) {
+  const double bc1 = 1.0 - pow((double)beta1, tstep);
+  const double bc2 = 1.0 - pow((double)beta2, tstep);
+  AdamConst c;
+  c.step_size = (float)((double)lr / bc1);
+  c.inv_bc2_sqrt = (float)(1.0 / sqrt(bc2));
+  c.decay = (float)(1.0 - (double)lr * (double)wd);
+  c.omb1 = (float)(1.0 - (double)beta1);
+  c.omb2 = (float)(1.0 - (double)beta2);
+  c.beta2 = beta2;
+  c.eps = eps;
+  return c;
+}
+__device__ __forceinline__ float adam_sq4(float4 r) { return r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w; }
+// clip coefficient from this thread's partial sum of squares; 256 threads, 4 wave partials in
+// s_part (LDS), summed in wave order (every workgroup forms the same value)
+__device__ __forceinline__ float adam_clip(float acc, float max_norm, float* s_part) {
+  const int t = threadIdx.x;
+  acc = wave_sum(acc);
+  if ((t & 63) == 0) s_part[t >> 6] = acc;
+  __syncthreads();
+  float tot = 0.f;
+  for (int w = 0; w < UPD_THREADS / 64; ++w) tot += s_part[w];
+  const float coef = max_norm / (sqrtf(tot) + 1e-6f);
+  return coef < 1.0f ? coef : 1.0f;
+}
+__device__ __forceinline__ void adam_quad(const AdamConst& c, float clipc, float4 g4, float4& m4,
+                                          float4& v4, float4& pw) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float gr = f4get(g4, e) * clipc;
+    float m = f4get(m4, e), v = f4get(v4, e), p = f4get(pw, e);
+    p = p * c.decay;
+    m = m + c.omb1 * (gr - m);
+    v = v * c.beta2 + c.omb2 * gr * gr;
+    const float denom = __builtin_amdgcn_sqrtf(v) * c.inv_bc2_sqrt + c.eps;
+    float rq = __builtin_amdgcn_rcpf(denom);
+    rq = rq * (2.0f - denom * rq);
+    p = p - c.step_size * (m * rq);
+    f4set(m4, e, m);
+    f4set(v4, e, v);
+    f4set(pw, e, p);
+  }
+}
+__device__ __forceinline__ float adam_loss(const float* grad, int Lp, float inv_count, float vf_coef,
+                                           float ent_coef) {
+  const float4 lp = *reinterpret_cast<const float4*>(grad + Lp);
+  return lp.x * inv_count + vf_coef * (lp.y * inv_count) - ent_coef * (lp.z * inv_count);
+}
+
+// The previous optimizer step's clip + AdamW folded into the next gradient launch (stepped mode):
+// every workgroup applies it to ALL parameters of its LDS copy (identical inputs and code, so the
+// copies agree), and workgroup g also writes quads [g Qp / G, (g+1) Qp / G) of the new parameter /
+// moment images.  in != out (other workgroups are still reading `in`), grad_prev != this launch's
+// grad_out: the caller double-buffers both.  grad_prev == nullptr: no prologue (first step).
+struct UpdFold {
+  const float* grad_prev;             // all-reduced gradient image (+ loss quad) of the previous step
+  const float *p_in, *m_in, *v_in;    // state before that step's AdamW
+  float *p_out, *m_out, *v_out;       // state after it
+  double tstep;                       // that step's AdamW step number (1-based)
+  float lr, beta1, beta2, eps, wd, max_norm, inv_count, vf_coef, ent_coef;
+  float* loss_out;                    // that step's loss (workgroup 0), may be null
+};
+
+// NI > 0: Qp <= 256 NI known at compile time, every load issued before the norm (one round trip);
+// NI == 0: runtime layout, norm loop then update loop.  Same summation order as ppo_adam_kernel.
+template <int NI>
+__device__ __forceinline__ void upd_fold_adam(const UpdFold& f, int Lp, float* W, float* s_part) {
+  const int t = threadIdx.x, g = blockIdx.x, G = gridDim.x, Qp = Lp / 4;
+  const int qlo = (int)((int64_t)g * Qp / G), qhi = (int)((int64_t)(g + 1) * Qp / G);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (NI > 0) {
+    float4 gq[NI], mq[NI], vq[NI], pq[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = t + i * UPD_THREADS;
+      const bool in = q < Qp;
+      gq[i] = in ? *reinterpret_cast<const float4*>(f.grad_prev + 4 * q) : z4;
+      mq[i] = in ? *reinterpret_cast<const float4*>(f.m_in + 4 * q) : z4;
+      vq[i] = in ? *reinterpret_cast<const float4*>(f.v_in + 4 * q) : z4;
+      pq[i] = in ? *reinterpret_cast<const float4*>(f.p_in + 4 * q) : z4;
+    }
+    const AdamConst c = adam_const(f.tstep, f.lr, f.beta1, f.beta2, f.eps, f.wd);
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) acc += adam_sq4(gq[i]);
+    const float clipc = adam_clip(acc, f.max_norm, s_part);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = t + i * UPD_THREADS;
+      if (q < Qp) {
+        adam_quad(c, clipc, gq[i], mq[i], vq[i], pq[i]);
+        *reinterpret_cast<float4*>(W + 4 * q) = pq[i];
+        if (q >= qlo && q < qhi) {
+          *reinterpret_cast<float4*>(f.p_out + 4 * q) = pq[i];
+          *reinterpret_cast<float4*>(f.m_out + 4 * q) = mq[i];
+          *reinterpret_cast<float4*>(f.v_out + 4 * q) = vq[i];
+        }
+      }
+    }
+  } else {
+    float acc = 0.f;
+    for (int q = t; q < Qp; q += UPD_THREADS) acc += adam_sq4(*reinterpret_cast<const float4*>(f.grad_prev + 4 * q));
+    const AdamConst c = adam_const(f.tstep, f.lr, f.beta1, f.beta2, f.eps, f.wd);
+    const float clipc = adam_clip(acc, f.max_norm, s_part);
+    for (int q = t; q < Qp; q += UPD_THREADS) {
+      const float4 g4 = *reinterpret_cast<const float4*>(f.grad_prev + 4 * q);
+      float4 m4 = *reinterpret_cast<const float4*>(f.m_in + 4 * q);
+      float4 v4 = *reinterpret_cast<const float4*>(f.v_in + 4 * q);
+      float4 pw = *reinterpret_cast<const float4*>(f.p_in + 4 * q);
+      adam_quad(c, clipc, g4, m4, v4, pw);
+      *reinterpret_cast<float4*>(W + 4 * q) = pw;
+      if (q >= qlo && q < qhi) {
+        *reinterpret_cast<float4*>(f.p_out + 4 * q) = pw;
+        *reinterpret_cast<float4*>(f.m_out + 4 * q) = m4;
+        *reinterpret_cast<float4*>(f.v_out + 4 * q) = v4;
+      }
+    }
+  }
+  if (g == 0 && t == 0 && f.loss_out)
+    f.loss_out[0] = adam_loss(f.grad_prev, Lp, f.inv_count, f.vf_coef, f.ent_coef);
+}
+
 // ---- stepped mode (world_size > 1): one optimizer step = grad kernel -> RCCL all-reduce of the
 // flat gradient (caller) -> AdamW kernel.  Parameters and moments live in HBM in the LDS-image
 // layout between launches ("images"); prl_ppo_image converts to / from torch's flat vectors.
@@ -1300,10 +1429,10 @@ __global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_evaluate_kerne
 // partial gradients per workgroup, then the in-GPU reduction into grad_out[Lp + 4] (the last
 // quad: loss partials {sum -min(s1,s2), sum SmoothL1, sum H}).  inv_count = 1 / (rows of the
 // union minibatch over all ranks), so the all-reduced sum is the union's gradient.
-template <int KD, int KA>
+template <int KD, int KA, int NI>
 __device__ __forceinline__ void ppo_grad_body(const UpdNet& n, const UpdArgs& args, const float* img,
                                               float* grad_out, int64_t row0, int B_local,
-                                              float inv_count) {
+                                              float inv_count, const UpdFold& fold) {
   constexpr int NW = upd_nw<KD, KA>(), NT = 64 * NW;
   extern __shared__ __align__(16) float upd_lds[];
   const int t = threadIdx.x, g = blockIdx.x, G = args.G;
@@ -1316,8 +1445,13 @@ __device__ __forceinline__ void ppo_grad_body(const UpdNet& n, const UpdArgs& ar
   float* s_ssq = hdr + 4;
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
   unsigned long long* tm = reinterpret_cast<unsigned long long*>(hdr + 16);
-  for (int q = t; q < Qp; q += NT)   // written by the previous launch: plain loads
-    *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(img + 4 * q);
+  static_assert(NT == UPD_THREADS, "the folded AdamW assumes 256-thread workgroups");
+  if (fold.grad_prev) {                // previous step's AdamW, then this step's gradient
+    upd_fold_adam<NI>(fold, Lp, W, scratch);
+  } else {
+    for (int q = t; q < Qp; q += NT)   // written by the previous launch: plain loads
+      *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(img + 4 * q);
+  }
   for (int k = t; k < Lp + 4; k += NT) Ga[k] = 0.0f;
   if (t < 24) tm[t] = 0ull;
   __syncthreads();
@@ -1350,17 +1484,23 @@ __device__ __forceinline__ void ppo_grad_body(const UpdNet& n, const UpdArgs& ar
 template <int KD, int KA, int KDIM>
 __global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_grad_kernel(UpdArgs args, const float* img,
                                                                 float* grad_out, int64_t row0,
-                                                                int B_local, float inv_count) {
+                                                                int B_local, float inv_count,
+                                                                UpdFold fold) {
   if constexpr (KDIM > 0) {
     constexpr UpdNet N = upd_make(KDIM, KA, KD);
-    ppo_grad_body<KD, KA>(N, args, img, grad_out, row0, B_local, inv_count);
+    constexpr int NI = (N.Lp / 4 + UPD_THREADS - 1) / UPD_THREADS;
+    ppo_grad_body<KD, KA, NI>(N, args, img, grad_out, row0, B_local, inv_count, fold);
   } else {
-    ppo_grad_body<KD, KA>(args.net, args, img, grad_out, row0, B_local, inv_count);
+    ppo_grad_body<KD, KA, 0>(args.net, args, img, grad_out, row0, B_local, inv_count, fold);
   }
 }
 
 // clip_grad_norm_(max_norm) + AdamW on the images, one parameter quad per thread.  Every
-// workgroup forms the same norm (same order), so no hand-off is needed.
+// workgroup forms the same norm (same order), so no hand-off is needed.  Latency-bound (a few
+// KB per workgroup): every load — the whole gradient for the norm AND this thread's own
+// gradient / moment / parameter quads — is issued at entry, so the kernel pays ONE memory
+// round trip; the bias corrections are formed while those loads are in flight.
+constexpr int ADAM_PF = 24;   // gradient quads per thread held in registers (Qp <= 6144)
 __global__ __launch_bounds__(UPD_THREADS) void ppo_adam_kernel(int Lp, float* img_p, float* img_m,
                                                              float* img_v, const float* grad,
                                                              double tstep, float lr, float beta1,
@@ -1370,53 +1510,35 @@ __global__ __launch_bounds__(UPD_THREADS) void ppo_adam_kernel(int Lp, float* im
                                                              float* loss_out) {
   __shared__ float s_part[UPD_THREADS / 64];
   const int t = threadIdx.x, Qp = Lp / 4;
-  float acc = 0.f;
-  for (int q = t; q < Qp; q += UPD_THREADS) {
-    const float4 r = *reinterpret_cast<const float4*>(grad + 4 * q);
-    acc += r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w;
-  }
-  acc = wave_sum(acc);
-  if ((t & 63) == 0) s_part[t >> 6] = acc;
-  __syncthreads();
-  float tot = 0.f;
-  for (int w = 0; w < UPD_THREADS / 64; ++w) tot += s_part[w];
-  const float coef = max_norm / (sqrtf(tot) + 1e-6f);
-  const float clipc = coef < 1.0f ? coef : 1.0f;
-  const double bc1 = 1.0 - pow((double)beta1, tstep);
-  const double bc2 = 1.0 - pow((double)beta2, tstep);
-  const float step_size = (float)((double)lr / bc1);
-  const float inv_bc2_sqrt = (float)(1.0 / sqrt(bc2));
-  const float decay = (float)(1.0 - (double)lr * (double)wd);
-  const float omb1 = (float)(1.0 - (double)beta1), omb2 = (float)(1.0 - (double)beta2);
   const int q = blockIdx.x * UPD_THREADS + t;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 g4 = z4, m4 = z4, v4 = z4, pw = z4;
   if (q < Qp) {
-    const float4 g4 = *reinterpret_cast<const float4*>(grad + 4 * q);
-    float4 m4 = *reinterpret_cast<const float4*>(img_m + 4 * q);
-    float4 v4 = *reinterpret_cast<const float4*>(img_v + 4 * q);
-    float4 pw = *reinterpret_cast<const float4*>(img_p + 4 * q);
+    g4 = *reinterpret_cast<const float4*>(grad + 4 * q);
+    m4 = *reinterpret_cast<const float4*>(img_m + 4 * q);
+    v4 = *reinterpret_cast<const float4*>(img_v + 4 * q);
+    pw = *reinterpret_cast<const float4*>(img_p + 4 * q);
+  }
+  float4 pre[ADAM_PF];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float gr = f4get(g4, e) * clipc;
-      float m = f4get(m4, e), v = f4get(v4, e), p = f4get(pw, e);
-      p = p * decay;
-      m = m + omb1 * (gr - m);
-      v = v * beta2 + omb2 * gr * gr;
-      const float denom = __builtin_amdgcn_sqrtf(v) * inv_bc2_sqrt + eps;
-      float rq = __builtin_amdgcn_rcpf(denom);
-      rq = rq * (2.0f - denom * rq);
-      p = p - step_size * (m * rq);
-      f4set(m4, e, m);
-      f4set(v4, e, v);
-      f4set(pw, e, p);
-    }
+  for (int i = 0; i < ADAM_PF; ++i) {
+    const int qq = t + i * UPD_THREADS;
+    pre[i] = qq < Qp ? *reinterpret_cast<const float4*>(grad + 4 * qq) : z4;
+  }
+  const AdamConst c = adam_const(tstep, lr, beta1, beta2, eps, wd);
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < ADAM_PF; ++i) acc += adam_sq4(pre[i]);
+  for (int qq = t + ADAM_PF * UPD_THREADS; qq < Qp; qq += UPD_THREADS)  // beyond the registers
+    acc += adam_sq4(*reinterpret_cast<const float4*>(grad + 4 * qq));
+  const float clipc = adam_clip(acc, max_norm, s_part);
+  if (q < Qp) {
+    adam_quad(c, clipc, g4, m4, v4, pw);
     *reinterpret_cast<float4*>(img_m + 4 * q) = m4;
     *reinterpret_cast<float4*>(img_v + 4 * q) = v4;
     *reinterpret_cast<float4*>(img_p + 4 * q) = pw;
   }
-  if (blockIdx.x == 0 && t == 0 && loss_out) {
-    const float4 lp = *reinterpret_cast<const float4*>(grad + Lp);
-    loss_out[0] = lp.x * inv_count + vf_coef * (lp.y * inv_count) - ent_coef * (lp.z * inv_count);
-  }
+  if (blockIdx.x == 0 && t == 0 && loss_out) loss_out[0] = adam_loss(grad, Lp, inv_count, vf_coef, ent_coef);
 }
 
 // torch flat vectors <-> images (to_image: flat -> image, else image -> flat)
@@ -1691,7 +1813,8 @@ extern "C" int prl_ppo_grad_step(const float* img_params, int32_t D, int32_t A, 
   int64_t r0 = row0;
   int bl = B_local;
   const float* img = img_params;
-  void* kargs[] = {&args, &img, &grad_out, &r0, &bl, &inv};
+  UpdFold nofold{};
+  void* kargs[] = {&args, &img, &grad_out, &r0, &bl, &inv, &nofold};
   // plain launch: G <= 256 workgroups of 1 per CU are co-resident in practice; the in-kernel
   // wait is bounded and reports a timeout through the status word like the persistent kernel
   PRL_HIP_TRY(hipLaunchKernel(kern, dim3(G), dim3(upd_nt(args.net)), kargs, lds, st));
@@ -1714,6 +1837,68 @@ extern "C" int prl_ppo_adam_step(float* img_params, float* img_m, float* img_v, 
 }
 
 // status word of the last launch on this workspace (device u32: 0 ok, 1 = in-kernel timeout)
+// One folded stepped launch: the previous optimizer step's clip + AdamW (state in_* -> out_*,
+// gradient grad_prev = its all-reduced gradient image) and then this rank's gradient of global
+// minibatch j from the updated parameters, into grad_out.  in_* != out_* and grad_prev !=
+// grad_out (the caller double-buffers).  grad_prev == NULL: no AdamW, parameters read from in_p.
+extern "C" int prl_ppo_grad_fold_step(const float* in_p, const float* in_m, const float* in_v,
+                                      float* out_p, float* out_m, float* out_v,
+                                      const float* grad_prev, int64_t step_prev,
+                                      float inv_count_prev, int32_t D, int32_t A, int32_t discrete,
+                                      const float* S, const float* actions, const float* old_logp,
+                                      const float* adv, const float* ret, int64_t N,
+                                      int32_t mini_batch, int64_t minibatch_index, float inv_count,
+                                      float clip, float vf_coef, float ent_coef, float lr,
+                                      float beta1, float beta2, float eps, float weight_decay,
+                                      float max_norm, float* loss_out, float* grad_out,
+                                      void* workspace, int64_t workspace_bytes, void* stream) {
+  UpdArgs args{};
+  PRL_REQUIRE(upd_layout(D, A, discrete, args.net), "prl_ppo_grad_fold_step: D=%d A=%d not supported", D, A);
+  PRL_REQUIRE(N >= 0 && mini_batch > 0 && minibatch_index >= 0, "prl_ppo_grad_fold_step: bad sizes");
+  PRL_REQUIRE(in_p && grad_out && workspace, "prl_ppo_grad_fold_step: null pointer");
+  PRL_REQUIRE(!grad_prev || (in_m && in_v && out_p && out_m && out_v && step_prev >= 1),
+              "prl_ppo_grad_fold_step: AdamW operands missing");
+  PRL_REQUIRE(grad_prev != grad_out && (!grad_prev || (out_p != in_p && out_m != in_m && out_v != in_v)),
+              "prl_ppo_grad_fold_step: in/out buffers must differ");
+  const int G = upd_grid(mini_batch);
+  UpdWs ws;
+  const size_t need = upd_ws_carve(args.net, G, reinterpret_cast<char*>(workspace), &ws);
+  PRL_REQUIRE((size_t)workspace_bytes >= need, "prl_ppo_grad_fold_step: workspace too small");
+  const int64_t row0 = minibatch_index * (int64_t)mini_batch;
+  const int B_local = (int)std::max<int64_t>(0, std::min<int64_t>(mini_batch, N - row0));
+  PRL_REQUIRE(B_local == 0 || (S && actions && old_logp && adv && ret), "prl_ppo_grad_fold_step: null input");
+  args.S = S;
+  args.act = actions;
+  args.old_logp = old_logp;
+  args.adv = adv;
+  args.ret = ret;
+  args.N = N;
+  args.mb = mini_batch;
+  args.G = G;
+  args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RT) * UPD_RT;
+  args.clip = clip;
+  args.vf_coef = vf_coef;
+  args.part = ws.part;
+  args.ctr = ws.ctr;
+  args.grad_target = (unsigned)G;
+  args.profile = upd_profile_enabled();
+  UpdFold f{grad_prev, in_p, in_m, in_v, out_p, out_m, out_v, (double)step_prev,
+            lr, beta1, beta2, eps, weight_decay, max_norm, inv_count_prev, vf_coef, ent_coef,
+            loss_out};
+  const size_t lds = upd_lds_bytes(args.net);
+  hipStream_t st = as_stream(stream);
+  const void* kern = upd_grad_kernel_for(args.net);
+  PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
+  float inv = inv_count;
+  int64_t r0 = row0;
+  int bl = B_local;
+  const float* img = in_p;
+  void* kargs[] = {&args, &img, &grad_out, &r0, &bl, &inv, &f};
+  PRL_HIP_TRY(hipLaunchKernel(kern, dim3(G), dim3(upd_nt(args.net)), kargs, lds, st));
+  return PRL_OK;
+}
+
 extern "C" int prl_ppo_update_status_ptr(void* workspace, uint32_t** status) {
   PRL_REQUIRE(workspace && status, "prl_ppo_update_status_ptr: null pointer");
   *status = reinterpret_cast<uint32_t*>(workspace) + 3;
@@ -1842,25 +2027,55 @@ extern "C" int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, 
   const unsigned adam_grid = (unsigned)cdiv(args.net.Lp / 4, UPD_THREADS);
   const size_t count = (size_t)args.net.Lp + 4;   // the image + its loss quad
   const ncclComm_t c = reinterpret_cast<ncclComm_t>(comm);
+  // Per step: ONE launch (the previous step's AdamW folded in front of this step's gradient) and
+  // the all-reduce; the last step's AdamW is a separate ppo_adam_kernel.  State and gradient
+  // double-buffered: set 0 = the caller's images / grad, set 1 = the workspace's persistent-launch
+  // images (unused in stepped mode) and reduction buffer.
+  float* sp[2] = {img_params, ws.img};
+  float* sm[2] = {img_m, ws.img + count};
+  float* sv[2] = {img_v, ws.img + 2 * count};
+  float* gb[2] = {grad, ws.red};
+  int cur = 0;
   int64_t step = step0;
   unsigned launches = 0;
-  for (int e = 0; e < k_epochs; ++e) {
-    for (int64_t j = 0; j < nb; ++j) {
-      const int64_t row0 = j * (int64_t)mini_batch;
-      int B_local = (int)std::max<int64_t>(0, std::min<int64_t>(mini_batch, N - row0));
-      float inv = 1.0f / (float)counts[j];
-      int64_t r0 = row0;
-      const float* img = img_params;
-      args.grad_target = (unsigned)G * (++launches);
-      void* kargs[] = {&args, &img, &grad, &r0, &B_local, &inv};
-      PRL_HIP_TRY(hipLaunchKernel(kern, dim3(G), dim3(nt), kargs, lds, st));
-      PRL_RCCL_TRY(g_rccl.all_reduce(grad, grad, count, ncclFloat32, ncclSum, c, st), "ncclAllReduce");
-      ++step;
-      hipLaunchKernelGGL(ppo_adam_kernel, dim3(adam_grid), dim3(UPD_THREADS), 0, st, args.net.Lp,
-                         img_params, img_m, img_v, grad, (double)step, lr, beta1, beta2, eps,
-                         weight_decay, max_norm, inv, vf_coef, ent_coef, loss_out);
-      PRL_LAUNCH_CHECK("ppo_adam_step");
+  const int64_t total = (int64_t)k_epochs * nb;
+  float inv_prev = 0.f;
+  for (int64_t s = 0; s < total; ++s) {
+    const int64_t j = s % nb;
+    const int64_t row0 = j * (int64_t)mini_batch;
+    int B_local = (int)std::max<int64_t>(0, std::min<int64_t>(mini_batch, N - row0));
+    float inv = 1.0f / (float)counts[j];
+    int64_t r0 = row0;
+    float* gout = gb[s & 1];
+    UpdFold f{};
+    const float* img = sp[cur];
+    if (s > 0) {
+      f = UpdFold{gb[(s - 1) & 1], sp[cur], sm[cur], sv[cur], sp[cur ^ 1], sm[cur ^ 1], sv[cur ^ 1],
+                  (double)step, lr, beta1, beta2, eps, weight_decay, max_norm, inv_prev, vf_coef,
+                  ent_coef, loss_out};
+      cur ^= 1;
     }
+    args.grad_target = (unsigned)G * (++launches);
+    void* kargs[] = {&args, &img, &gout, &r0, &B_local, &inv, &f};
+    PRL_HIP_TRY(hipLaunchKernel(kern, dim3(G), dim3(nt), kargs, lds, st));
+    PRL_RCCL_TRY(g_rccl.all_reduce(gout, gout, count, ncclFloat32, ncclSum, c, st), "ncclAllReduce");
+    ++step;
+    inv_prev = inv;
+  }
+  if (total > 0) {
+    hipLaunchKernelGGL(ppo_adam_kernel, dim3(adam_grid), dim3(UPD_THREADS), 0, st, args.net.Lp,
+                       sp[cur], sm[cur], sv[cur], gb[(total - 1) & 1], (double)step, lr, beta1,
+                       beta2, eps, weight_decay, max_norm, inv_prev, vf_coef, ent_coef, loss_out);
+    PRL_LAUNCH_CHECK("ppo_adam_step");
+    if (cur != 0) {
+      for (int a = 0; a < 3; ++a) {
+        float* src = a == 0 ? sp[1] : a == 1 ? sm[1] : sv[1];
+        float* dst = a == 0 ? sp[0] : a == 1 ? sm[0] : sv[0];
+        PRL_HIP_TRY(hipMemcpyAsync(dst, src, sizeof(float) * args.net.Lp, hipMemcpyDeviceToDevice, st));
+      }
+    }
+    if (((total - 1) & 1) != 0)   // the caller's grad holds the last all-reduced gradient
+      PRL_HIP_TRY(hipMemcpyAsync(grad, ws.red, sizeof(float) * count, hipMemcpyDeviceToDevice, st));
   }
   return PRL_OK;
 }

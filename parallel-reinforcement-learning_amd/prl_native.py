@@ -67,6 +67,8 @@ SIGNATURES = {
     "prl_ppo_grad_step": [_P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I64, _F32, _F32,
                           _F32, _P, _P, _I64, _P],
     "prl_ppo_adam_step": [_P, _P, _P, _I32, _I32, _I32, _P, _I64] + [_F32] * 9 + [_P, _P],
+    "prl_ppo_grad_fold_step": [_P] * 7 + [_I64, _F32, _I32, _I32, _I32] + [_P] * 5
+                              + [_I64, _I32, _I64] + [_F32] * 10 + [_P, _P, _P, _I64, _P],
 }
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64,
              "prl_ppo_image_floats": _I64}

@@ -418,3 +418,79 @@ def test_generic_shape_engine_gradient(cont, D, A):
         m = p.optimizer.state[prm]["exp_avg"].double().cpu() / 0.1
         per[name] = float((m - gr).abs().max()) / (float(gr.abs().max()) + 1e-30)
     assert max(per.values()) <= 1e-4, per
+
+
+def _unfolded_stepped(eng, S, A, old, adv, ret, k_epochs, n_ranks):
+    """The stepped loop in its unfolded form (prl_ppo_grad_step -> identity all-reduce ->
+    prl_ppo_adam_step per optimizer step): the reference for the folded launch."""
+    import ctypes
+    import prl_native
+    ppo = eng.ppo
+    group = ppo.optimizer.param_groups[0]
+    beta1, beta2 = group["betas"]
+    L = prl_native.ppo_image_floats(eng.D, eng.A, eng.discrete)
+    img = [torch.zeros(L, device="cuda") for _ in range(3)]
+    grad = torch.zeros(L, device="cuda")
+    prl_native.ppo_image(eng.D, eng.A, eng.discrete, eng.flat, eng.m, eng.v, *img, True)
+    mb = eng.mini_batch
+    nb = max(-(-n // mb) for n in n_ranks)
+    counts = [sum(min(mb, max(0, n - j * mb)) for n in n_ranks) for j in range(nb)]
+    A2 = (A if A.dim() == 2 else A.reshape(-1, 1)).contiguous()
+    tens = [S.contiguous(), A2, old.contiguous(), adv.contiguous(), ret.contiguous()]
+    P, lib = ctypes.c_void_p, prl_native.lib()
+    stream = P(torch.cuda.current_stream().cuda_stream)
+    step = int(round(float(eng.step.item())))
+    for _ in range(k_epochs):
+        for j in range(nb):
+            inv = ctypes.c_float(1.0 / counts[j])
+            assert lib.prl_ppo_grad_step(P(img[0].data_ptr()), eng.D, eng.A, int(eng.discrete),
+                                         *(P(x.data_ptr()) for x in tens), int(S.shape[0]), mb, j,
+                                         inv, ctypes.c_float(ppo.policy_clip),
+                                         ctypes.c_float(ppo.value_coef), P(grad.data_ptr()),
+                                         P(eng.ws.data_ptr()), eng.ws.numel(), stream) == 0
+            step += 1
+            assert lib.prl_ppo_adam_step(*(P(x.data_ptr()) for x in img), eng.D, eng.A,
+                                         int(eng.discrete), P(grad.data_ptr()), step,
+                                         *(ctypes.c_float(x) for x in (
+                                             group["lr"], beta1, beta2, group["eps"],
+                                             group["weight_decay"], 2.0)), inv,
+                                         ctypes.c_float(ppo.value_coef),
+                                         ctypes.c_float(ppo.entropy_coef),
+                                         P(eng.loss.data_ptr()), stream) == 0
+    torch.cuda.synchronize()
+    return [x.cpu() for x in img], grad.cpu(), float(eng.loss.item())
+
+
+@pytest.mark.parametrize("cont,D,A", [(False, 4, 2), (True, 3, 1), (False, 6, 3)])
+def test_folded_step_equals_grad_then_adam(cont, D, A):
+    """prl_ppo_grad_fold_step (previous step's AdamW folded in front of the next gradient,
+    double-buffered state) gives the same bits as the unfolded prl_ppo_grad_step ->
+    prl_ppo_adam_step sequence: parameter / moment images, last gradient and loss.  Covers the
+    compile-time layouts (all loads before the norm) and the runtime layout (D=6, A=3)."""
+    import prl_native
+    from PPO import PPO
+    N = 2500 + 3
+    data = _data(N, D, cont, seed=31)
+    torch.manual_seed(0)
+    p = PPO(cont, D, A, action_scaling=2.0 if cont else None, k_epochs=2, batch_size=64,
+            mini_batch_size=512)
+    p.show_progress = False
+    p.memory.push_device(*data)
+    p._world = staticmethod(lambda: 1)
+    captured = {}
+
+    def stepped_update(S, A_, old, adv, ret, n_ranks):
+        eng = p._fused_engine()
+        if not eng.bound():
+            eng._bind()
+        captured["ref"] = _unfolded_stepped(eng, S, A_, old, adv, ret, p.k_epochs, n_ranks)
+        p.last_loss = eng.run_stepped(S, A_, old, adv, ret, p.k_epochs, n_ranks, lambda t: t)
+        torch.cuda.synchronize()
+        captured["fold"] = ([x.cpu() for x in eng.img], eng.grad.cpu(), float(eng.loss.item()))
+    p._update = stepped_update
+    p.learn()
+    (ri, rg, rl), (fi, fg, fl) = captured["ref"], captured["fold"]
+    for a, b in zip(ri, fi):
+        assert torch.equal(a, b)
+    assert torch.equal(rg, fg) and rl == fl
+    assert float(p._engine.step.item()) == 2 * 5

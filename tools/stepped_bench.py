@@ -25,6 +25,19 @@ N, mb, k = 1 << 20, 512, 11
 batch = synthetic_batch(N)
 import prl_native  # noqa: E402
 prl_native.dp_rccl_open()
+# host-side enqueue time of the native loop: if it approaches the GPU time, the loop is host-bound
+_enq = []
+_orig_dp = prl_native.ppo_update_dp
+
+
+def _timed_dp(*a, **k):
+    t = time.perf_counter()
+    r = _orig_dp(*a, **k)
+    _enq.append(time.perf_counter() - t)
+    return r
+
+
+prl_native.ppo_update_dp = _timed_dp
 comm = prl_native.dp_comm_init(prl_native.dp_unique_id(), 1, 0)
 for label, ar, cm in (("identity", lambda t: t, None), ("rccl-1rank", dist.all_reduce, None),
                       ("native-rccl-1rank", None, comm)):
@@ -45,7 +58,10 @@ for label, ar, cm in (("identity", lambda t: t, None), ("rccl-1rank", dist.all_r
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     steps = k * -(-N // mb)
-    print(json.dumps({"all_reduce": label, "learn_update_ms_per_1M": round(dt * 1e3, 1),
-                      "us_per_step": round(dt / steps * 1e6, 2)}), flush=True)
+    rec = {"all_reduce": label, "learn_update_ms_per_1M": round(dt * 1e3, 1),
+           "us_per_step": round(dt / steps * 1e6, 2)}
+    if cm is not None and _enq:
+        rec["host_enqueue_us_per_step"] = round(_enq[-1] / steps * 1e6, 2)
+    print(json.dumps(rec), flush=True)
 prl_native.dp_comm_destroy(comm)
 dist.destroy_process_group()
