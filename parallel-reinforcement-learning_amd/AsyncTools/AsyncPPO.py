@@ -178,6 +178,7 @@ class AsyncPPO:  # AsyncPPO.py:104-165
         self.sample_seed = int.from_bytes(os.urandom(8), "little") if seed is None else (
             int(seed) * 0x9E3779B97F4A7C15 + 0x1234567) & (2**64 - 1)
         self._rollouts = 0
+        self._evals = 0
         self._traj = None
         self.last_vector_steps = 0
 
@@ -205,13 +206,19 @@ class AsyncPPO:  # AsyncPPO.py:104-165
                 break
 
     def _device_worker(self):
+        seed = (self.sample_seed + self._rollouts * 0xD1B54A32D192ED03) & (2**64 - 1)
+        self._rollouts += 1
+        k = self._device_rollout(seed)
+        return self._device_collect(k)
+
+    def _device_rollout(self, seed):
+        """One episode per env on the device (fused rollout step kernel per vector step, policy
+        on traj_obs[t]); returns the index of the last vector step taken."""
         env, spec = self.env, self.env.spec
         E = self.num_envs
         if self._traj is None:
             self._traj = DeviceTrajectory(E, spec, env.device)
         tr = self._traj
-        seed = (self.sample_seed + self._rollouts * 0xD1B54A32D192ED03) & (2**64 - 1)
-        self._rollouts += 1
         scaling = float(getattr(self.ppo, "action_scaling", None) or 1.0)
         env.reset_device(tr.obs[0])
         tr.active_after.zero_()
@@ -242,6 +249,11 @@ class AsyncPPO:  # AsyncPPO.py:104-165
             if finished:
                 break
         self.last_vector_steps = k + 1
+        return k
+
+    def _device_collect(self, k):
+        env, spec, tr = self.env, self.env.spec, self._traj
+        E = self.num_envs
         # env-major flatten straight into learn()'s input tensors
         prl_native.exclusive_scan_i32(tr.ep_len, tr.offsets)
         N = int(tr.offsets[E].item())
@@ -255,6 +267,26 @@ class AsyncPPO:  # AsyncPPO.py:104-165
         self.step_score = self.step_score + N
         self.reward_score = self.reward_score + float(tr.reward_sum.item())
         return N
+
+    # ------------------------------------------------------------------ evaluation
+    def evaluate(self):
+        """Test.py:19-35 without rendering, batched: one episode per env with the current
+        policy (the duck-typed ppo's dist_params, i.e. policy_old as in get_action), nothing
+        pushed to ppo.memory and the score counters untouched.  Returns (episode returns f64
+        [num_envs], episode lengths int [num_envs]) — Test.py's `reward_per_episode` and step
+        count of each env's episode.  Sampling keys come from a stream of their own, so
+        evaluating does not change the keys of later training rollouts."""
+        if not hasattr(self.ppo, "dist_params"):
+            raise RuntimeError("evaluate() needs the device policy path (ppo.dist_params)")
+        seed = (self.sample_seed ^ 0x5851F42D4C957F2D) + self._evals * 0xD1B54A32D192ED03
+        self._evals += 1
+        k = self._device_rollout(seed & (2**64 - 1))
+        tr = self._traj
+        T = k + 1
+        live = (torch.arange(T, device=tr.ep_len.device)[:, None] < tr.ep_len[None, :])
+        returns = torch.where(live, tr.rew[:T].double(), torch.zeros((), dtype=torch.float64,
+                                                                     device=live.device))
+        return returns.sum(0).cpu().numpy(), tr.ep_len.cpu().numpy().astype(np.int64)
 
     # ------------------------------------------------------------------ run
     def run(self):  # AsyncPPO.py:148-165

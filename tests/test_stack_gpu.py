@@ -134,6 +134,44 @@ def test_device_worker_bit_exact_vs_oracle_worker(E):
     assert len(stub.memory) == n + len(stub.memory._segments[1][0])
 
 
+def test_evaluate_matches_oracle_episodes():
+    """AsyncPPO.evaluate() (Test.py:19-35 batched, no render): per-env episode returns and
+    lengths equal the oracle's replay of the same rollout (same PCG64 resets, the evaluation's
+    own Philox key); nothing is pushed to memory and the score counters stay untouched; a
+    training rollout afterwards uses the same keys as without the evaluation."""
+    from AsyncTools.AsyncPPO import AsyncPPO
+    E, seed = 512, 11
+    probs = np.random.default_rng(3).dirichlet([2, 2], E).astype(np.float32)
+    stub = _FixedDist(torch.from_numpy(probs).cuda())
+    a = AsyncPPO("CartPole-v1", stub, num_envs=E, seed=seed)
+    ret, lens = a.evaluate()
+    assert len(stub.memory) == 0 and int(a.step_score) == 0 and float(a.reward_score) == 0.0
+    orc = O.CartPoleOracle(E)
+    orc.seed(np.arange(E) + seed)
+    es = ((a.sample_seed ^ 0x5851F42D4C957F2D) + 0) & (2**64 - 1)
+    ref = O.worker_oracle(orc, lambda s, idx, t: O.sample_categorical(
+        probs, es, np.full(E, t, np.int32))[idx])
+    ends = np.flatnonzero(ref["D"] == 1)
+    ref_len = np.diff(np.concatenate([[-1], ends]))
+    assert len(ref_len) == E
+    np.testing.assert_array_equal(lens, ref_len)
+    ref_ret = np.add.reduceat(ref["R"].astype(np.float64), np.concatenate([[0], ends[:-1] + 1]))
+    np.testing.assert_array_equal(ret, ref_ret)
+    # training keys unaffected: the first worker() after evaluate() samples with sample_seed
+    b = AsyncPPO("CartPole-v1", _FixedDist(torch.from_numpy(probs).cuda()), num_envs=E, seed=seed)
+    b.evaluate()
+    n = b.worker()
+    orc2 = O.CartPoleOracle(E)
+    orc2.seed(np.arange(E) + seed)
+    O.worker_oracle(orc2, lambda s, idx, t: O.sample_categorical(
+        probs, es, np.full(E, t, np.int32))[idx])          # the evaluation's episode
+    ref2 = O.worker_oracle(orc2, lambda s, idx, t: O.sample_categorical(
+        probs, b.sample_seed, np.full(E, t, np.int32))[idx])
+    assert n == len(ref2["S"])
+    S = b.ppo.memory.device_tensors("cuda")[0].cpu().numpy()
+    np.testing.assert_array_equal(S, ref2["S"])
+
+
 def test_device_worker_pendulum_shapes_and_truncation():
     from AsyncTools.AsyncPPO import AsyncPPO
     E = 4096
