@@ -27,20 +27,29 @@ import prl_native  # noqa: E402
 prl_native.dp_rccl_open()
 # host-side enqueue time of the native loop: if it approaches the GPU time, the loop is host-bound
 _enq = []
-_orig_dp = prl_native.ppo_update_dp
 
 
-def _timed_dp(*a, **k):
-    t = time.perf_counter()
-    r = _orig_dp(*a, **k)
-    _enq.append(time.perf_counter() - t)
-    return r
+def _timed(fn):
+    def wrap(*a, **k):
+        t = time.perf_counter()
+        r = fn(*a, **k)
+        _enq.append(time.perf_counter() - t)
+        return r
+    return wrap
 
 
-prl_native.ppo_update_dp = _timed_dp
+prl_native.ppo_update_dp = _timed(prl_native.ppo_update_dp)
+prl_native.ppo_update_dp_persistent = _timed(prl_native.ppo_update_dp_persistent)
 comm = prl_native.dp_comm_init(prl_native.dp_unique_id(), 1, 0)
-for label, ar, cm in (("identity", lambda t: t, None), ("rccl-1rank", dist.all_reduce, None),
-                      ("native-rccl-1rank", None, comm)):
+MODES = (("identity", lambda t: t, None, {}), ("rccl-1rank", dist.all_reduce, None, {}),
+         ("native-stepped-rccl-1rank", None, comm, {"PRL_DP_PERSISTENT": "0"}),
+         ("native-persistent-rccl-1rank", None, comm, {"PRL_DP_PERSISTENT": "1"}),
+         ("native-persistent-stand-in-kernel", None, comm,
+          {"PRL_DP_PERSISTENT": "1", "PRL_DP_STAND_IN": "1"}))
+for label, ar, cm, env in MODES:
+    for key in ("PRL_DP_PERSISTENT", "PRL_DP_STAND_IN"):
+        os.environ.pop(key, None)
+    os.environ.update(env)
     torch.manual_seed(0)
     p = PPO(False, 4, 2, lr=1e-3, k_epochs=k, batch_size=1, mini_batch_size=mb)
     p.show_progress = False
@@ -60,7 +69,7 @@ for label, ar, cm in (("identity", lambda t: t, None), ("rccl-1rank", dist.all_r
     steps = k * -(-N // mb)
     rec = {"all_reduce": label, "learn_update_ms_per_1M": round(dt * 1e3, 1),
            "us_per_step": round(dt / steps * 1e6, 2)}
-    if cm is not None and _enq:
+    if cm is not None and _enq:   # the timed (last) call of this mode
         rec["host_enqueue_us_per_step"] = round(_enq[-1] / steps * 1e6, 2)
     print(json.dumps(rec), flush=True)
 prl_native.dp_comm_destroy(comm)
