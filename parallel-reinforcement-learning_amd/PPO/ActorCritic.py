@@ -19,7 +19,7 @@ from torch import distributions, nn
 
 import prl_native
 
-from .layers import GroupNormSiLU, hidden_block as _block
+from .layers import GroupNormSiLU, Linear, hidden_block as _block
 
 
 class _CategoricalLogProb(torch.autograd.Function):
@@ -52,12 +52,12 @@ class ActorCritic(nn.Module):
         self.is_continuous = is_continuous
         self.model = nn.Sequential(*_block(observ_dim, 64))
         if is_continuous:
-            self.mu_head = nn.Sequential(*_block(64, 64), nn.Linear(64, action_dim))
-            self.log_std_head = nn.Sequential(*_block(64, 64), nn.Linear(64, action_dim))
+            self.mu_head = nn.Sequential(*_block(64, 64), Linear(64, action_dim))
+            self.log_std_head = nn.Sequential(*_block(64, 64), Linear(64, action_dim))
         else:
-            self.actor = nn.Sequential(*_block(64, 64), nn.Linear(64, action_dim),
+            self.actor = nn.Sequential(*_block(64, 64), Linear(64, action_dim),
                                        nn.Softmax(dim=-1))
-        self.critic = nn.Sequential(*_block(64, 64), nn.Linear(64, 1))
+        self.critic = nn.Sequential(*_block(64, 64), Linear(64, 1))
         self.init_weights()
         if device is None:
             device = torch.device("cuda" if torch.cuda.is_available() else "cpu")

@@ -15,14 +15,14 @@ from torch import nn, optim
 
 import prl_native
 
-from .layers import GroupNormSiLU
+from .layers import GroupNormSiLU, Linear
 
 
 class RND(nn.Module):
     def __init__(self, in_features: int, out_features: int, beta: float = 0.001, device=None):
         super().__init__()
-        model = nn.Sequential(nn.Linear(in_features, 64), GroupNormSiLU(8, 64), nn.Identity(),
-                              nn.Linear(64, out_features))
+        model = nn.Sequential(Linear(in_features, 64), GroupNormSiLU(8, 64), nn.Identity(),
+                              Linear(64, out_features))
         self.target_net = deepcopy(model)
         self.pred_net = deepcopy(model)
         del model

@@ -50,6 +50,58 @@ class GroupNormSiLU(nn.GroupNorm):
         return F.silu(F.group_norm(x, self.num_groups, self.weight, self.bias, self.eps))
 
 
+SPLIT_ROWS = 4096        # rows per split-K chunk of a weight gradient
+SPLIT_MIN_ROWS = 16384   # below this the plain GEMM already fills the chip
+
+
+class _SplitKLinear(torch.autograd.Function):
+    """y = x W^T + b whose backward forms dW = dy^T x (and db = 1^T dy) split over row chunks:
+    one batched GEMM [k, out, 4096] x [k, 4096, in] + a sum over k.  At the per-step update's
+    65,536-row minibatches the library GEMM for dW (output 64 x 348, K = 65,536) runs on 12
+    workgroups of 256 CUs (~210 us); the batched form gives it k x the tiles.  db through the
+    same batched GEMM with a ones column (PyTorch's dim-0 column sum of a [65,536, 348] gradient
+    took ~170 us).  Float32 throughout; only the summation order differs from the plain GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = dy @ weight if ctx.needs_input_grad[0] else None
+        dw = db = None
+        n = x.shape[0]
+        k = n // SPLIT_ROWS
+        main = k * SPLIT_ROWS
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dyT = dy[:main].view(k, SPLIT_ROWS, -1).transpose(1, 2)          # [k, out, rows]
+        if ctx.needs_input_grad[1]:
+            dw = torch.bmm(dyT, x[:main].view(k, SPLIT_ROWS, -1)).sum(0)
+            if main < n:
+                dw = dw + dy[main:].t() @ x[main:]
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            ones = torch.ones(k, SPLIT_ROWS, 1, dtype=dy.dtype, device=dy.device)
+            db = torch.bmm(dyT, ones).sum(0).reshape(-1)
+            if main < n:
+                db = db + dy[main:].sum(0)
+        return dx, dw, db
+
+
+class Linear(nn.Linear):
+    """nn.Linear (same parameters and state_dict keys) whose weight / bias gradients are formed
+    split-K on large device batches (_SplitKLinear); otherwise exactly F.linear."""
+
+    def forward(self, x):
+        if (x.is_cuda and x.dim() == 2 and x.shape[0] >= SPLIT_MIN_ROWS and torch.is_grad_enabled()
+                and (self.weight.requires_grad or x.requires_grad)):
+            return _SplitKLinear.apply(x.contiguous(), self.weight, self.bias)
+        return F.linear(x, self.weight, self.bias)
+
+
 def hidden_block(in_features: int, out_features: int = 64, bias: bool = False):
     """[Linear, GroupNorm(8,64)+SiLU, Identity] — the reference's [Linear, GroupNorm, SiLU]."""
-    return [nn.Linear(in_features, out_features, bias=bias), GroupNormSiLU(8, 64), nn.Identity()]
+    return [Linear(in_features, out_features, bias=bias), GroupNormSiLU(8, 64), nn.Identity()]

@@ -23,6 +23,7 @@ constexpr int GN_C = 64, GN_G = 8, GN_GS = 8;       // channels, groups, group s
 constexpr int GN_THREADS = 256;                     // 32 rows x 8 groups per slab
 constexpr int GN_ROWS = GN_THREADS / GN_G;          // 32
 constexpr int GN_MAX_BLOCKS = 240;
+constexpr int GN_U = 4;                             // rows per thread per backward pass
 
 struct GnRow {
   float x[GN_GS];
@@ -93,11 +94,26 @@ __global__ __launch_bounds__(GN_THREADS) void gn_silu_bwd_kernel(
     accw[k] = 0.f;
     accb[k] = 0.f;
   }
-  for (int64_t row = (int64_t)blockIdx.x * GN_ROWS + rloc; row < N;
-       row += (int64_t)gridDim.x * GN_ROWS) {
-    float v[GN_GS], go[GN_GS];
-    gn_load(x + row * GN_C + c0, v);
-    gn_load(dout + row * GN_C + c0, go);
+  // GN_U rows per thread per pass, all loads issued first (at 240 workgroups of 4 waves, one
+  // row at a time left the kernel latency-bound at ~0.7 TB/s); rows stay in ascending order per
+  // thread, so the column sums are accumulated exactly as before
+  const int64_t stride = (int64_t)gridDim.x * GN_ROWS;
+  for (int64_t row0 = (int64_t)blockIdx.x * GN_ROWS + rloc; row0 < N; row0 += GN_U * stride) {
+    float vv[GN_U][GN_GS], gg[GN_U][GN_GS];
+#pragma unroll
+    for (int u = 0; u < GN_U; ++u) {
+      const int64_t row = row0 + u * stride;
+      if (row < N) {
+        gn_load(x + row * GN_C + c0, vv[u]);
+        gn_load(dout + row * GN_C + c0, gg[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < GN_U; ++u) {
+    const int64_t row = row0 + u * stride;
+    if (row >= N) break;
+    float* v = vv[u];
+    const float* go = gg[u];
     float mean, rstd;
     gn_stats(v, eps, mean, rstd);
     float xh[GN_GS], dxh[GN_GS];
@@ -122,6 +138,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_silu_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < GN_GS; ++k) v[k] = rstd * (dxh[k] - m1 - xh[k] * m2);
     gn_store(dx + row * GN_C + c0, v);
+    }
   }
   // column sums: rows of this block -> one partial per channel
 #pragma unroll

@@ -607,3 +607,29 @@ def test_gae_statistics_exact_size_workspace_every_tile_count():
             torch.testing.assert_close(sums, host, rtol=1e-12, atol=1e-9,
                                        msg=f"nt={nt} rep={rep}")
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("fin,fout,bias", [(348, 64, False), (348, 64, True), (64, 348, True)])
+def test_split_k_linear_grads_vs_float64(fin, fout, bias):
+    """PPO.layers.Linear on a large device batch (65,536 + 123 rows: 16 split-K chunks of 4,096
+    plus a remainder) gives the float64 input / weight / bias gradients of x W^T + b to float32
+    accumulation accuracy, and the same forward as F.linear (bit-exact)."""
+    from PPO.layers import Linear
+    torch.manual_seed(3)
+    N = 65536 + 123
+    lin = Linear(fin, fout, bias=bias).cuda()
+    x = torch.randn(N, fin, device="cuda", requires_grad=True)
+    dy = torch.randn(N, fout, device="cuda")
+    y = lin(x)
+    assert torch.equal(y.detach(), torch.nn.functional.linear(x.detach(), lin.weight.detach(),
+                                                            None if lin.bias is None else lin.bias.detach()))
+    y.backward(dy)
+    x64, dy64, w64 = x.detach().double().cpu(), dy.double().cpu(), lin.weight.detach().double().cpu()
+    gw = dy64.t() @ x64
+    gx = dy64 @ w64
+    torch.testing.assert_close(lin.weight.grad.double().cpu(), gw, rtol=0, atol=2e-5 * float(gw.abs().max()))
+    torch.testing.assert_close(x.grad.double().cpu(), gx, rtol=0, atol=2e-5 * float(gx.abs().max()))
+    if bias:
+        gb = dy64.sum(0)
+        torch.testing.assert_close(lin.bias.grad.double().cpu(), gb, rtol=0,
+                                   atol=2e-5 * float(dy64.abs().sum(0).max()))
