@@ -27,18 +27,51 @@ struct GatherArgs {
   int32_t count;
 };
 
+// 16-B copies (4 quads in flight per thread per pass) wherever the tensor's rows are 16-B
+// aligned, element copies otherwise; rows past nrows are zero-filled (the ragged last minibatch)
 __global__ __launch_bounds__(256) void gather_minibatch_kernel(GatherArgs a, const int64_t* cursor,
                                                                int64_t mb, int64_t nrows) {
   const int64_t base = cursor[0] * mb;
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int t = 0; t < a.count; ++t) {
     const int w = a.width[t];
     const int64_t total = mb * w;
     const float* src = a.src[t] + base * w;
     float* dst = a.dst[t];
     const int64_t limit = (nrows - base) * w;  // never read past the source
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x)
-      dst[i] = i < limit ? src[i] : 0.0f;
+    const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+    int64_t done = 0;
+    if (vec) {
+      const int64_t nq = total / 4;
+      const float4* s4 = reinterpret_cast<const float4*>(src);
+      float4* d4 = reinterpret_cast<float4*>(dst);
+      for (int64_t q0 = tid; q0 < nq; q0 += 4 * nthreads) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t q = q0 + u * nthreads;
+          if (q < nq) {
+            if (4 * q + 3 < limit) {
+              v[u] = s4[q];
+            } else {
+              const int64_t i = 4 * q;
+              v[u].x = i < limit ? src[i] : 0.0f;
+              v[u].y = i + 1 < limit ? src[i + 1] : 0.0f;
+              v[u].z = i + 2 < limit ? src[i + 2] : 0.0f;
+              v[u].w = i + 3 < limit ? src[i + 3] : 0.0f;
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t q = q0 + u * nthreads;
+          if (q < nq) d4[q] = v[u];
+        }
+      }
+      done = nq * 4;
+    }
+    for (int64_t i = done + tid; i < total; i += nthreads) dst[i] = i < limit ? src[i] : 0.0f;
   }
 }
 
@@ -108,7 +141,9 @@ extern "C" int prl_gather_minibatch(const float* const* srcs, float* const* dsts
     a.dst[t] = dsts[t];
     a.width[t] = widths[t];
   }
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(mb * 4, 256), 256);
+  int64_t widest = 1;
+  for (int t = 0; t < count; ++t) widest = std::max<int64_t>(widest, widths[t]);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(mb * widest, 4 * 256 * 4), 1024));
   hipLaunchKernelGGL(gather_minibatch_kernel, dim3(grid), dim3(256), 0, as_stream(stream), a,
                      cursor, mb, nrows);
   PRL_LAUNCH_CHECK("gather_minibatch");

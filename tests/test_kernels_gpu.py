@@ -633,3 +633,28 @@ def test_split_k_linear_grads_vs_float64(fin, fout, bias):
         gb = dy64.sum(0)
         torch.testing.assert_close(lin.bias.grad.double().cpu(), gb, rtol=0,
                                    atol=2e-5 * float(dy64.abs().sum(0).max()))
+
+
+@pytest.mark.parametrize("mb", [512, 4096 + 4])
+def test_gather_minibatch_every_cursor_bit_exact(mb):
+    """prl_gather_minibatch (graph-step input copy) for every minibatch index incl. the ragged
+    last one (zero-filled past the end): widths 1, 3, 348 (16-B rows), 5 (element path) and an
+    odd row offset, against torch slicing."""
+    import prl_native
+    g = torch.Generator(device="cuda").manual_seed(9)
+    nrows = 3 * mb + 37
+    widths = [1, 3, 348, 5]
+    srcs = [torch.randn(nrows, w, device="cuda", generator=g) if w > 1
+            else torch.randn(nrows, device="cuda", generator=g) for w in widths]
+    dsts = [torch.full((mb, w) if w > 1 else (mb,), float("nan"), device="cuda") for w in widths]
+    cursor = torch.zeros(1, dtype=torch.int64, device="cuda")
+    gat = prl_native.MinibatchGather(srcs, dsts, cursor, mb)
+    for j in range(-(-nrows // mb)):
+        cursor.fill_(j)
+        gat()
+        torch.cuda.synchronize()
+        for s_, d_ in zip(srcs, dsts):
+            ref = torch.zeros_like(d_)
+            part = s_[j * mb:(j + 1) * mb]
+            ref[:part.shape[0]] = part
+            assert torch.equal(d_, ref), (j, s_.shape)
