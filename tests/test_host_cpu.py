@@ -217,3 +217,30 @@ def test_kernel_bench_tool_imports():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert mod.CARTPOLE_STEP_BYTES == 111 and mod.GAE_BYTES_PER_TRANSITION == 20
+
+
+@pytest.mark.parametrize("n", [3 * 64, 3 * 64 + 5])
+def test_split_k_linear_function_vs_autograd(monkeypatch, n):
+    """PPO.layers._SplitKLinear (the large-batch Linear's split-K weight / bias gradient) is plain
+    torch code: on CPU tensors with 64-row chunks it gives F.linear's forward and autograd's
+    gradients in float64 (chunked sums, with and without a remainder)."""
+    from PPO import layers
+    monkeypatch.setattr(layers, "SPLIT_ROWS", 64)
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(n, 7, dtype=torch.float64, generator=g, requires_grad=True)
+    w = torch.randn(5, 7, dtype=torch.float64, generator=g, requires_grad=True)
+    b = torch.randn(5, dtype=torch.float64, generator=g, requires_grad=True)
+    dy = torch.randn(n, 5, dtype=torch.float64, generator=g)
+    y = layers._SplitKLinear.apply(x, w, b)
+    gx, gw, gb = torch.autograd.grad(y, (x, w, b), dy)
+    x2, w2, b2 = (t.detach().clone().requires_grad_() for t in (x, w, b))
+    y2 = torch.nn.functional.linear(x2, w2, b2)
+    rx, rw, rb = torch.autograd.grad(y2, (x2, w2, b2), dy)
+    assert torch.equal(y, y2)
+    torch.testing.assert_close(gx, rx, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(gw, rw, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(gb, rb, rtol=1e-12, atol=1e-12)
+    # no bias, weight only
+    y3 = layers._SplitKLinear.apply(x, w, None)
+    (gw3,) = torch.autograd.grad(y3, (w,), dy)
+    torch.testing.assert_close(gw3, rw, rtol=1e-12, atol=1e-12)
