@@ -1196,17 +1196,18 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
                               nmb0 + (int64_t)g * R, std::min(UPD_RT, nrows), nin);
     }
     if (t < 64) {
-      if (t == 0) {
-        upd_arrive(args.ctr, UPD_CTR_A, g);
-        // this step's AdamW bias corrections (float64 pow, as torch's AdamW), off the critical path
-        const double tstep = (double)step0 + (double)(s + 1);
-        const double bc1 = 1.0 - pow((double)args.beta1, tstep);
-        const double bc2 = 1.0 - pow((double)args.beta2, tstep);
-        s_adam[0] = (float)((double)args.lr / bc1);   // step size
-        s_adam[1] = (float)(1.0 / sqrt(bc2));         // 1 / sqrt(bias correction 2)
-      }
+      if (t == 0) upd_arrive(args.ctr, UPD_CTR_A, g);
       const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));
       if (t == 0) *s_abort = ok ? 0 : 1;
+    } else if (t == 64) {
+      // this step's AdamW bias corrections (float64 pow, as torch's AdamW) on the second wave,
+      // which only waits at the barrier: off the polling wave's path (for the last workgroup
+      // to arrive the poll ends at once, and its phase B gates every other workgroup)
+      const double tstep = (double)step0 + (double)(s + 1);
+      const double bc1 = 1.0 - pow((double)args.beta1, tstep);
+      const double bc2 = 1.0 - pow((double)args.beta2, tstep);
+      s_adam[0] = (float)((double)args.lr / bc1);   // step size
+      s_adam[1] = (float)(1.0 / sqrt(bc2));         // 1 / sqrt(bias correction 2)
     }
     __syncthreads();
     if (*s_abort) { dp_release(); return; }
