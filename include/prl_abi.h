@@ -270,9 +270,9 @@ int prl_ppo_grad_fold_step(const float* in_p, const float* in_m, const float* in
                            void* workspace, int64_t workspace_bytes, void* stream);
 /* The data-parallel loop of prl_ppo_update_dp as ONE persistent launch per rank (the world = 1
  * engine's structure, grid <= 128 workgroups): per step the launch reduces its gradient in-GPU
- * and raises a ready word; a second stream, enqueued here for all steps up front, waits for it
- * (hipStreamWaitValue32), all-reduces that step's buffer over the ranks (ncclAllReduce) and
- * raises a done word (hipStreamWriteValue32) that the launch waits for before clip + AdamW.
+ * and raises a ready word; a second stream, enqueued here for all steps up front, runs per step
+ * a one-lane gate kernel that waits for it, then ncclAllReduce of that step's buffer over the
+ * ranks; the next gate raises a done word that the launch waits for before clip + AdamW.
  * Same bits as prl_ppo_update_dp.  adam_step: device float (AdamW steps so far, advanced);
  * counts_dev: device copy of counts.  No reference counterpart (single-process reference);
  * replaces PPO.py:216-255 on data-parallel ranks. */

@@ -2170,8 +2170,8 @@ extern "C" int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, 
 
 // The data-parallel loop as ONE persistent launch per learn() (the world = 1 engine's structure):
 // per step the launch reduces its gradient in-GPU, raises dp_ready; a second stream, enqueued
-// here for every step up front, waits for that value (hipStreamWaitValue32), all-reduces the
-// buffer over the ranks (ncclAllReduce, RCCL over xGMI) and raises dp_done (hipStreamWriteValue32),
+// here for every step up front, waits for that value (dp_gate_kernel), all-reduces the buffer
+// over the ranks (ncclAllReduce, RCCL over xGMI) and raises dp_done (the next gate),
 // which the launch waits for before clip + AdamW.  The all-reduce runs on CUs the launch leaves
 // free (grid <= 128 workgroups).  Same bits as prl_ppo_update_dp (stepped).  adam_step: device
 // float, AdamW steps so far (advanced by the launch); counts_dev: device copy of counts.

@@ -500,7 +500,7 @@ def test_folded_step_equals_grad_then_adam(cont, D, A):
 @pytest.mark.parametrize("stand_in", ["0", "1"])
 def test_persistent_dp_launch_equals_python_loop(cont, stand_in, monkeypatch):
     """prl_ppo_update_dp_persistent (the data-parallel loop as ONE persistent launch; each step's
-    all-reduce on a second stream gated by hipStreamWaitValue32 / hipStreamWriteValue32) gives
+    all-reduce on a second stream behind one-lane gate kernels) gives
     the same bits as the stepped Python loop: parameters, both moments, step count and loss.
     stand_in = "1" runs a real kernel on the second stream in place of the (one-rank, launch-free)
     RCCL all-reduce, so a kernel executes beside the persistent launch on this one GPU."""
