@@ -377,6 +377,7 @@ def main():
         print(json.dumps(out), flush=True)
     if eng is not None:
         eng.events = None     # release the HIP events before interpreter teardown
+        eng.close()           # the engine's own RCCL communicator (world > 1)
     if world > 1:
         dist.destroy_process_group()
 

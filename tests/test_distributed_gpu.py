@@ -87,3 +87,36 @@ def test_two_ranks_graphed_equal_one_process_on_the_union(tmp_path, fused):
     assert p.last_graph_replays == k * nb - 2
     for key in ref:
         np.testing.assert_allclose(outs[0][key], ref[key], rtol=0, atol=2e-5, err_msg=key)
+
+
+def _nccl_one_rank_worker(port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = PATHS
+    torch.cuda.set_device(0)
+    torch.distributed.init_process_group("nccl", rank=0, world_size=1,
+                                         device_id=torch.device("cuda", 0))
+    p = _make_ppo(512, 2)
+    eng = p._fused_engine()
+    comm = eng.dp_comm()
+    ok = bool(comm)
+    eng.close()
+    ok = ok and not eng._comm and eng.dp_comm() is None
+    torch.distributed.destroy_process_group()
+    with open(os.path.join(out_dir, "ok"), "w") as f:
+        f.write("1" if ok else "0")
+
+
+def test_engine_rccl_communicator_build_and_close(tmp_path):
+    """On the nccl backend the engine builds its own RCCL communicator (one rank here) and
+    close() destroys it before destroy_process_group (bench.py's teardown order)."""
+    import random
+    port = 29700 + random.randint(0, 200)
+    ctx = mp.get_context("spawn")
+    proc = ctx.Process(target=_nccl_one_rank_worker, args=(port, str(tmp_path)))
+    proc.start()
+    proc.join(90)
+    if proc.is_alive():
+        proc.kill()
+        pytest.fail("one-rank nccl worker hung")
+    assert proc.exitcode == 0
+    assert (tmp_path / "ok").read_text() == "1"
