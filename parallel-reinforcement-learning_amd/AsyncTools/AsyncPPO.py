@@ -22,6 +22,7 @@ prl_flatten_env_major) and handed to ppo.memory as device tensors.  Any other du
 from __future__ import annotations
 
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -179,6 +180,8 @@ class AsyncPPO:  # AsyncPPO.py:104-165
             int(seed) * 0x9E3779B97F4A7C15 + 0x1234567) & (2**64 - 1)
         self._rollouts = 0
         self._evals = 0
+        self._warm = False      # one eager rollout first (warm-up before graph capture)
+        self._graph = None
         self._traj = None
         self.last_vector_steps = 0
 
@@ -213,7 +216,9 @@ class AsyncPPO:  # AsyncPPO.py:104-165
 
     def _device_rollout(self, seed):
         """One episode per env on the device (fused rollout step kernel per vector step, policy
-        on traj_obs[t]); returns the index of the last vector step taken."""
+        on traj_obs[t]); returns the index of the last vector step taken.  From the second
+        rollout of this runner on, one vector step (policy forward + rollout step kernel) is a
+        captured HIP graph replayed per step (PRL_ROLLOUT_GRAPH=0: eager launches)."""
         env, spec = self.env, self.env.spec
         E = self.num_envs
         if self._traj is None:
@@ -224,32 +229,83 @@ class AsyncPPO:  # AsyncPPO.py:104-165
         tr.active_after.zero_()
         tr.reward_sum.zero_()
         stream = torch.cuda.current_stream()
+        graph = None
+        if (self._warm and not getattr(self, "_graph_failed", False)
+                and os.environ.get("PRL_ROLLOUT_GRAPH", "1") != "0"):
+            graph = self._capture_step(seed, scaling)
         events = []
         checked = -1           # last step whose counter has been read
         finished = False
         k = 0
-        for k in range(tr.T):
-            dist = self.ppo.dist_params(tr.obs[k])
-            if dist.dtype != torch.float32 or not dist.is_contiguous():
-                dist = dist.float().contiguous()
-            prl_native.rollout_step(spec.kind, k, env.phys, env.t_elapsed, env.terminal, dist,
-                                    scaling, seed, tr.T, tr.obs, tr.act, tr.rew, tr.done,
-                                    tr.ep_len, tr.active_after, tr.reward_sum)
-            tr.pinned[k:k + 1].copy_(tr.active_after[k:k + 1], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            events.append(ev)
-            # poll completed steps without blocking; block only when too far ahead
-            while checked < k and (k - checked > self.poll_lag or events[checked + 1].query()):
-                events[checked + 1].synchronize()
-                checked += 1
-                if int(tr.pinned[checked]) == 0:
-                    finished = True
+        with torch.no_grad():
+            for k in range(tr.T):
+                if graph is not None:
+                    graph.replay()
+                else:
+                    self._vector_step(k, tr.obs[k], seed, scaling, tr.active_after)
+                tr.pinned[k:k + 1].copy_(tr.active_after[k:k + 1], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                events.append(ev)
+                # poll completed steps without blocking; block only when too far ahead
+                while checked < k and (k - checked > self.poll_lag or events[checked + 1].query()):
+                    events[checked + 1].synchronize()
+                    checked += 1
+                    if int(tr.pinned[checked]) == 0:
+                        finished = True
+                        break
+                if finished:
                     break
-            if finished:
-                break
+            if (not self._warm and not getattr(self, "_graph_failed", False)
+                    and os.environ.get("PRL_ROLLOUT_GRAPH", "1") != "0"):
+                # every env is terminal now: capture and replay the step once (a no-op for
+                # terminal envs) so the first capture's one-time cost (~85 ms at C2) falls in
+                # this warm-up rollout, not in the first graphed one
+                g = self._capture_step(seed, scaling)
+                if g is not None:
+                    g.replay()
+        self._warm = True
         self.last_vector_steps = k + 1
         return k
+
+    def _vector_step(self, k, obs, seed, scaling, active_after):
+        """Policy forward on this step's observations + the fused rollout step kernel."""
+        spec, env, tr = self.env.spec, self.env, self._traj
+        dist = self.ppo.dist_params(obs)
+        if dist.dtype != torch.float32 or not dist.is_contiguous():
+            dist = dist.float().contiguous()
+        prl_native.rollout_step(spec.kind, k, env.phys, env.t_elapsed, env.terminal, dist,
+                                scaling, seed, tr.T, tr.obs, tr.act, tr.rew, tr.done,
+                                tr.ep_len, active_after, tr.reward_sum)
+
+    def _capture_step(self, seed, scaling):
+        """One vector step as a HIP graph for this rollout's sampling key: the step index k lives
+        on the device (k_dev, advanced by the graph), the policy reads traj_obs[k_dev] through a
+        gather, the kernel counts the still-active envs into a scalar that the graph then
+        writes to active_after[k_dev].  Same kernels and arguments as the eager step, so the
+        same bits.  None if capture fails (eager launches then)."""
+        tr, E, D = self._traj, self.num_envs, self.env.spec.obs_dim
+        dev = tr.obs.device
+        if getattr(self, "_k_dev", None) is None:
+            self._k_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+            self._active_now = torch.zeros(1, dtype=torch.int32, device=dev)
+        k_dev, now = self._k_dev, self._active_now
+        self._graph = None
+        k_dev.zero_()
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.no_grad(), torch.cuda.graph(g):
+                obs = tr.obs.index_select(0, k_dev).view(E, D)
+                now.zero_()
+                self._vector_step(0, obs, seed, scaling, now)
+                tr.active_after.index_copy_(0, k_dev, now)
+                k_dev.add_(1)
+        except RuntimeError as e:   # e.g. a host sync inside a duck-typed policy
+            warnings.warn(f"rollout step not capturable ({e}); eager launches")
+            self._graph_failed = True
+            return None
+        self._graph = g
+        return g
 
     def _device_collect(self, k):
         env, spec, tr = self.env, self.env.spec, self._traj

@@ -314,3 +314,30 @@ def test_graphed_update_equals_eager_update(cont):
     for k in sd_e:
         torch.testing.assert_close(sd_g[k], sd_e[k], rtol=0, atol=0, msg=k)
     assert float(loss_g) == float(loss_e)
+
+
+@pytest.mark.parametrize("env,cont", [("CartPole-v1", False), ("Pendulum-v1", True)])
+def test_graphed_rollout_equals_eager_rollout(env, cont, monkeypatch):
+    """From the second rollout on, the device worker replays one captured HIP graph per vector
+    step (policy forward + rollout step kernel, step index on the device).  Three rollouts with a
+    real PPO policy: the graphed runner's memory and scores equal an eager runner's
+    (PRL_ROLLOUT_GRAPH=0) bit for bit."""
+    from AsyncTools.AsyncPPO import AsyncPPO
+    from PPO import PPO
+    outs = []
+    for graphed in ("1", "0"):
+        monkeypatch.setenv("PRL_ROLLOUT_GRAPH", graphed)
+        torch.manual_seed(0)
+        p = PPO(cont, 3 if cont else 4, 1 if cont else 2, action_scaling=2.0 if cont else None,
+                batch_size=10**9)
+        a = AsyncPPO(env, p, num_envs=3000, seed=5)
+        rec = []
+        for _ in range(3):
+            n = a.worker()
+            rec.append((n, float(a.reward_score)))   # (vector steps taken depend on poll timing)
+        assert (a._graph is not None) == (graphed == "1")
+        outs.append((rec, [x.cpu() for x in p.memory.device_tensors("cuda")]))
+    (r1, m1), (r0, m0) = outs
+    assert r1 == r0
+    for x, y in zip(m1, m0):
+        assert torch.equal(x, y)
