@@ -294,7 +294,9 @@ class AsyncPPO:  # AsyncPPO.py:104-165
         k_dev.zero_()
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.no_grad(), torch.cuda.graph(g):
+            # thread_local: other threads' HIP calls (e.g. the nccl process group's watchdog
+            # querying its events on data-parallel ranks) must not invalidate this capture
+            with torch.no_grad(), torch.cuda.graph(g, capture_error_mode="thread_local"):
                 obs = tr.obs.index_select(0, k_dev).view(E, D)
                 now.zero_()
                 self._vector_step(0, obs, seed, scaling, now)

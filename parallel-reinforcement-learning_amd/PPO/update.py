@@ -110,14 +110,15 @@ class GraphedUpdate:
             self.ppo.optimizer.zero_grad(set_to_none=True)
             self.graph = torch.cuda.CUDAGraph()
             if self.scales is None:
-                with torch.cuda.graph(self.graph):
+                with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                     self._forward_backward()
                     self._apply()
             else:
-                with torch.cuda.graph(self.graph):
+                with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                     self._forward_backward()
                 self.graph_b = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.graph_b, pool=self.graph.pool()):
+                with torch.cuda.graph(self.graph_b, pool=self.graph.pool(),
+                                      capture_error_mode="thread_local"):
                     self._apply()
         for _ in range(n_steps - done):
             self._replay()

@@ -101,6 +101,14 @@ def _nccl_one_rank_worker(port, out_dir):
     ok = bool(comm)
     eng.close()
     ok = ok and not eng._comm and eng.dp_comm() is None
+    # rollouts with the nccl process group (and its watchdog thread) alive: the vector-step
+    # graph is captured and replayed (thread-local capture mode)
+    from AsyncTools.AsyncPPO import AsyncPPO
+    a = AsyncPPO("CartPole-v1", p, num_envs=4096, seed=1)
+    for _ in range(3):
+        a.worker()
+    torch.cuda.synchronize()
+    ok = ok and a._graph is not None and not getattr(a, "_graph_failed", False)
     torch.distributed.destroy_process_group()
     with open(os.path.join(out_dir, "ok"), "w") as f:
         f.write("1" if ok else "0")
@@ -108,7 +116,8 @@ def _nccl_one_rank_worker(port, out_dir):
 
 def test_engine_rccl_communicator_build_and_close(tmp_path):
     """On the nccl backend the engine builds its own RCCL communicator (one rank here) and
-    close() destroys it before destroy_process_group (bench.py's teardown order)."""
+    close() destroys it before destroy_process_group (bench.py's teardown order); device-worker
+    rollouts capture and replay their vector-step graph with the process group alive."""
     import random
     port = 29700 + random.randint(0, 200)
     ctx = mp.get_context("spawn")
