@@ -286,6 +286,13 @@ int prl_ppo_update_dp_persistent(float* img_params, float* img_m, float* img_v, 
                                  float weight_decay, float max_norm, float* loss_out,
                                  void* workspace, int64_t workspace_bytes, void* comm,
                                  void* stream);
+/* Column sums out[c] = sum_r x[r][c] of a row-major f32 matrix (1 <= cols <= 1024): the bias
+ * gradient of a Linear over a large batch (nn.Linear backward, reached from PPO.py:249 /
+ * RND.py:112).  Two deterministic passes; `partial` holds prl_colsum_partial_floats(rows, cols)
+ * floats of scratch. */
+int64_t prl_colsum_partial_floats(int64_t rows, int32_t cols);
+int prl_colsum_f32(const float* x, int64_t rows, int32_t cols, float* out, float* partial,
+                   int64_t partial_floats, void* stream);
 /* Host call: device address of the u32 status words inside an engine workspace ([0] last
  * launch, [1] sticky timeout flag). */
 int prl_ppo_update_status_ptr(void* workspace, uint32_t** status);

@@ -58,9 +58,10 @@ class _SplitKLinear(torch.autograd.Function):
     """y = x W^T + b whose backward forms dW = dy^T x (and db = 1^T dy) split over row chunks:
     one batched GEMM [k, out, 4096] x [k, 4096, in] + a sum over k.  At the per-step update's
     65,536-row minibatches the library GEMM for dW (output 64 x 348, K = 65,536) runs on 12
-    workgroups of 256 CUs (~210 us); the batched form gives it k x the tiles.  db through the
-    same batched GEMM with a ones column (PyTorch's dim-0 column sum of a [65,536, 348] gradient
-    took ~170 us).  Float32 throughout; only the summation order differs from the plain GEMM."""
+    workgroups of 256 CUs (~210 us); the batched form gives it k x the tiles.  db on the device
+    by prl_colsum_f32 (PyTorch's dim-0 column sum of a [65,536, 348] gradient took ~170 us, a
+    batched GEMM with a ones column ~36 us); elsewhere through that batched GEMM.  Float32
+    throughout; only the summation order differs from the plain GEMM."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -84,10 +85,13 @@ class _SplitKLinear(torch.autograd.Function):
             if main < n:
                 dw = dw + dy[main:].t() @ x[main:]
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            ones = torch.ones(k, SPLIT_ROWS, 1, dtype=dy.dtype, device=dy.device)
-            db = torch.bmm(dyT, ones).sum(0).reshape(-1)
-            if main < n:
-                db = db + dy[main:].sum(0)
+            if dy.is_cuda and dy.dtype == torch.float32 and dy.shape[1] <= 1024:
+                db = prl_native.colsum(dy)       # deterministic two-pass HIP column sum
+            else:
+                ones = torch.ones(k, SPLIT_ROWS, 1, dtype=dy.dtype, device=dy.device)
+                db = torch.bmm(dyT, ones).sum(0).reshape(-1)
+                if main < n:
+                    db = db + dy[main:].sum(0)
         return dx, dw, db
 
 

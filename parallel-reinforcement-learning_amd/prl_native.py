@@ -67,6 +67,8 @@ SIGNATURES = {
     "prl_ppo_grad_step": [_P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I64, _F32, _F32,
                           _F32, _P, _P, _I64, _P],
     "prl_ppo_adam_step": [_P, _P, _P, _I32, _I32, _I32, _P, _I64] + [_F32] * 9 + [_P, _P],
+    "prl_colsum_partial_floats": [_I64, _I32],
+    "prl_colsum_f32": [_P, _I64, _I32, _P, _P, _I64, _P],
     "prl_ppo_update_dp_persistent": [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64,
                                      _I32, _I32, _I64, _P, _P] + [_F32] * 9 + [_P, _P, _I64, _P,
                                                                                _P],
@@ -74,7 +76,7 @@ SIGNATURES = {
                               + [_I64, _I32, _I64] + [_F32] * 10 + [_P, _P, _P, _I64, _P],
 }
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64,
-             "prl_ppo_image_floats": _I64}
+             "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
 
 _lib = None
 _lock = threading.Lock()
@@ -369,6 +371,19 @@ class MinibatchGather:
         _check(lib().prl_gather_minibatch(self.srcs, self.dsts, self.widths, self.n,
                                           _dev(self.cursor, torch.int64, "cursor"), self.mb,
                                           self.nrows, _stream()), "prl_gather_minibatch")
+
+
+def colsum(x: torch.Tensor) -> torch.Tensor:
+    """Column sums of a 2-D f32 device matrix (1^T x), deterministic (prl_colsum_f32)."""
+    rows, cols = x.shape
+    x = x.contiguous()
+    out = torch.empty(cols, dtype=torch.float32, device=x.device)
+    npart = int(lib().prl_colsum_partial_floats(int(rows), int(cols)))
+    part = torch.empty(max(npart, 1), dtype=torch.float32, device=x.device)
+    _check(lib().prl_colsum_f32(_dev(x, torch.float32, "x"), int(rows), int(cols),
+                                _dev(out, torch.float32, "out"), _dev(part, torch.float32, "part"),
+                                npart, _stream()), "prl_colsum_f32")
+    return out
 
 
 def categorical_fwd(probs, actions, logp, entropy=None):

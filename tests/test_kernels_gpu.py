@@ -658,3 +658,19 @@ def test_gather_minibatch_every_cursor_bit_exact(mb):
             part = s_[j * mb:(j + 1) * mb]
             ref[:part.shape[0]] = part
             assert torch.equal(d_, ref), (j, s_.shape)
+
+
+@pytest.mark.parametrize("rows,cols", [(0, 5), (1, 1), (65536 + 123, 1), (65536, 17), (1000, 64),
+                                       (65536, 348), (7, 1024)])
+def test_colsum_vs_float64_and_deterministic(rows, cols):
+    """prl_colsum_f32 (the large-batch Linear's bias gradient) against float64 column sums, and
+    bit-identical across two calls (fixed reduction order)."""
+    import prl_native
+    g = torch.Generator(device="cuda").manual_seed(rows + cols)
+    x = torch.randn(rows, cols, device="cuda", generator=g)
+    a = prl_native.colsum(x)
+    b = prl_native.colsum(x)
+    assert torch.equal(a, b)
+    ref = x.double().sum(0).cpu()
+    scale = x.double().abs().sum(0).cpu().clamp_min(1e-30)
+    assert float(((a.double().cpu() - ref).abs() / scale).max() if rows else a.abs().max()) < 1e-6
