@@ -286,7 +286,7 @@ int prl_ppo_update_dp_persistent(float* img_params, float* img_m, float* img_v, 
                                  float weight_decay, float max_norm, float* loss_out,
                                  void* workspace, int64_t workspace_bytes, void* comm,
                                  void* stream);
-/* Column sums out[c] = sum_r x[r][c] of a row-major f32 matrix (1 <= cols <= 1024): the bias
+/* Column sums out[c] = sum_r x[r][c] of a row-major f32 matrix (cols >= 1): the bias
  * gradient of a Linear over a large batch (nn.Linear backward, reached from PPO.py:249 /
  * RND.py:112).  Two deterministic passes; `partial` holds prl_colsum_partial_floats(rows, cols)
  * floats of scratch. */

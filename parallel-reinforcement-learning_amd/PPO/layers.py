@@ -85,7 +85,7 @@ class _SplitKLinear(torch.autograd.Function):
             if main < n:
                 dw = dw + dy[main:].t() @ x[main:]
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            if dy.is_cuda and dy.dtype == torch.float32 and dy.shape[1] <= 1024:
+            if dy.is_cuda and dy.dtype == torch.float32:
                 db = prl_native.colsum(dy)       # deterministic two-pass HIP column sum
             else:
                 ones = torch.ones(k, SPLIT_ROWS, 1, dtype=dy.dtype, device=dy.device)

@@ -125,53 +125,43 @@ __global__ __launch_bounds__(256) void categorical_bwd_kernel(const float* __res
 }
 
 // Column sums of a row-major [rows][cols] f32 matrix (the bias gradient 1^T dy of a Linear over
-// a large batch): pass 1, block b sums its contiguous row chunk into partial[b][cols] (each
-// iteration reads 256 consecutive floats: R = 256 / cols rows at a time for narrow matrices,
-// or one row in 256-column strides for wide ones), slots combined in LDS in a fixed order;
-// pass 2, the same kernel as one block over the partials.  Deterministic, graph-capturable.
+// a large batch).  Block (window, b) sums columns [W window, W window + W) over its contiguous
+// row chunk: W = cols (<= 64, 256 / W row slots) or 64 (4 row slots), so each sweep reads whole
+// 64-float row segments; the slots are combined in LDS in a fixed order into partial[b][cols].
+// Pass 2 is the same kernel over the [nblk][cols] partials with one row chunk.  Deterministic,
+// graph-capturable, and every thread loops over at most ~64 rows.
 constexpr int CS_THREADS = 256;
-constexpr int CS_MAXC = 4;   // columns per thread for cols > 256 (cols <= 1024)
+constexpr int CS_MAXBLK = 256;
+__host__ __device__ inline int cs_width(int cols) { return cols <= 64 ? cols : 64; }
 __global__ __launch_bounds__(CS_THREADS) void colsum_partial_kernel(const float* __restrict__ x,
                                                                     int64_t rows, int cols,
                                                                     int64_t chunk,
                                                                     float* __restrict__ partial) {
   __shared__ float s_acc[CS_THREADS];
-  const int t = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * chunk, r1 = std::min(rows, r0 + chunk);
-  if (cols <= CS_THREADS) {
-    const int R = CS_THREADS / cols, slot = t / cols, c = t % cols;
-    float acc = 0.f;
-    if (slot < R) {
+  const int t = threadIdx.x, W = cs_width(cols), slots = CS_THREADS / W;
+  const int slot = t / W, c = blockIdx.x * W + t % W;
+  const int64_t r0 = (int64_t)blockIdx.y * chunk, r1 = std::min(rows, r0 + chunk);
+  float acc = 0.f;
+  if (slot < slots && c < cols) {
 #pragma unroll 8
-      for (int64_t r = r0 + slot; r < r1; r += R) acc += x[r * cols + c];
-    }
-    s_acc[t] = acc;
-    __syncthreads();
-    if (t < cols) {
-      float sum = 0.f;
-      for (int k = 0; k < R; ++k) sum += s_acc[k * cols + t];
-      partial[(int64_t)blockIdx.x * cols + t] = sum;
-    }
-  } else {
-    float acc[CS_MAXC] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int64_t r = r0; r < r1; ++r)
-#pragma unroll
-      for (int k = 0; k < CS_MAXC; ++k) {
-        const int c = t + k * CS_THREADS;
-        if (c < cols) acc[k] += x[r * cols + c];
-      }
-#pragma unroll
-    for (int k = 0; k < CS_MAXC; ++k) {
-      const int c = t + k * CS_THREADS;
-      if (c < cols) partial[(int64_t)blockIdx.x * cols + c] = acc[k];
-    }
+    for (int64_t r = r0 + slot; r < r1; r += slots) acc += x[r * cols + c];
+  }
+  s_acc[t] = acc;
+  __syncthreads();
+  if (t < W && c < cols) {
+    float sum = 0.f;
+    for (int k = 0; k < slots; ++k) sum += s_acc[k * W + t];
+    partial[(int64_t)blockIdx.y * cols + c] = sum;
   }
 }
+inline int64_t colsum_chunk(int64_t rows, int cols) {
+  const int W = cs_width(cols);
+  int64_t chunk = std::max<int64_t>(CS_THREADS / W, (16384 + W - 1) / W);
+  if ((rows + chunk - 1) / chunk > CS_MAXBLK) chunk = (rows + CS_MAXBLK - 1) / CS_MAXBLK;
+  return chunk;
+}
 inline int colsum_blocks(int64_t rows, int cols) {
-  // about 16 K elements per block, at most 1024 blocks
-  const int64_t per = std::max<int64_t>(1, (16384 + cols - 1) / cols);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (rows + per - 1) / per));
+  return (int)std::max<int64_t>(1, (rows + colsum_chunk(rows, cols) - 1) / colsum_chunk(rows, cols));
 }
 
 }  // namespace prl
@@ -229,8 +219,7 @@ extern "C" int64_t prl_colsum_partial_floats(int64_t rows, int32_t cols) {
 
 extern "C" int prl_colsum_f32(const float* x, int64_t rows, int32_t cols, float* out,
                               float* partial, int64_t partial_floats, void* stream) {
-  PRL_REQUIRE(rows >= 0 && cols > 0 && cols <= CS_THREADS * CS_MAXC,
-              "prl_colsum_f32: cols must be 1..%d", CS_THREADS * CS_MAXC);
+  PRL_REQUIRE(rows >= 0 && cols > 0, "prl_colsum_f32: bad sizes");
   PRL_REQUIRE(out && (rows == 0 || (x && partial)), "prl_colsum_f32: null pointer");
   hipStream_t st = as_stream(stream);
   if (rows == 0) {
@@ -239,12 +228,12 @@ extern "C" int prl_colsum_f32(const float* x, int64_t rows, int32_t cols, float*
   }
   const int nblk = colsum_blocks(rows, cols);
   PRL_REQUIRE(partial_floats >= (int64_t)nblk * cols, "prl_colsum_f32: partial buffer too small");
-  const int64_t chunk = (rows + nblk - 1) / nblk;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3(nblk), dim3(CS_THREADS), 0, st, x, rows, (int)cols,
-                     chunk, partial);
+  const unsigned windows = (unsigned)cdiv((int64_t)cols, (int64_t)cs_width(cols));
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(windows, nblk), dim3(CS_THREADS), 0, st, x, rows,
+                     (int)cols, colsum_chunk(rows, cols), partial);
   PRL_LAUNCH_CHECK("colsum_partial");
-  // pass 2: the same kernel, one block over the [nblk][cols] partials (block order fixed)
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3(1), dim3(CS_THREADS), 0, st, partial,
+  // pass 2: the same kernel over the [nblk][cols] partials as one row chunk (block order fixed)
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(windows, 1), dim3(CS_THREADS), 0, st, partial,
                      (int64_t)nblk, (int)cols, (int64_t)nblk, out);
   PRL_LAUNCH_CHECK("colsum_fold");
   return PRL_OK;
