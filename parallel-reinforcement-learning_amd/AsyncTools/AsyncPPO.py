@@ -165,6 +165,18 @@ class DeviceTrajectory:
         self.pinned = torch.zeros(T, dtype=torch.int32, pin_memory=True)
 
 
+def sample_key(seed, rank=None):
+    """The Philox key of the in-kernel action sampling.  Under torch.distributed the rank is
+    mixed in (as EnvVectorizer.seed offsets the env seeds by rank * num_envs), so ranks given the
+    same seed draw independent exploration noise; rank 0 keeps the single-process key."""
+    if seed is None:
+        return int.from_bytes(os.urandom(8), "little")
+    if rank is None:
+        rank = _rank_world()[0]
+    key = (int(seed) * 0x9E3779B97F4A7C15 + 0x1234567) & (2**64 - 1)
+    return (key + rank * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+
+
 class AsyncPPO:  # AsyncPPO.py:104-165
     def __init__(self, env, ppo: object, num_envs: int = 32, steps: int = 100000, seed=None,
                  poll_lag: int = 4):
@@ -176,8 +188,7 @@ class AsyncPPO:  # AsyncPPO.py:104-165
         self.reward_score = np.array(0.0, dtype=np.float32)
         self.buffer = VecMemory(num_envs)
         self.poll_lag = poll_lag
-        self.sample_seed = int.from_bytes(os.urandom(8), "little") if seed is None else (
-            int(seed) * 0x9E3779B97F4A7C15 + 0x1234567) & (2**64 - 1)
+        self.sample_seed = sample_key(seed)
         self._rollouts = 0
         self._evals = 0
         self._warm = False      # one eager rollout first (warm-up before graph capture)

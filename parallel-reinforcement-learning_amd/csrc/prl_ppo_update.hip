@@ -1157,7 +1157,8 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     const int B = (int)std::min<int64_t>(args.mb, args.N - mb0);
     // DP: this rank's rows may be fewer than the union's (or none); scale by the union's rows
     const float invB = DP ? 1.0f / (float)args.counts[j] : 1.0f / (float)B;
-    const int myrows = std::max(0, std::min(R, B - g * R));
+    // profile mode 2 (PRL_UPD_PROFILE=2, diagnostics only): no rows, i.e. the exchange alone
+    const int myrows = args.profile == 2 ? 0 : std::max(0, std::min(R, B - g * R));
     const int64_t myrow0 = mb0 + (int64_t)g * R;
     // ---- phase A: partial gradient of this workgroup's rows ------------------------------------
     if (s == 0 && myrows > 0)
@@ -1647,9 +1648,9 @@ int upd_nq(const UpdNet& n) { return (int)cdiv(n.Lp / 4, upd_nt(n)); }
 // Specialisations for the configs' shapes (CartPole: discrete, A = 2; Pendulum: continuous,
 // A = 1); every other shape runs the generic (runtime head configuration) kernel.
 // PRL_UPD_PROFILE=1: the engine records workgroup 0's per-phase times (FusedUpdate.profile)
-bool upd_profile_enabled() {
+int upd_profile_enabled() {
   const char* e = getenv("PRL_UPD_PROFILE");
-  return e && e[0] == '1';
+  return e && e[0] == '1' ? 1 : (e && e[0] == '2' ? 2 : 0);
 }
 // PRL_UPD_GENERIC=1 routes every shape through the runtime-layout kernels (testing)
 bool upd_force_generic() {

@@ -128,8 +128,11 @@ __global__ __launch_bounds__(256) void categorical_bwd_kernel(const float* __res
 // a large batch).  Block (window, b) sums columns [W window, W window + W) over its contiguous
 // row chunk: W = cols (<= 64, 256 / W row slots) or 64 (4 row slots), so each sweep reads whole
 // 64-float row segments; the slots are combined in LDS in a fixed order into partial[b][cols].
-// Pass 2 is the same kernel over the [nblk][cols] partials with one row chunk.  Deterministic,
-// graph-capturable, and every thread loops over at most ~64 rows.
+// Pass 2 is the same kernel over the [nblk][cols] partials with one row chunk.  Deterministic and
+// graph-capturable.  Rows per thread in pass 1 = chunk / slots, chunk = max(slots, ceil(16384 / W))
+// grown to ceil(rows / 256) once more than 256 row chunks would be needed: 64 up to 65,536 rows
+// (cols > 64), max(64, rows / (256 slots)) beyond (rows = 2^20, cols = 348: 1,024); pass 2 loops
+// over at most 256 / slots partial rows per thread.
 constexpr int CS_THREADS = 256;
 constexpr int CS_MAXBLK = 256;
 __host__ __device__ inline int cs_width(int cols) { return cols <= 64 ? cols : 64; }

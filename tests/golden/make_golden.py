@@ -16,6 +16,10 @@ re-implemented here):
                advantages, per-minibatch surrogate inputs, the loss pieces and d loss/d logp,
                d loss/d V captured by autograd hooks, initial + final policy state_dict
   rnd.npz      RND.compute_intrinsic_reward (PPO/RND.py:71-94) for D in {4, 348}
+  learn_rnd.npz, learn_rnd_c5.npz
+               PPO.learn() with use_RND=True (PPO.py:157-178): the above plus the intrinsic
+               rewards, the RND state before and after update_pred; ckpt_<tag>/ holds the
+               reference's own save_weights() files (Policy_weights.pth, RND_weights.pth)
   worker.npz   AsyncPPO.worker (AsyncTools/AsyncPPO.py:117-146) over a scripted env: per-step
                envs_active masks, env-major memory, scores
   envs.npz     EnvVectorizer.reset/step (AsyncPPO.py:48-102) over gym_restated CartPole/Pendulum
@@ -31,6 +35,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import gym_restated  # noqa: E402
+from learn_inputs import digest, learn_inputs  # noqa: E402
 
 
 def import_reference(ref):
@@ -133,23 +138,33 @@ class _TorchProxy:
         return out
 
 
-def make_learn(torch, ppo_pkg, continuous=False, tag="learn", N=1500, mb=512, k_epochs=2):
+def make_learn(torch, ppo_pkg, continuous=False, tag="learn", N=1500, mb=512, k_epochs=2,
+               use_rnd=False, D=None, A=None, ckpt=False, store_inputs=True):
     ppo_mod = sys.modules["PPO.PPO"]  # the package re-exports the class under the same name
     torch.manual_seed(0)
-    D, A = (3, 1) if continuous else (4, 2)
+    if D is None:
+        D, A = (3, 1) if continuous else (4, 2)
     ppo = ppo_pkg.PPO(is_continuous=continuous, observ_dim=D, action_dim=A,
                       action_scaling=2.0 if continuous else None, lr=1e-3, k_epochs=k_epochs,
-                      policy_clip=0.2, GAE_lambda=0.95, gamma=0.995, batch_size=1024,
-                      mini_batch_size=mb)
-    rng = np.random.default_rng(7)
-    S = (rng.normal(0, 1, (N, D)) * 0.5).astype(np.float32)
-    if continuous:
-        Aa = np.tanh(rng.normal(0, 1, (N, A))).astype(np.float32) * 2.0
-    else:
-        Aa = (rng.random(N) < 0.5).astype(np.int64)
-    R = rng.normal(1.0, 0.5, N).astype(np.float32)
-    Dn = (rng.random(N) < 0.05)
-    Dn[-1] = True
+                      policy_clip=0.2, GAE_lambda=0.95, gamma=0.995, batch_size=min(1024, N),
+                      mini_batch_size=mb, use_RND=use_rnd, beta=0.001)
+    rnd_rec = {}
+    if use_rnd:   # PPO.learn's RND section (PPO.py:157-178): reward, then update_pred
+        rnd_rec["init"] = sd_to_np(ppo.rnd.state_dict())
+        orig_cir, orig_up = ppo.rnd.compute_intrinsic_reward, ppo.rnd.update_pred
+
+        def cir(values):
+            out = orig_cir(values)
+            rnd_rec["r_int"] = out.detach().cpu().numpy().copy()
+            return out
+
+        def up(values):
+            out = orig_up(values)
+            rnd_rec["after_update"] = sd_to_np(ppo.rnd.state_dict())
+            return out
+
+        ppo.rnd.compute_intrinsic_reward, ppo.rnd.update_pred = cir, up
+    S, Aa, R, Dn = learn_inputs(N, D, A, continuous)
     for i in range(N):
         ppo.memory.push(S[i], np.asarray(Aa[i]), np.float64(R[i]), np.asarray(Dn[i]))
     init_sd = sd_to_np(ppo.policy.state_dict())
@@ -205,8 +220,10 @@ def make_learn(torch, ppo_pkg, continuous=False, tag="learn", N=1500, mb=512, k_
     final_sd = sd_to_np(ppo.policy.state_dict())
 
     cat = lambda L: torch.cat(L).numpy()  # noqa: E731
-    out = {
-        "S": S, "A": Aa.astype(np.float32), "R": R, "Dn": Dn.astype(np.float32),
+    out = {"S": S, "A": Aa.astype(np.float32)} if store_inputs else {
+        "inputs_sha256": digest(S, Aa.astype(np.float32))}   # regenerate: learn_inputs.py
+    out.update({
+        "R": R, "Dn": Dn.astype(np.float32), "D": D, "A_dim": A, "continuous": int(continuous),
         "mb": mb, "k_epochs": k_epochs, "N": N,
         "old_logp": cat(rec["old_logp"]), "old_V": cat(rec["old_V"]),
         "returns": rec["gae_ret"][0], "adv_raw": rec["adv_raw"][0].numpy(),
@@ -218,12 +235,23 @@ def make_learn(torch, ppo_pkg, continuous=False, tag="learn", N=1500, mb=512, k_
         "step_sl1": torch.stack(rec["sl1"]).numpy(), "step_dlogp": cat(rec["dlogp"]),
         "step_dV": cat(rec["dV"]), "step_ret": cat(rec["sl1_in_R"]),
         "step_adv": cat(rec["adv_mb"]),
-    }
+    })
     for k, v in init_sd.items():
         out["init/" + k] = v
     for k, v in final_sd.items():
         out["final/" + k] = v
+    if use_rnd:
+        out["use_rnd"] = 1
+        out["r_int"] = rnd_rec["r_int"]
+        for k, v in rnd_rec["init"].items():
+            out["rnd_init/" + k] = v
+        for k, v in rnd_rec["after_update"].items():
+            out["rnd_final/" + k] = v
     np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **out)
+    if ckpt:   # the reference's own checkpoint files (PPO.save_weights, PPO.py:279-283)
+        d = os.path.join(HERE, f"ckpt_{tag}")
+        os.makedirs(d, exist_ok=True)
+        ppo.save_weights(d)
 
 
 # ------------------------------------------------------------------------------------ RND
@@ -365,15 +393,35 @@ def make_envs(apo):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="", help="comma-separated fixture names to (re)generate")
     args = ap.parse_args()
     torch, ppo_pkg, _, apo, utils = import_reference(args.ref)
     torch.set_num_threads(4)
-    make_gae(ppo_pkg)
-    make_learn(torch, ppo_pkg, continuous=False, tag="learn")
-    make_learn(torch, ppo_pkg, continuous=True, tag="learn_cont", N=1200, mb=256, k_epochs=1)
-    make_rnd(torch, ppo_pkg)
-    make_worker(apo, utils, ppo_pkg)
-    make_envs(apo)
+    jobs = {
+        "gae": lambda: make_gae(ppo_pkg),
+        "learn": lambda: make_learn(torch, ppo_pkg, continuous=False, tag="learn"),
+        "learn_cont": lambda: make_learn(torch, ppo_pkg, continuous=True, tag="learn_cont",
+                                         N=1200, mb=256, k_epochs=1),
+        # learn(use_RND=True): CartPole shapes (mb not dividing N), and C5's shapes (D 348,
+        # A 17, continuous) at a CPU-sized N; both also write the reference's save_weights()
+        "learn_rnd": lambda: make_learn(torch, ppo_pkg, continuous=False, tag="learn_rnd",
+                                        N=1100, mb=256, k_epochs=2, use_rnd=True, ckpt=True),
+        "learn_rnd_c5": lambda: make_learn(torch, ppo_pkg, continuous=True, tag="learn_rnd_c5",
+                                           N=700, mb=256, k_epochs=1, use_rnd=True, D=348,
+                                           A=17, ckpt=True),
+        # mini_batch >= layers.SPLIT_MIN_ROWS: the split-K weight gradients and the colsum bias
+        # gradients of the policy and of update_pred, end to end (inputs not stored: 28 MB)
+        "learn_rnd_big": lambda: make_learn(torch, ppo_pkg, continuous=True, tag="learn_rnd_big",
+                                            N=20000, mb=16384, k_epochs=1, use_rnd=True, D=348,
+                                            A=17, store_inputs=False),
+        "rnd": lambda: make_rnd(torch, ppo_pkg),
+        "worker": lambda: make_worker(apo, utils, ppo_pkg),
+        "envs": lambda: make_envs(apo),
+    }
+    only = [x for x in args.only.split(",") if x]
+    for name, job in jobs.items():
+        if not only or name in only:
+            job()
     import torch as _t
     with open(os.path.join(HERE, "VERSIONS.txt"), "w") as f:
         f.write(f"numpy {np.__version__}\ntorch {_t.__version__}\n"

@@ -129,3 +129,61 @@ def test_engine_rccl_communicator_build_and_close(tmp_path):
         pytest.fail("one-rank nccl worker hung")
     assert proc.exitcode == 0
     assert (tmp_path / "ok").read_text() == "1"
+
+
+def _config_worker(rank, world, port, cfg, out_dir):
+    """One rank of a BASELINE config's per-GPU shape: a device rollout of cfg['E'] envs (rank-
+    offset env seeds, rank-mixed sampling key), then learn() as data-parallel rank."""
+    sys.path[:0] = PATHS
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from AsyncTools.AsyncPPO import AsyncPPO
+        from PPO import PPO
+        torch.manual_seed(0)                      # same initial weights on every rank
+        p = PPO(cfg["cont"], cfg["D"], cfg["A"], action_scaling=1.0 if cfg["cont"] else None,
+                lr=1e-3, k_epochs=cfg["k"], batch_size=1, mini_batch_size=cfg["mb"],
+                use_RND=cfg["rnd"])
+        p.show_progress = False
+        a = AsyncPPO(cfg["env"], p, num_envs=cfg["E"], seed=7)   # same seed: rank offsets apply
+        a.worker()
+        S = p.memory.device_tensors("cuda")[0]
+        n = S.shape[0]
+        head = S[:64].cpu().numpy()
+        p.learn()
+        torch.cuda.synchronize()
+        sd = {kk: v.cpu().numpy() for kk, v in p.policy.state_dict().items()}
+        if cfg["rnd"]:
+            sd.update({"rnd." + kk: v.cpu().numpy() for kk, v in p.rnd.state_dict().items()})
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **sd, _n=np.int64(n), _head=head,
+                 _key=np.uint64(a.sample_seed), _loss=np.float32(p.last_loss.item()),
+                 _path=np.array(p.last_update_path))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+# BASELINE.json configs[3] (C4: CartPole, 65,536 envs per rank) and configs[4] (C5: synthetic
+# D 348 / A 17 + RND, 16,384 envs per rank), on 2 ranks sharing cuda:0, k_epochs 1
+C4 = dict(env="CartPole-v1", E=65536, cont=False, D=4, A=2, mb=512, k=1, rnd=False)
+C5 = dict(env="SyntheticHumanoid-v0", E=16384, cont=True, D=348, A=17, mb=65536, k=1, rnd=True)
+
+
+@pytest.mark.parametrize("name,cfg", [("c4", C4), ("c5", C5)])
+def test_two_ranks_at_config_per_rank_shape(tmp_path, name, cfg):
+    """C4 / C5 per-rank shapes end to end on 2 ranks: independent rollouts (different envs and
+    sampling keys per rank), one data-parallel learn() (C4: stepped engine + all-reduce per
+    step; C5: graphed per-step path + RND update_pred with its gradient all-reduced); both ranks
+    end with bit-identical policy (and predictor) weights and finite losses."""
+    import random
+    port = 29800 + random.randint(0, 150)
+    mp.spawn(_config_worker, args=(2, port, cfg, str(tmp_path)), nprocs=2, join=True)
+    outs = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(2)]
+    assert int(outs[0]["_key"]) != int(outs[1]["_key"])              # rank-mixed sampling keys
+    assert not np.array_equal(outs[0]["_head"], outs[1]["_head"])    # different rollouts
+    assert min(int(o["_n"]) for o in outs) >= cfg["E"]               # >= one step per env
+    assert str(outs[0]["_path"]) == ("fused-dp" if name == "c4" else "graph")
+    for key in outs[0].files:
+        if not key.startswith("_"):
+            np.testing.assert_array_equal(outs[0][key], outs[1][key], err_msg=key)
+    assert all(np.isfinite(o["_loss"]) for o in outs)   # each rank reports its own rows

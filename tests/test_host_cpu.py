@@ -244,3 +244,37 @@ def test_split_k_linear_function_vs_autograd(monkeypatch, n):
     y3 = layers._SplitKLinear.apply(x, w, None)
     (gw3,) = torch.autograd.grad(y3, (w,), dy)
     torch.testing.assert_close(gw3, rw, rtol=1e-12, atol=1e-12)
+
+
+def test_sample_key_mixes_rank():
+    """data-parallel ranks given the same seed must not share the sampling key; rank 0
+    keeps the single-process key (so 1-rank results are unchanged)."""
+    from AsyncTools.AsyncPPO import sample_key
+    k0 = sample_key(123, rank=0)
+    assert k0 == sample_key(123)            # no process group: rank 0
+    keys = {sample_key(123, rank=r) for r in range(8)}
+    assert len(keys) == 8 and all(0 <= k < 2**64 for k in keys)
+    assert sample_key(124, rank=0) != k0
+
+
+@pytest.mark.parametrize("tag", ["learn_rnd", "learn_rnd_c5"])
+def test_checkpoint_files_match_reference_format(tmp_path, tag):
+    """§8 f3 on the CPU: the reference's save_weights() files (weights_only loads) and ours carry
+    the same keys, shapes and dtypes, for the policy and for RND."""
+    import os
+    from PPO import PPO
+    ref_dir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"ckpt_{tag}")
+    cont, D, A = (False, 4, 2) if tag == "learn_rnd" else (True, 348, 17)
+    p = PPO(cont, D, A, action_scaling=2.0 if cont else None, use_RND=True)
+    p.save_weights(str(tmp_path))
+    for name in ("Policy_weights.pth", "RND_weights.pth"):
+        ref = torch.load(os.path.join(ref_dir, name), weights_only=True)
+        ours = torch.load(os.path.join(str(tmp_path), name), weights_only=True)
+        assert list(ref) == list(ours), name
+        for k in ref:
+            assert ref[k].shape == ours[k].shape and ref[k].dtype == ours[k].dtype, (name, k)
+    q = PPO(cont, D, A, action_scaling=2.0 if cont else None, use_RND=True)
+    q.load_weights(ref_dir)                 # the reference's files load into ours (CPU)
+    ref = torch.load(os.path.join(ref_dir, "Policy_weights.pth"), weights_only=True)
+    for k, v in q.policy.state_dict().items():
+        assert torch.equal(v.cpu(), ref[k])

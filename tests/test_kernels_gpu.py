@@ -661,7 +661,7 @@ def test_gather_minibatch_every_cursor_bit_exact(mb):
 
 
 @pytest.mark.parametrize("rows,cols", [(0, 5), (1, 1), (65536 + 123, 1), (65536, 17), (1000, 64),
-                                       (65536, 348), (7, 1024)])
+                                       (65536, 348), (7, 1024), (1 << 20, 348)])
 def test_colsum_vs_float64_and_deterministic(rows, cols):
     """prl_colsum_f32 (the large-batch Linear's bias gradient) against float64 column sums, and
     bit-identical across two calls (fixed reduction order)."""

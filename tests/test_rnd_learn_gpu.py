@@ -1,0 +1,144 @@
+"""PPO.learn(use_RND=True) on the GPU against the reference's own learn():
+tests/golden/learn_rnd*.npz were written by tests/golden/make_golden.py from the reference's
+PPO.learn with use_RND=True (PPO/PPO.py:157-178, PPO/RND.py:71-115).
+
+Checked, from the same initial policy / RND weights and the same memory:
+  * the intrinsic rewards (HIP prl_rnd_forward)            1e-5 relative
+  * the GAE returns on rewards + r_int (HIP prl_gae)        1e-5 relative (+1e-5 absolute guard)
+  * the normalised advantages (HIP prl_adv_normalize)       1e-5 relative (+1e-5 absolute guard)
+  * the predictor after update_pred (PyTorch + HIP GN/colsum backward) and the updated policy
+    (fused engine or graphed per-step path): absolute tolerances per case below.
+The C5-shaped cases (D = 348, A = 17, continuous) run the graphed per-step path (the fused engine
+covers D <= 64); learn_rnd_big's mini_batch of 16,384 puts the policy's and the predictor's
+Linear backward on the split-K + colsum path (layers.SPLIT_MIN_ROWS).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+from learn_inputs import digest, learn_inputs  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+# absolute tolerances on the weights after learn(), per fixture: (policy, RND predictor).
+# CartPole shapes: 2e-6 (measured 1.8e-7 fused / 4.8e-7 graph; predictor 1.5e-8).  D = 348: the
+# float32 GEMMs reduce over K = 348 (and the split-K chunks over 4,096 rows) in another order
+# than the reference's CPU GEMMs; AdamW's per-element steps (~lr = 1e-3) turn those ~1e-6
+# relative gradient differences into |dw| of a few 1e-6 over 1-2 steps (measured 5.1e-6 policy,
+# 1.3e-6 predictor on learn_rnd_c5): 1e-5 / 5e-6, i.e. <= 1 % of the step size.  learn_rnd_big
+# (mini_batch 16,384: 17-dim Gaussian log-probs of random actions reach |logp| ~ 1e2, whose float32
+# rounding alone moves each ratio by ~1e-5) measured 2.5e-5 on the policy after its
+# 2 steps (1.2 % of the 2e-3 the steps move a weight) and 8.6e-7 on the predictor: 5e-5 / 5e-6.
+WEIGHT_ATOL = {"learn_rnd": (2e-6, 2e-6), "learn_rnd_c5": (1e-5, 5e-6), "learn_rnd_big": (5e-5, 5e-6)}
+
+
+def _sub(g, prefix):
+    return {k[len(prefix):]: torch.from_numpy(np.array(g[k])) for k in g.files if k.startswith(prefix)}
+
+
+def _inputs(g):
+    cont = bool(int(g["continuous"]))
+    if "S" in g.files:
+        return g["S"], g["A"]
+    S, A, _, _ = learn_inputs(int(g["N"]), int(g["D"]), int(g["A_dim"]), cont)
+    A = A.astype(np.float32)
+    assert digest(S, A) == str(g["inputs_sha256"]), "learn_inputs() no longer reproduces the fixture"
+    return S, A
+
+
+def _ppo_from_fixture(g, path):
+    from PPO import PPO
+    cont = bool(int(g["continuous"]))
+    N = int(g["N"])
+    p = PPO(is_continuous=cont, observ_dim=int(g["D"]), action_dim=int(g["A_dim"]),
+            action_scaling=2.0 if cont else None, lr=1e-3, k_epochs=int(g["k_epochs"]),
+            policy_clip=0.2, GAE_lambda=0.95, gamma=0.995, batch_size=min(1024, N),
+            mini_batch_size=int(g["mb"]), use_RND=True, beta=0.001)
+    p.show_progress = False
+    p.use_fused = path == "fused"
+    init = _sub(g, "init/")
+    p.policy.load_state_dict(init)
+    p.policy_old.load_state_dict(init)
+    p.rnd.load_state_dict(_sub(g, "rnd_init/"))
+    S, A = _inputs(g)
+    for i in range(N):
+        p.memory.push(S[i], A[i] if cont else np.asarray(A[i]), g["R"][i], g["Dn"][i])
+    return p
+
+
+def _close(got, ref, rtol, atol, what):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(got - ref) - (rtol * np.abs(ref) + atol)
+    assert float(err.max()) <= 0.0, f"{what}: worst excess {err.max():.3e}"
+
+
+def _max_abs(a, b):
+    return float(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)).max())
+
+
+@pytest.mark.parametrize("tag,path", [("learn_rnd", "fused"), ("learn_rnd", "graph"),
+                                      ("learn_rnd_c5", "graph"), ("learn_rnd_big", "graph")])
+def test_learn_with_rnd_matches_reference_learn(golden, tag, path):
+    g = golden(tag)
+    p = _ppo_from_fixture(g, path)
+    rec = {}
+    orig = p.rnd.compute_intrinsic_reward
+
+    def cir(values):
+        out = orig(values)
+        rec["r_int"] = out.detach().clone()
+        return out
+
+    p.rnd.compute_intrinsic_reward = cir
+    p.learn()
+    torch.cuda.synchronize()
+    assert p.last_update_path == path and len(p.memory) == 0
+    _close(rec["r_int"].cpu().numpy(), g["r_int"], 1e-5, 1e-9, "intrinsic reward")
+    _, _, _, adv, returns = p._last_update_inputs
+    _close(returns.cpu().numpy(), g["returns"], 1e-5, 1e-5, "GAE returns")
+    _close(adv.cpu().numpy(), g["adv"], 1e-5, 1e-5, "normalised advantages")
+    pol_atol, rnd_atol = WEIGHT_ATOL[tag]
+    sd, ref = p.rnd.state_dict(), _sub(g, "rnd_final/")
+    worst_rnd = max(_max_abs(sd[k].cpu(), ref[k]) for k in ref)
+    sd, ref = p.policy.state_dict(), _sub(g, "final/")
+    worst_pol = max(_max_abs(sd[k].cpu(), ref[k]) for k in ref)
+    print(f"{tag}/{path}: max |policy - ref| {worst_pol:.3e}, max |predictor - ref| {worst_rnd:.3e}")
+    assert worst_rnd <= rnd_atol and worst_pol <= pol_atol, (worst_pol, worst_rnd)
+    old = p.policy_old.state_dict()
+    for k, v in p.policy.state_dict().items():
+        assert torch.equal(old[k], v)
+
+
+@pytest.mark.parametrize("tag", ["learn_rnd", "learn_rnd_c5"])
+def test_load_reference_checkpoint_then_learn(golden, tag):
+    """§8 f3: the reference's own save_weights() files (tests/golden/ckpt_<tag>/, written by its
+    PPO.save_weights after learn) load into our PPO (torch.load weights_only=True), give exactly
+    the reference's post-learn weights, and a GPU learn() continues from them."""
+    g = golden(tag)
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"ckpt_{tag}")
+    p = _ppo_from_fixture(g, "fused" if tag == "learn_rnd" else "graph")
+    p.load_weights(d)
+    for k, v in _sub(g, "final/").items():
+        assert torch.equal(p.policy.state_dict()[k].cpu(), v), k
+        assert torch.equal(p.policy_old.state_dict()[k].cpu(), v), k
+    for k, v in _sub(g, "rnd_final/").items():
+        assert torch.equal(p.rnd.state_dict()[k].cpu(), v), k
+    before = {k: v.clone() for k, v in p.policy.state_dict().items()}
+    p.learn()
+    torch.cuda.synchronize()
+    assert torch.isfinite(p.last_loss).item()
+    moved = max(float((p.policy.state_dict()[k] - before[k]).abs().max()) for k in before)
+    assert 0.0 < moved < 1.0
+    # and our own save_weights() round-trips through the reference's file names
+    import tempfile
+    with tempfile.TemporaryDirectory() as tmp:
+        p.save_weights(tmp)
+        assert sorted(os.listdir(tmp)) == ["Policy_weights.pth", "RND_weights.pth"]
+        sd = torch.load(os.path.join(tmp, "Policy_weights.pth"), weights_only=True)
+        for k, v in p.policy.state_dict().items():
+            assert torch.equal(sd[k].to(v.device), v)

@@ -14,8 +14,9 @@ from learn_bench import synthetic_batch  # noqa: E402
 from PPO import PPO  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+MBS = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else (512, 2048, 65536)
 batch = synthetic_batch(N)
-for mb in (512, 2048, 65536):
+for mb in MBS:
     for k in (11,):
         torch.manual_seed(0)
         p = PPO(False, 4, 2, lr=1e-3, k_epochs=k, batch_size=1, mini_batch_size=mb)
