@@ -11,7 +11,7 @@
 // Why one kernel: at the reference's mini_batch_size = 512 a step is ~25 MFLOP spread over ~50
 // tiny kernels; the graph-replayed PyTorch step costs ~180 us, almost all launch gaps.
 //
-// Decomposition (G workgroups of 256 threads, one per CU, co-resident: cooperative launch):
+// Decomposition (G workgroups of 256 threads, one per CU, co-resident: occupancy-checked plain launch):
 //   phase A  workgroup g takes rows [g*R, (g+1)*R) of the step's minibatch in chunks of RC = 8
 //            rows; forward + backward run out of LDS with the CURRENT parameters in LDS (every
 //            workgroup holds a full, bit-identical copy), accumulating this workgroup's partial
@@ -1688,6 +1688,23 @@ const void* upd_eval_kernel_for(const UpdNet& n) {
 
 int upd_grid(int64_t mb) { return (int)std::min<int64_t>(256, cdiv(mb, UPD_RT)); }
 
+// The persistent kernels need all G workgroups resident at once (they hand data to each other).
+// A plain launch gives the same residency as a cooperative one (MI355X_MICROARCH.md,
+// coop-launch); what the cooperative API adds is this check, ~15-19 us of host time per launch,
+// and, under rocprofv3's kernel tracing, a SIGSEGV inside exit() at process teardown (round 1's
+// profiled bench; tools/teardown_probe.sh isolates it to the cooperative launch).  So: check the
+// occupancy ourselves, then launch plainly.
+hipError_t upd_launch_resident(const void* kern, int G, int threads, size_t lds, void** kargs,
+                               hipStream_t st) {
+  int per_cu = 0, dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds);
+  if (e != hipSuccess) return e;
+  if ((int64_t)per_cu * cus < G) return hipErrorCooperativeLaunchTooLarge;
+  return hipLaunchKernel(kern, dim3(G), dim3(threads), kargs, lds, st);
+}
+
 size_t upd_lds_bytes(const UpdNet& n) {
   return sizeof(float) * (size_t)(UPD_HDR + 2 * n.Lp + 4 + ((upd_scratch_floats(n.D, upd_nw_host(n)) + 3) & ~3));
 }
@@ -1812,7 +1829,7 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
   hipLaunchKernelGGL(ppo_image_kernel, dim3(img_grid), dim3(UPD_THREADS), 0, st, args.net, params,
                      exp_avg, exp_avg_sq, img_p, img_m, img_v, 1);
   PRL_LAUNCH_CHECK("ppo_image");
-  PRL_HIP_TRY(hipLaunchCooperativeKernel(kern, dim3(G), dim3(upd_nt(args.net)), kargs, (unsigned)lds, st));
+  PRL_HIP_TRY(upd_launch_resident(kern, G, upd_nt(args.net), lds, kargs, st));
   hipLaunchKernelGGL(ppo_image_kernel, dim3(img_grid), dim3(UPD_THREADS), 0, st, args.net, params,
                      exp_avg, exp_avg_sq, img_p, img_m, img_v, 0);
   PRL_LAUNCH_CHECK("ppo_image");
@@ -2299,7 +2316,7 @@ extern "C" int prl_ppo_update_dp_persistent(float* img_params, float* img_m, flo
   PRL_RCCL_TRY(g_rccl.all_reduce(ws.red2, ws.red2, count, ncclFloat32, ncclSum, c, st), "ncclAllReduce");
   PRL_HIP_TRY(hipEventRecord(g_dp_ev[0], st));
   void* kargs[] = {&args};
-  PRL_HIP_TRY(hipLaunchCooperativeKernel(kern, dim3(G), dim3(upd_nt(args.net)), kargs, (unsigned)lds, st));
+  PRL_HIP_TRY(upd_launch_resident(kern, G, upd_nt(args.net), lds, kargs, st));
   PRL_HIP_TRY(hipStreamWaitEvent(g_dp_stream, g_dp_ev[0], 0));
   const bool stand_in = dp_stand_in();
   for (int64_t s = 0; s < total; ++s) {

@@ -5,7 +5,7 @@ PPO.learn with use_RND=True (PPO/PPO.py:157-178, PPO/RND.py:71-115).
 Checked, from the same initial policy / RND weights and the same memory:
   * the intrinsic rewards (HIP prl_rnd_forward)            1e-5 relative
   * the GAE returns on rewards + r_int (HIP prl_gae)        1e-5 relative (+1e-5 absolute guard)
-  * the normalised advantages (HIP prl_adv_normalize)       1e-5 relative (+1e-5 absolute guard)
+  * the normalised advantages (HIP prl_adv_normalize)       1e-5 relative (+1e-6 absolute guard)
   * the predictor after update_pred (PyTorch + HIP GN/colsum backward) and the updated policy
     (fused engine or graphed per-step path): absolute tolerances per case below.
 The C5-shaped cases (D = 348, A = 17, continuous) run the graphed per-step path (the fused engine
@@ -101,7 +101,7 @@ def test_learn_with_rnd_matches_reference_learn(golden, tag, path):
     _close(rec["r_int"].cpu().numpy(), g["r_int"], 1e-5, 1e-9, "intrinsic reward")
     _, _, _, adv, returns = p._last_update_inputs
     _close(returns.cpu().numpy(), g["returns"], 1e-5, 1e-5, "GAE returns")
-    _close(adv.cpu().numpy(), g["adv"], 1e-5, 1e-5, "normalised advantages")
+    _close(adv.cpu().numpy(), g["adv"], 1e-5, 1e-6, "normalised advantages")
     pol_atol, rnd_atol = WEIGHT_ATOL[tag]
     sd, ref = p.rnd.state_dict(), _sub(g, "rnd_final/")
     worst_rnd = max(_max_abs(sd[k].cpu(), ref[k]) for k in ref)

@@ -11,18 +11,7 @@ BENCH="bench.py ${BENCH_ARGS:-}"
 step bench 600 python $BENCH --dump-gae /tmp/gae_inputs.pt
 tail -1 $O/bench.log
 N=$(python -c "import torch; print(torch.load('/tmp/gae_inputs.pt', weights_only=True)['V'].numel())")
-# the profiled python process may segfault at interpreter teardown AFTER rocprofv3 has written
-# its output ("tool finalization" logged): accept exactly that case, nothing else
-timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o bench --output-format csv -- python $BENCH --no-cpu-baseline > "$O/prof_bench.log" 2>&1; rc=$?
-echo "[prof_bench] rc=$rc"
-if [ $rc -ne 0 ]; then
-  if [ $rc -eq 139 ] && grep -q "tool finalization" "$O/prof_bench.log" && [ -s $O/prof_bench/bench_kernel_stats.csv ] \
-     && grep -q '"metric"' "$O/prof_bench.log"; then
-    echo "[prof_bench] segfault at teardown after profiler finalization: output complete, continuing"
-  else
-    tail -5 "$O/prof_bench.log"; exit $rc
-  fi
-fi
+step prof_bench 900 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o bench --output-format csv -- python $BENCH --no-cpu-baseline
 grep '"metric"' $O/prof_bench.log | tail -1 > $O/bench_under_rocprof.json
 step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o fetch --output-format csv -- python tools/kernel_bench.py --gae-file /tmp/gae_inputs.pt --reps 3
 step pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o write --output-format csv -- python tools/kernel_bench.py --gae-file /tmp/gae_inputs.pt --reps 3
