@@ -134,6 +134,40 @@ def env_at_scale(env_name, spec, scaling, bpe, E=1 << 22):
             "frac": round(ach / HBM_PEAK_GBS, 4), "cache": "cold (512 MiB read-only flush)"}
 
 
+def learn_fixed(spec, cfg, mbs=(512, 65536), N=1 << 20, k_epochs=11):
+    """PPO.learn() on SURVEY.md section 8d's FIXED synthetic memory (N = 2^20 CartPole-shaped
+    transitions: S ~ 0.05 N(0,1), A ~ Bernoulli(1/2), r = 1, d ~ Bernoulli(0.05), last d = 1,
+    numpy default_rng(0)), k_epochs 11, at the reference's mini_batch 512 and at 65,536: unlike
+    the iteration above (whose learn batch grows as the policy learns to balance), this number
+    is comparable across runs and rounds.  Wall time of one learn() after a warm-up learn()."""
+    from PPO import PPO
+    rng = np.random.default_rng(0)
+    S = (0.05 * rng.normal(size=(N, 4))).astype(np.float32)
+    A = (rng.random(N) < 0.5).astype(np.float32)
+    R = np.ones(N, np.float32)
+    D = (rng.random(N) < 0.05).astype(np.float32)
+    D[-1] = 1
+    batch = [torch.from_numpy(x).cuda() for x in (S, A, R, D)]
+    out = {"N": N, "k_epochs": k_epochs, "data": "fixed synthetic (SURVEY.md 8d), default_rng(0)"}
+    for mb in mbs:
+        torch.manual_seed(0)
+        p = PPO(False, 4, 2, lr=1e-3, k_epochs=k_epochs, batch_size=1, mini_batch_size=mb)
+        p.show_progress = False
+        times = []
+        for _ in range(2):
+            p.memory.push_device(*batch)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            p.learn()
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        steps = k_epochs * -(-N // mb)
+        out[f"mb{mb}"] = {"learn_ms": round(times[-1] * 1e3, 1), "optimizer_steps": steps,
+                          "us_per_optimizer_step": round(times[-1] / steps * 1e6, 2),
+                          "path": p.last_update_path}
+    return out
+
+
 def pmc_traffic(n):
     """HBM bytes per GAE launch from the committed PMC summary (profiles/*gae_pmc.json, written by
     tools/gpu_benchprof.sh: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the same
@@ -159,7 +193,10 @@ def main():
     ap.add_argument("--mb", type=int, default=None)
     ap.add_argument("--k-epochs", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-envs", type=int, default=8192)
+    ap.add_argument("--no-learn-fixed", action="store_true",
+                    help="skip learn() on the fixed synthetic 2^20 memory (learn_fixed_2p20)")
+    ap.add_argument("--cpu-envs", type=int, default=8192,
+                    help="num_envs of the CPU baseline's sample iteration (~20 s of host work)")
     ap.add_argument("--no-env-scale", action="store_true",
                     help="skip the rollout-step kernel's 2^22-env re-timing (roofline_env.at_scale)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -336,19 +373,35 @@ def main():
         if not args.no_env_scale:
             roofline_env["at_scale"] = env_at_scale(cfg["env"], spec_, scaling, bpe)
 
+    fixed = None
+    if rank == 0 and world == 1 and args.config == "c2" and not args.no_learn_fixed:
+        fixed = learn_fixed(spec, cfg)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["env"] == "CartPole-v1":
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cpu_port
-        n_cpu, tr, tl, threads = cpu_port.cpu_iteration(E=args.cpu_envs, mb=cfg["mb"],
-                                                        k_epochs=cfg["k_epochs"])
-        cpu = {"value": round(n_cpu / (tr + tl), 1), "unit": "env-steps/s", "cores": threads,
-               "kind": "port",
-               "sample": f"one CartPole iteration at num_envs={args.cpu_envs} ({n_cpu} "
-                         f"transitions): C per-env stepping {tr:.2f}s + torch-CPU learn "
-                         f"(mb={cfg['mb']}, k={cfg['k_epochs']}) {tl:.2f}s",
-               "rollout_env_steps_per_s": round(n_cpu / tr, 1),
-               "learn_ms_per_1M": round(tl / n_cpu * (1 << 20) * 1e3, 1)}
+        rec = cpu_port.cpu_iteration(E=args.cpu_envs, mb=cfg["mb"], k_epochs=cfg["k_epochs"])
+        n_cpu = rec["N"]
+        t_roll = rec["rollout_s"] + rec["flatten_s"]
+        t_learn = rec["gae_s"] + rec["learn_s"]
+        n_step = total_n / args.steps / world          # this GPU's transitions per iteration
+        t_c2 = cpu_port.extrapolate(rec, cfg["num_envs"], n_step)
+        cpu = {"value": round(n_cpu / (t_roll + t_learn), 1), "unit": "env-steps/s",
+               "cores": rec["threads"], "affinity_cores": rec["affinity_cores"], "kind": "port",
+               "sample": f"one CartPole AsyncPPO iteration of the reference's CPU path at "
+                         f"num_envs={args.cpu_envs} ({n_cpu} transitions): rollout with the "
+                         f"torch-CPU policy {rec['rollout_s']:.2f}s + sum(list, []) flatten "
+                         f"{rec['flatten_s']:.2f}s + list.insert GAE {rec['gae_s']:.2f}s + "
+                         f"torch-CPU learn (DataLoader minibatches, mb={cfg['mb']}, "
+                         f"k={cfg['k_epochs']}) {rec['learn_s']:.2f}s",
+               "rollout_env_steps_per_s": round(n_cpu / t_roll, 1),
+               "learn_ms_per_1M": round(t_learn / n_cpu * (1 << 20) * 1e3, 1),
+               "extrapolated_to_gpu_workload": {
+                   "num_envs": cfg["num_envs"], "transitions": round(n_step),
+                   "seconds_per_iteration": round(t_c2, 1),
+                   "env_steps_per_s": round(n_step / t_c2, 2),
+                   "rule": cpu_port.EXTRAPOLATION_RULE}}
 
     if rank == 0:
         out = {
@@ -372,6 +425,7 @@ def main():
             "roofline": roofline,
             "roofline_gae": roofline_gae,
             "roofline_env": roofline_env,
+            "learn_fixed_2p20": fixed,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -2316,7 +2316,9 @@ extern "C" int prl_ppo_update_dp_persistent(float* img_params, float* img_m, flo
   PRL_RCCL_TRY(g_rccl.all_reduce(ws.red2, ws.red2, count, ncclFloat32, ncclSum, c, st), "ncclAllReduce");
   PRL_HIP_TRY(hipEventRecord(g_dp_ev[0], st));
   void* kargs[] = {&args};
-  PRL_HIP_TRY(upd_launch_resident(kern, G, upd_nt(args.net), lds, kargs, st));
+  // cooperative here (unlike prl_ppo_update): with a plain launch the gate kernels on the second
+  // stream were never dispatched beside this launch and every step timed out (measured)
+  PRL_HIP_TRY(hipLaunchCooperativeKernel(kern, dim3(G), dim3(upd_nt(args.net)), kargs, (unsigned)lds, st));
   PRL_HIP_TRY(hipStreamWaitEvent(g_dp_stream, g_dp_ev[0], 0));
   const bool stand_in = dp_stand_in();
   for (int64_t s = 0; s < total; ++s) {
