@@ -159,11 +159,14 @@ class FusedUpdate:
         """This engine's own RCCL communicator for the native step loop (world > 1 on the nccl
         backend), or None: then run_stepped loops in Python with torch's all_reduce.  Every rank
         opens RCCL and votes; the communicator is built only if all ranks could open it.
-        PRL_DP_NATIVE=0 disables it."""
+        Opt-in (PRL_DP_NATIVE=1): it gives the Python loop's bits on one rank
+        (test_native_dp_loop_equals_python_loop), but RCCL refuses two ranks on one GPU, so no
+        test here has run it across ranks; until an 8-GPU run confirms it, the default is the
+        Python loop (the 2-rank tests cover that one)."""
         if getattr(self, "_comm_tried", False):
             return self._comm
         self._comm_tried, self._comm = True, None
-        if os.environ.get("PRL_DP_NATIVE", "1") == "0":
+        if os.environ.get("PRL_DP_NATIVE", "0") != "1":
             return None
         import torch.distributed as tdist
         if not (tdist.is_available() and tdist.is_initialized() and tdist.get_backend() == "nccl"):

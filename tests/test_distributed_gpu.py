@@ -90,7 +90,7 @@ def test_two_ranks_graphed_equal_one_process_on_the_union(tmp_path, fused):
 
 
 def _nccl_one_rank_worker(port, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PRL_DP_NATIVE="1")
     sys.path[:0] = PATHS
     torch.cuda.set_device(0)
     torch.distributed.init_process_group("nccl", rank=0, world_size=1,
