@@ -31,14 +31,11 @@
 //     sequential chain over the successor's head segment, so the result is bit-identical and
 //     correctness never depends on placement or order.  No ticket atomic: a single contended word
 //     caps at ~88 ops/us on MI355X (guide: dequeue row), i.e. ~73 us at 6400 tiles.
-//   * statistics: when adv is requested each tile hands {sum adv, sum adv^2} (f64) to its
-//     64-tile group with write-through (sc1) stores + s_waitcnt vmcnt(0) + the group counter
-//     (one counter per 64-B line); the last tile of a group folds the group (tile order) and
-//     bumps the global counter; the last group folds the groups (group order) -> sums_out.
-//     Deterministic, no L2 write-back fences, <= 64 arrivals per contended word.
-//   * the workspace is zero-initialised once by the caller and re-armed by every launch (the
-//     last arriver resets the counters and advances the epoch used as the granule tag); its
-//     layout depends only on the buffer's size, so calls of different n can share it.
+//   * statistics: when adv is requested each tile stores {sum adv, sum adv^2} (f64) to its slot;
+//     a one-workgroup fold kernel behind the scan sums the slots in tile order -> sums_out
+//     (deterministic) and advances the epoch used as the granule tag;
+//   * the workspace is zero-initialised once by the caller; its layout depends only on the
+//     buffer's size, so calls of different n can share it.  Two launches per call (scan, fold).
 #include "prl_common.h"
 
 #include <algorithm>
@@ -145,6 +142,19 @@ __device__ inline float chunk_apply(const ChunkDC& x, float carry) {
   carry = x.da.x + x.ca.x * carry;
   return carry;
 }
+// Walk chunks hi, hi-1, ..., lo: write each one's carry-in (g at the first element of the chunk to
+// its right) to s_cin, and apply every chunk > stop to the carry.  The next chunk's delta / c are
+// read from LDS while the current one is applied (the walk is the kernel's serial path: ~500
+// dependent mul/add pairs for a trained CartPole episode, 13 us per tile without the prefetch).
+__device__ inline float chunk_walk(const float* s_delta, const float* s_c, float* s_cin, int hi,
+                                   int lo, int stop, float carry) {
+  for (int k = hi; k >= lo; --k) {
+    s_cin[k] = carry;
+    if (k > stop) carry = chunk_apply(chunk_load(s_delta, s_c, k), carry);
+  }
+  return carry;
+}
+
 // g at index `start` computed from global memory: walk forward to the first break (c == 0) or
 // the end, then run the chain backward in the reference's order.  Used only when a successor's
 // granule did not show up in time; bit-identical to the granule path.
@@ -160,68 +170,50 @@ __device__ float gae_lookahead(const float* r, const float* d, const float* V, f
   return g;
 }
 
-// Block end.  Hands the tile's statistics to its group, the group's to the global fold, and
-// re-arms the workspace (see the file header).  Every thread of the block calls it.
-__device__ inline void gae_arrive(const GaeWs& ws, int64_t ntiles, int64_t tile, unsigned tag,
-                                  bool with_sums, double2 mine, double* out) {
-  __shared__ int s_stage;  // 0: done, 1: last of group, 2: last overall
-  __shared__ double s_part[2][GAE_THREADS / 64];
-  const int64_t ng = gae_ngroups(ntiles);
-  const int64_t g = tile / GAE_GROUP;
-  const int64_t g0 = g * GAE_GROUP;
-  const int64_t gsize = std::min<int64_t>(GAE_GROUP, ntiles - g0);
-  if (threadIdx.x == 0) {
-    if (with_sums) {
-      st_sc1_d2(ws.tile_sums + tile, mine);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    unsigned* gc = ws.group_ctr + 16 * g;
-    const unsigned old = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_stage = (old == (unsigned)(gsize - 1)) ? 1 : 0;
-  }
-  __syncthreads();
-  if (s_stage == 0) return;
-  // last tile of group g: fold the group's tile sums in tile order (lanes load in parallel)
-  __shared__ double2 s_tiles[GAE_GROUP];
-  if (with_sums && threadIdx.x < gsize) s_tiles[threadIdx.x] = ld_sc1_d2(ws.tile_sums + g0 + threadIdx.x);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double2 acc{0.0, 0.0};
-    if (with_sums)
-      for (int64_t t = 0; t < gsize; ++t) {
-        acc.x += s_tiles[t].x;
-        acc.y += s_tiles[t].y;
-      }
-    __hip_atomic_store(ws.group_ctr + 16 * g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (with_sums) st_sc1_d2(ws.group_sums + g, acc);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(&ws.ctrs[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_stage = (old == (unsigned)(ng - 1)) ? 2 : 0;
-  }
-  __syncthreads();
-  if (s_stage != 2) return;
-  if (with_sums) {  // last group: fold the groups in group order
+// Block end: the tile's {sum adv, sum adv^2} go to tile_sums[tile] with a plain store; the fold
+// kernel launched behind this one (gae_fold_kernel) sums them in tile order after the kernel
+// boundary.  (An in-launch hand-off to a last arriver cost every tile a write-through drain plus
+// a returning atomic, ~2 us of a ~19 us tile lifetime at 7 tiles per CU.)
+__device__ inline void gae_tile_sums(const GaeWs& ws, int64_t tile, bool with_sums, double2 mine) {
+  if (with_sums && threadIdx.x == 0) ws.tile_sums[tile] = mine;
+}
+
+// One workgroup: sums_out = the tile sums folded in a fixed order (thread t: tiles t, t + 1024,
+// ... ascending; then the waves' partials in wave order), and the workspace's granule epoch
+// advanced to this launch's tag.  Deterministic.
+constexpr int GAE_FOLD_THREADS = 1024;
+__global__ __launch_bounds__(GAE_FOLD_THREADS) void gae_fold_kernel(GaeWs ws, int64_t ntiles,
+                                                                    int with_sums,
+                                                                    double* __restrict__ out) {
+  __shared__ double s_part[2][GAE_FOLD_THREADS / 64];
+  if (with_sums) {
     double a = 0.0, b = 0.0;
-    for (int64_t t = threadIdx.x; t < ng; t += GAE_THREADS) {
-      const double2 v = ld_sc1_d2(ws.group_sums + t);
+    for (int64_t t = threadIdx.x; t < ntiles; t += GAE_FOLD_THREADS) {
+      const double2 v = ws.tile_sums[t];
       a += v.x;
       b += v.y;
     }
     a = wave_sum(a);
     b = wave_sum(b);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane == 0) { s_part[0][wid] = a; s_part[1][wid] = b; }
+    if (lane == 0) {
+      s_part[0][wid] = a;
+      s_part[1][wid] = b;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
       double sa = 0.0, sb = 0.0;
-      for (int w = 0; w < GAE_THREADS / 64; ++w) { sa += s_part[0][w]; sb += s_part[1][w]; }
+      for (int w = 0; w < GAE_FOLD_THREADS / 64; ++w) {
+        sa += s_part[0][w];
+        sb += s_part[1][w];
+      }
       out[0] = sa;
       out[1] = sb;
     }
   }
   if (threadIdx.x == 0) {
-    __hip_atomic_store(&ws.ctrs[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&ws.ctrs[3], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned t = ws.ctrs[3] + 1u;
+    ws.ctrs[3] = t ? t : 1u;   // the tag the launch before used (gae_tag)
   }
 }
 
@@ -346,11 +338,7 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
         }
       }
     }
-    float carry = g[0];
-    for (int k = tid - 1; k >= (p < 0 ? 0 : p); --k) {
-      s_cin[k] = carry;
-      if (k > p) carry = chunk_apply(chunk_load(s_delta, s_c, k), carry);
-    }
+    const float carry = chunk_walk(s_delta, s_c, s_cin, tid - 1, p < 0 ? 0 : p, p, g[0]);
     if (p < 0 && tid > 0) publish(carry);   // walked to chunk 0: carry = g(tile start)
   }
   if (tid == GAE_THREADS - 1 && pb != GAE_EPT - 1) {
@@ -381,22 +369,22 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
         break;
       }
     }
-    float carry = cin;
-    for (int k = GAE_THREADS - 1; k >= (L < 0 ? 0 : L); --k) {
-      s_cin[k] = carry;
-      if (k > L) carry = chunk_apply(chunk_load(s_delta, s_c, k), carry);
-    }
+    const float carry = chunk_walk(s_delta, s_c, s_cin, GAE_THREADS - 1, L < 0 ? 0 : L, L, cin);
     if (L < 0) publish(carry);               // no break in the tile
   }
   __syncthreads();
   PRL_GAE_MARK(3);
-  // every chunk's elements after its last break, from its carry-in
+  // every chunk's elements after its last break, from its carry-in (delta / c re-read from LDS:
+  // not keeping them in registers across the walk keeps the kernel at 8 waves per SIMD)
   if (pb != GAE_EPT - 1) {
+    const ChunkDC x = chunk_load(s_delta, s_c, tid);
+    const float dl2[GAE_EPT] = {x.da.x, x.da.y, x.da.z, x.da.w, x.db.x, x.db.y, x.db.z, x.db.w};
+    const float cc2[GAE_EPT] = {x.ca.x, x.ca.y, x.ca.z, x.ca.w, x.cb.x, x.cb.y, x.cb.z, x.cb.w};
     float carry = s_cin[tid];
 #pragma unroll
     for (int k = GAE_EPT - 1; k >= 0; --k) {
       if (k > pb) {
-        carry = dl[k] + cc[k] * carry;
+        carry = dl2[k] + cc2[k] * carry;
         g[k] = carry;
       }
     }
@@ -449,7 +437,7 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
     if (tid == 0)
       for (int w = 0; w < GAE_THREADS / 64; ++w) { mine.x += s_red[0][w]; mine.y += s_red[1][w]; }
   }
-  gae_arrive(ws, ntiles, tile, tag, adv != nullptr, mine, sums_out);
+  gae_tile_sums(ws, tile, adv != nullptr, mine);
   PRL_GAE_MARK(6);
 }
 
@@ -457,8 +445,6 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
 __global__ __launch_bounds__(GAE_THREADS) void stats_kernel(const float* __restrict__ x, int64_t n,
                                                             GaeWs ws, int64_t ntiles,
                                                             double* __restrict__ sums_out) {
-  __shared__ unsigned s_tag;
-  if (threadIdx.x == 0) s_tag = gae_tag(ws);
   const int64_t tile = blockIdx.x;
   const int64_t i0 = tile * GAE_TILE + (int64_t)threadIdx.x * GAE_EPT;
   double s1 = 0.0, s2 = 0.0;
@@ -480,7 +466,7 @@ __global__ __launch_bounds__(GAE_THREADS) void stats_kernel(const float* __restr
   double2 mine{0.0, 0.0};
   if (threadIdx.x == 0)
     for (int w = 0; w < GAE_THREADS / 64; ++w) { mine.x += s_red[0][w]; mine.y += s_red[1][w]; }
-  gae_arrive(ws, ntiles, tile, s_tag, true, mine, sums_out);
+  gae_tile_sums(ws, tile, true, mine);
 }
 
 // (x - mean) / (std_unbiased + eps) in float32, statistics from f64 sums (PPO.py:199).
@@ -545,6 +531,9 @@ extern "C" int prl_gae(const float* r, const float* d, const float* V, const flo
     hipLaunchKernelGGL(gae_kernel<false>, dim3((unsigned)nt), dim3(GAE_THREADS), 0, s, r, d, V,
                        next_value, n, gf, glf, ret, adv, ws, nt, sums_out);
   PRL_LAUNCH_CHECK("gae");
+  hipLaunchKernelGGL(gae_fold_kernel, dim3(1), dim3(GAE_FOLD_THREADS), 0, s, ws, nt,
+                     adv ? 1 : 0, sums_out);
+  PRL_LAUNCH_CHECK("gae_fold");
   return PRL_OK;
 }
 
@@ -564,6 +553,8 @@ extern "C" int prl_adv_stats(const float* x, int64_t n, double* sums_out, void* 
   GaeWs ws = gae_ws_carve(workspace, gae_capacity_tiles(workspace_bytes));
   hipLaunchKernelGGL(stats_kernel, dim3((unsigned)nt), dim3(GAE_THREADS), 0, s, x, n, ws, nt, sums_out);
   PRL_LAUNCH_CHECK("adv_stats");
+  hipLaunchKernelGGL(gae_fold_kernel, dim3(1), dim3(GAE_FOLD_THREADS), 0, s, ws, nt, 1, sums_out);
+  PRL_LAUNCH_CHECK("adv_stats_fold");
   return PRL_OK;
 }
 

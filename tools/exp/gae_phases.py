@@ -15,11 +15,16 @@ import prl_native  # noqa: E402
 
 lib = ctypes.CDLL(os.path.join(HERE, "libgae_phases.so"))
 P = ctypes.c_void_p
-for n, seg in ((8_269_824, 126), (2_277_376, 35)):
+CASES = [(int(a), int(b)) for a, b in (x.split(":") for x in sys.argv[1].split(","))] if len(sys.argv) > 1 else [(8_269_824, 126), (2_277_376, 35)]
+for n, seg in CASES:
     g = torch.Generator(device="cuda").manual_seed(1)
     r = torch.ones(n, device="cuda")
     V = torch.randn(n, device="cuda", generator=g)
-    d = (torch.rand(n, device="cuda", generator=g) < 1.0 / seg).float()
+    if seg < 0:   # every -seg-th transition ends an episode (trained CartPole: 500, Pendulum: 200)
+        d = torch.zeros(n, device="cuda")
+        d[-seg - 1::-seg] = 1
+    else:
+        d = (torch.rand(n, device="cuda", generator=g) < 1.0 / seg).float()
     d[-1] = 1
     ret, adv = torch.empty_like(V), torch.empty_like(V)
     sums = torch.zeros(2, dtype=torch.float64, device="cuda")
