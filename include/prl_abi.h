@@ -268,24 +268,6 @@ int prl_ppo_grad_fold_step(const float* in_p, const float* in_m, const float* in
                            float ent_coef, float lr, float beta1, float beta2, float eps,
                            float weight_decay, float max_norm, float* loss_out, float* grad_out,
                            void* workspace, int64_t workspace_bytes, void* stream);
-/* The data-parallel loop of prl_ppo_update_dp as ONE persistent launch per rank (the world = 1
- * engine's structure, grid <= 128 workgroups): per step the launch reduces its gradient in-GPU
- * and raises a ready word; a second stream, enqueued here for all steps up front, runs per step
- * a one-lane gate kernel that waits for it, then ncclAllReduce of that step's buffer over the
- * ranks; the next gate raises a done word that the launch waits for before clip + AdamW.
- * Same bits as prl_ppo_update_dp.  adam_step: device float (AdamW steps so far, advanced);
- * counts_dev: device copy of counts.  No reference counterpart (single-process reference);
- * replaces PPO.py:216-255 on data-parallel ranks. */
-int prl_ppo_update_dp_persistent(float* img_params, float* img_m, float* img_v, float* adam_step,
-                                 int32_t D, int32_t A, int32_t discrete, const float* S,
-                                 const float* actions, const float* old_logp, const float* adv,
-                                 const float* ret, int64_t N, int32_t mini_batch,
-                                 int32_t k_epochs, int64_t nb, const int64_t* counts,
-                                 const int64_t* counts_dev, float clip, float vf_coef,
-                                 float ent_coef, float lr, float beta1, float beta2, float eps,
-                                 float weight_decay, float max_norm, float* loss_out,
-                                 void* workspace, int64_t workspace_bytes, void* comm,
-                                 void* stream);
 /* Column sums out[c] = sum_r x[r][c] of a row-major f32 matrix (cols >= 1): the bias
  * gradient of a Linear over a large batch (nn.Linear backward, reached from PPO.py:249 /
  * RND.py:112).  Two deterministic passes; `partial` holds prl_colsum_partial_floats(rows, cols)

@@ -107,8 +107,8 @@ class FusedUpdate:
         trunk, heads, outs = self.D * H, nh * H * H, nout * H
         return 2 * (trunk + heads + outs) * 2 + 2 * (heads + outs)
 
-    PHASES = ("forward+backward", "publish", "wait A", "slice reduce", "wait B", "norm",
-              "AdamW")
+    PHASES = ("forward+backward", "publish", "gather partials", "slice reduce", "gather reduced",
+              "norm", "AdamW")
 
     CHUNK_STAGES = ("forward", "barrier 1", "loss", "heads bwd + dW2", "barrier 2", "dW1",
                     "dF + trunk bwd", "dW0 + biases")
@@ -198,55 +198,6 @@ class FusedUpdate:
             prl_native.dp_comm_destroy(comm)
         self._comm = None
 
-    def _dp_persistent_ok(self):
-        """Opt-in (PRL_DP_PERSISTENT=1): the persistent data-parallel launch.  Bit-identical to
-        the stepped loop, but measured slower on MI355X (39 vs 23 us per step with a one-rank
-        communicator, tools/stepped_bench.py): the second stream's per-step gate launch and the
-        all-reduce behind it are dispatched with ~10-20 us of queue latency while the persistent
-        launch occupies the other queue.  Needs free CUs beside it (grid <= 128 workgroups,
-        mini_batch <= 2048); a failed launch turns it off for the rest of the process."""
-        if os.environ.get("PRL_DP_PERSISTENT", "0") != "1" or getattr(self, "_dp_pers_off", False):
-            return False
-        return -(-self.mini_batch // 16) <= 128
-
-    def _run_dp_persistent(self, tens, k_epochs, counts, step, group, beta1, beta2, comm,
-                           n_local, nb):
-        """One persistent launch for the whole data-parallel loop (the all-reduce of each step on
-        a second stream beside it).  If any rank's launch reports an in-kernel timeout, every
-        rank restores its state and the caller runs the stepped loop instead (same bits)."""
-        import torch.distributed as tdist
-        img_p, img_m, img_v = self.img
-        snap = [x.clone() for x in self.img]
-        stat = prl_native.ppo_update_status(self.ws)
-        stat.zero_()
-        self.step.fill_(float(step))
-        if self.events is not None:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record()
-        keep = prl_native.ppo_update_dp_persistent(
-            img_p, img_m, img_v, self.step, self.D, self.A, self.discrete, *tens, self.mini_batch,
-            k_epochs, counts, self.ppo.policy_clip, self.ppo.value_coef, self.ppo.entropy_coef,
-            group["lr"], beta1, beta2, group["eps"], group["weight_decay"], 2.0, self.loss,
-            self.ws, comm)
-        if self.events is not None:
-            ev[1].record()
-            self.events.append(("ppo_update_kernel_dp", ev[0], ev[1], n_local * k_epochs,
-                                k_epochs * nb))
-        ok = (stat.max() == 0).to(torch.int32).reshape(1)
-        if tdist.is_available() and tdist.is_initialized():
-            tdist.all_reduce(ok, op=tdist.ReduceOp.MIN)
-        del keep
-        if int(ok.item()) == 1:
-            return True
-        warnings.warn("persistent data-parallel launch timed out; using the stepped loop")
-        self._dp_pers_off = True
-        for dst, src in zip(self.img, snap):
-            dst.copy_(src)
-        stat.zero_()
-        if self.events is not None:
-            self.events.pop()
-        return False
-
     def run_stepped(self, S, A, old_logp, adv, ret, k_epochs: int, n_ranks, all_reduce,
                     comm=None):
         """The same update loop for data-parallel ranks.  Per optimizer step ONE launch,
@@ -289,12 +240,6 @@ class FusedUpdate:
             beta2, group["eps"], group["weight_decay"], 2.0))
         step = int(round(float(self.step.item())))
         n_local = int(S.shape[0])
-        if comm is not None and self._dp_persistent_ok():
-            done = self._run_dp_persistent(tens, k_epochs, counts, step, group, beta1, beta2,
-                                           comm, n_local, nb)
-            if done:
-                step += k_epochs * nb
-                k_epochs = 0
         if comm is not None and k_epochs > 0:
             if self.events is not None:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

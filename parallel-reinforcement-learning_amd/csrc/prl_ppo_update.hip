@@ -140,14 +140,6 @@ struct UpdArgs {
   unsigned long long* prof;  // [8] workgroup 0's time per phase (100 MHz ticks, summed over steps)
   unsigned grad_target;      // ppo_grad_kernel: arrivals on ctr[0] that end its hand-off
   int profile;               // 1: workgroup 0 records its phase / tile-stage times (PRL_UPD_PROFILE)
-  // data-parallel persistent mode (ppo_update_kernel<..., DP = true>): the reduced gradient of
-  // step s goes to red (s even) / red2 (s odd); workgroup 0 raises dp_ready to s + 1, a second
-  // stream waits for that value, all-reduces the buffer over the ranks (RCCL) and raises dp_done
-  // to s + 1; every workgroup waits for dp_done.  counts[j] = rows of union minibatch j.
-  const int64_t* counts;
-  float* red2;
-  unsigned* dp_ready;
-  unsigned* dp_done;
 };
 
 // ---- sc1 (write-through / L1-bypassing) accessors -------------------------------------------
@@ -227,22 +219,6 @@ __device__ inline bool upd_wait(unsigned* ctr, int which, unsigned target) {
     if (ld_sc1u(ctr + which) >= target) return true;
     if (ld_sc1u(ctr + 2) != 0u) return false;
     if (spins > UPD_SPIN_LIMIT) {
-      __hip_atomic_store(ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_or(ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// one lane, data-parallel persistent mode: wait until the all-reduce stream has raised *done to
-// `target` (RCCL over xGMI between the ranks: a longer budget than the in-GPU hand-offs)
-__device__ inline bool upd_wait_dp(const unsigned* done, unsigned target, unsigned* ctr) {
-  for (unsigned spins = 0;; ++spins) {
-    if (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= target) return true;
-    if (ld_sc1u(ctr + 2) != 0u) return false;
-    if (spins > 16u * UPD_SPIN_LIMIT) {
       __hip_atomic_store(ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_or(ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky
@@ -1087,7 +1063,7 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
 }
 
 // NQ = parameter quads per thread (ceil(Lp / 4 / 256)): AdamW's moments live in registers.
-template <int NQ, int KD, int KA, bool DP>
+template <int NQ, int KD, int KA>
 __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& args) {
   constexpr int NW = upd_nw<KD, KA>(), NT = 64 * NW;
   extern __shared__ __align__(16) float upd_lds[];
@@ -1105,14 +1081,6 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
   const UpdScr sc = upd_scr(scratch, n.D, NW);
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
   float* s_adam = hdr + 10;         // [2] this step's AdamW step size, 1 / sqrt(bc2)
-  float* s_norm = hdr + 4;          // [4] DP: per-wave squared-norm partials
-  static_assert(!DP || NT == UPD_THREADS, "DP mode assumes 256-thread workgroups");
-  // DP: a workgroup that gives up releases the all-reduce stream (every later wait passes)
-  auto dp_release = [&]() {
-    if constexpr (DP) {
-      if (t == 0) __hip_atomic_store(args.dp_ready, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  };
 
   // ---- load the parameter image into LDS and this thread's moment quads (q = t + NT i) into
   //      registers: args.params / exp_avg / exp_avg_sq are IMAGES here (prl_ppo_update converts
@@ -1155,8 +1123,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     const int j = s % args.nb;
     const int64_t mb0 = (int64_t)j * args.mb;
     const int B = (int)std::min<int64_t>(args.mb, args.N - mb0);
-    // DP: this rank's rows may be fewer than the union's (or none); scale by the union's rows
-    const float invB = DP ? 1.0f / (float)args.counts[j] : 1.0f / (float)B;
+    const float invB = 1.0f / (float)B;
     // profile mode 2 (PRL_UPD_PROFILE=2, diagnostics only): no rows, i.e. the exchange alone
     const int myrows = args.profile == 2 ? 0 : std::max(0, std::min(R, B - g * R));
     const int64_t myrow0 = mb0 + (int64_t)g * R;
@@ -1182,7 +1149,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     __syncthreads();
     mark(0);   // phase A compute
     const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part),
-                                 rs_red = upd_rsrc(DP && (s & 1) ? args.red2 : args.red);
+                                 rs_red = upd_rsrc(args.red);
     for (int q = t; q < Qtot; q += NT)
       st4_sc1(rs_part, ((size_t)g * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1211,7 +1178,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       s_adam[1] = (float)(1.0 / sqrt(bc2));         // 1 / sqrt(bias correction 2)
     }
     __syncthreads();
-    if (*s_abort) { dp_release(); return; }
+    if (*s_abort) return;
     mark(2);   // wait A
     // ---- phase B: reduce this workgroup's slice over the G partials --------------------------
     {
@@ -1228,17 +1195,8 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
         if (t == 0) *s_abort = ok ? 0 : 1;
       }
       __syncthreads();
-      if (*s_abort) { dp_release(); return; }
-      if constexpr (DP) {   // every slice is out: hand the buffer to the all-reduce stream
-        if (t == 0) {
-          if (g == 0)
-            __hip_atomic_store(args.dp_ready, (unsigned)(s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          *s_abort = upd_wait_dp(args.dp_done, (unsigned)(s + 1), args.ctr) ? 0 : 1;
-        }
-        __syncthreads();
-        if (*s_abort) { dp_release(); return; }
-      }
-      mark(4);   // wait B (+ DP: the all-reduce)
+      if (*s_abort) return;
+      mark(4);   // wait B
     }
     // ---- phase C: clip_grad_norm_(2.0) + AdamW on every workgroup's own copy ------------------
     float4 gq[NQ];   // this thread's gradient quads: loads issued first, in flight under the norm
@@ -1248,20 +1206,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       if (q < Qp) gq[i] = ld4_sc1(rs_red, (size_t)q * 4);
     }
     float clipc;
-    if constexpr (DP) {
-      // the norm of the all-reduced gradient, summed exactly as ppo_adam_kernel sums it (per
-      // thread quads q = t + 256 i ascending, wave sum, waves in order): same bits as the
-      // stepped engine
-      float acc = 0.f;
-#pragma unroll
-      for (int i = 0; i < NQ; ++i)
-        if (t + i * NT < Qp) acc += adam_sq4(gq[i]);
-      clipc = adam_clip(acc, args.max_norm, s_norm);
-      if (g == 0 && t == 0 && s + 1 == args.total_steps) {
-        const float4 lp = ld4_sc1(rs_red, (size_t)Qp * 4);
-        loss_last = lp.x * invB + args.vf_coef * (lp.y * invB) - args.ent_coef * (lp.z * invB);
-      }
-    } else {
+    {
       // every wave of every workgroup sums the NW G pieces in the same order (no LDS, no barrier)
       const int l = t & 63;
       float piece = 0.f;
@@ -1276,25 +1221,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       }
     }
     mark(5);   // norm + loss
-    if constexpr (DP) {   // ppo_adam_kernel's arithmetic (adam_quad): same bits as the stepped engine
-      AdamConst c;
-      c.step_size = s_adam[0];
-      c.inv_bc2_sqrt = s_adam[1];
-      c.decay = (float)(1.0 - (double)args.lr * (double)args.wd);
-      c.omb1 = (float)(1.0 - (double)args.beta1);
-      c.omb2 = (float)(1.0 - (double)args.beta2);
-      c.beta2 = args.beta2;
-      c.eps = args.eps;
-#pragma unroll
-      for (int i = 0; i < NQ; ++i) {
-        const int q = t + i * NT;
-        if (q < Qp) {
-          float4 pw = *reinterpret_cast<float4*>(W + 4 * q);
-          adam_quad(c, clipc, gq[i], mreg[i], vreg[i], pw);
-          *reinterpret_cast<float4*>(W + 4 * q) = pw;
-        }
-      }
-    } else {
+    {
       const float step_size = s_adam[0];
       const float inv_bc2_sqrt = s_adam[1];   // scalar divide -> one multiply
       const float decay = (float)(1.0 - (double)args.lr * (double)args.wd);
@@ -1362,13 +1289,13 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
 
 // KDIM > 0: the observation dim is a compile-time constant and the whole parameter layout folds
 // into immediates (the specialised shapes); KDIM = 0: runtime layout from the kernel argument.
-template <int NQ, int KD, int KA, int KDIM, bool DP = false>
+template <int NQ, int KD, int KA, int KDIM>
 __global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_update_kernel(UpdArgs args) {
   if constexpr (KDIM > 0) {
     constexpr UpdNet N = upd_make(KDIM, KA, KD);
-    ppo_update_body<NQ, KD, KA, DP>(N, args);
+    ppo_update_body<NQ, KD, KA>(N, args);
   } else {
-    ppo_update_body<NQ, KD, KA, DP>(args.net, args);
+    ppo_update_body<NQ, KD, KA>(args.net, args);
   }
 }
 
@@ -1665,14 +1592,6 @@ const void* upd_kernel_for(const UpdNet& n) {
   if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0>);
   return nullptr;
 }
-const void* upd_dp_kernel_for(const UpdNet& n) {
-  const int nq = upd_nq(n);
-  if (upd_force_generic()) return nq <= 20 ? reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0, true>) : nullptr;
-  if (n.discrete && n.A == 2 && n.D == 4 && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4, true>);
-  if (!n.discrete && n.A == 1 && n.D == 3 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3, true>);
-  if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0, true>);
-  return nullptr;
-}
 const void* upd_grad_kernel_for(const UpdNet& n) {
   if (upd_force_generic()) return reinterpret_cast<const void*>(ppo_grad_kernel<-1, 0, 0>);
   if (n.discrete && n.A == 2 && n.D == 4) return reinterpret_cast<const void*>(ppo_grad_kernel<1, 2, 4>);
@@ -1716,8 +1635,6 @@ struct UpdWs {
   float* red;
   float* part;
   float* img;   // [3][Lp + 4]: parameter, exp_avg, exp_avg_sq images of the persistent launch
-  float* red2;  // [Qtot * 4]: DP persistent mode, the odd steps' reduced gradient
-  unsigned* dp; // DP persistent mode: [0] ready, [32] done, [64] gate step counter (own lines)
 };
 
 // workspace: ctr[UPD_CTR_WORDS] (words 0-3 and the shards zeroed per launch, word 4 sticky) | prof[32] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4]
@@ -1726,8 +1643,7 @@ size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
   const size_t o_ctr = take(4 * UPD_CTR_WORDS), o_prof = take(256), o_sq = take(2048 * 4), o_red = take(Qtot * 16),
-               o_part = take((size_t)G * Qtot * 16), o_img = take((size_t)3 * Qtot * 16),
-               o_red2 = take(Qtot * 16), o_dp = take(512);
+               o_part = take((size_t)G * Qtot * 16), o_img = take((size_t)3 * Qtot * 16);
   if (ws) {
     ws->ctr = reinterpret_cast<unsigned*>(base + o_ctr);
     ws->prof = reinterpret_cast<unsigned long long*>(base + o_prof);
@@ -1735,8 +1651,6 @@ size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
     ws->red = reinterpret_cast<float*>(base + o_red);
     ws->part = reinterpret_cast<float*>(base + o_part);
     ws->img = reinterpret_cast<float*>(base + o_img);
-    ws->red2 = reinterpret_cast<float*>(base + o_red2);
-    ws->dp = reinterpret_cast<unsigned*>(base + o_dp);
   }
   return off;
 }
@@ -2183,159 +2097,5 @@ extern "C" int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, 
     if (((total - 1) & 1) != 0)   // the caller's grad holds the last all-reduced gradient
       PRL_HIP_TRY(hipMemcpyAsync(grad, ws.red, sizeof(float) * count, hipMemcpyDeviceToDevice, st));
   }
-  return PRL_OK;
-}
-
-// The data-parallel loop as ONE persistent launch per learn() (the world = 1 engine's structure):
-// per step the launch reduces its gradient in-GPU, raises dp_ready; a second stream, enqueued
-// here for every step up front, waits for that value (dp_gate_kernel), all-reduces the buffer
-// over the ranks (ncclAllReduce, RCCL over xGMI) and raises dp_done (the next gate),
-// which the launch waits for before clip + AdamW.  The all-reduce runs on CUs the launch leaves
-// free (grid <= 128 workgroups).  Same bits as prl_ppo_update_dp (stepped).  adam_step: device
-// float, AdamW steps so far (advanced by the launch); counts_dev: device copy of counts.
-namespace {
-hipStream_t g_dp_stream = nullptr;
-hipEvent_t g_dp_ev[2] = {nullptr, nullptr};
-// PRL_DP_STAND_IN=1 (tests on one GPU): the second stream runs this kernel in place of the
-// all-reduce, so the one-GPU test has a real kernel executing beside the persistent launch (a
-// one-rank RCCL all-reduce in place launches nothing)
-__global__ void dp_stand_in_kernel(float* buf, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) buf[i] = buf[i] * 1.0f;
-}
-// The second stream's gate, one launch per step (hipStreamWaitValue32 / WriteValue32 cost
-// ~18 us of host time each here, ~3x a launch): with the step counter c = dp[64] (advanced by
-// the gates themselves, so a captured block of gates replays), signal done = c (the all-reduce of
-// step c - 1 ahead of this gate on the stream has completed), then wait for ready >= c + 1 and
-// advance c.  signal_only: the last gate.  Bounded: on timeout it raises the launch's abort word.
-__global__ void dp_gate_kernel(unsigned* dp, unsigned* ctr, int signal_only) {
-  if (threadIdx.x != 0) return;
-  const unsigned c = __hip_atomic_load(dp + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (c > 0) __hip_atomic_store(dp + 32, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (signal_only) return;
-  for (unsigned spins = 0;; ++spins) {
-    if (__hip_atomic_load(dp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= c + 1) break;
-    if (__hip_atomic_load(ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
-    if (spins > 16u * UPD_SPIN_LIMIT) {
-      __hip_atomic_store(ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_or(ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __hip_atomic_store(dp + 64, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-bool dp_stand_in() {
-  const char* e = getenv("PRL_DP_STAND_IN");
-  return e && e[0] == '1';
-}
-}
-extern "C" int prl_ppo_update_dp_persistent(float* img_params, float* img_m, float* img_v,
-                                            float* adam_step, int32_t D, int32_t A,
-                                            int32_t discrete, const float* S, const float* actions,
-                                            const float* old_logp, const float* adv,
-                                            const float* ret, int64_t N, int32_t mini_batch,
-                                            int32_t k_epochs, int64_t nb, const int64_t* counts,
-                                            const int64_t* counts_dev, float clip, float vf_coef,
-                                            float ent_coef, float lr, float beta1, float beta2,
-                                            float eps, float weight_decay, float max_norm,
-                                            float* loss_out, void* workspace,
-                                            int64_t workspace_bytes, void* comm, void* stream) {
-  UpdArgs args{};
-  PRL_REQUIRE(upd_layout(D, A, discrete, args.net), "prl_ppo_update_dp_persistent: D=%d A=%d not supported", D, A);
-  PRL_REQUIRE(N >= 0 && mini_batch > 0 && k_epochs >= 0 && nb >= 0 && counts && counts_dev,
-              "prl_ppo_update_dp_persistent: bad sizes");
-  PRL_REQUIRE(img_params && img_m && img_v && adam_step && workspace && comm,
-              "prl_ppo_update_dp_persistent: null pointer");
-  PRL_REQUIRE(g_rccl.all_reduce, "prl_ppo_update_dp_persistent: RCCL not opened (prl_dp_rccl_open)");
-  PRL_REQUIRE(N == 0 || (S && actions && old_logp && adv && ret), "prl_ppo_update_dp_persistent: null input");
-  const int G = upd_grid(mini_batch);
-  PRL_REQUIRE(G <= 128, "prl_ppo_update_dp_persistent: %d workgroups leave no CUs for the all-reduce", G);
-  UpdWs ws;
-  const size_t need = upd_ws_carve(args.net, G, reinterpret_cast<char*>(workspace), &ws);
-  PRL_REQUIRE((size_t)workspace_bytes >= need, "prl_ppo_update_dp_persistent: workspace too small");
-  PRL_REQUIRE((int64_t)k_epochs * nb < (int64_t)(1u << 31) / 256, "prl_ppo_update_dp_persistent: too many steps");
-  for (int64_t j = 0; j < nb; ++j)
-    PRL_REQUIRE(counts[j] > 0, "prl_ppo_update_dp_persistent: empty union minibatch %lld", (long long)j);
-  const int64_t total = (int64_t)k_epochs * nb;
-  if (total == 0) return PRL_OK;
-  args.S = S;
-  args.act = actions;
-  args.old_logp = old_logp;
-  args.adv = adv;
-  args.ret = ret;
-  args.N = N;
-  args.mb = mini_batch;
-  args.nb = (int)nb;
-  args.total_steps = (int)total;
-  args.G = G;
-  args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RT) * UPD_RT;
-  args.clip = clip;
-  args.vf_coef = vf_coef;
-  args.ent_coef = ent_coef;
-  args.lr = lr;
-  args.beta1 = beta1;
-  args.beta2 = beta2;
-  args.eps = eps;
-  args.wd = weight_decay;
-  args.max_norm = max_norm;
-  args.params = img_params;
-  args.exp_avg = img_m;
-  args.exp_avg_sq = img_v;
-  args.adam_step = adam_step;
-  args.loss_out = loss_out;
-  args.part = ws.part;
-  args.red = ws.red;
-  args.red2 = ws.red2;
-  args.sq = ws.sq;
-  args.ctr = ws.ctr;
-  args.prof = ws.prof;
-  args.profile = upd_profile_enabled();
-  args.counts = counts_dev;
-  args.dp_ready = ws.dp;
-  args.dp_done = ws.dp + 32;
-  const size_t lds = upd_lds_bytes(args.net);
-  PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_update_dp_persistent: %zu B of LDS needed", lds);
-  const void* kern = upd_dp_kernel_for(args.net);
-  PRL_REQUIRE(kern, "prl_ppo_update_dp_persistent: %d parameter quads per thread not built", upd_nq(args.net));
-  hipStream_t st = as_stream(stream);
-  if (!g_dp_stream) {
-    PRL_HIP_TRY(hipStreamCreateWithFlags(&g_dp_stream, hipStreamNonBlocking));
-    PRL_HIP_TRY(hipEventCreateWithFlags(&g_dp_ev[0], hipEventDisableTiming));
-    PRL_HIP_TRY(hipEventCreateWithFlags(&g_dp_ev[1], hipEventDisableTiming));
-  }
-  const ncclComm_t c = reinterpret_cast<ncclComm_t>(comm);
-  const size_t count = (size_t)args.net.Lp + 4;   // the reduced gradient image + its loss quad
-  PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
-  PRL_HIP_TRY(hipMemsetAsync(ws.ctr + UPD_CTR_A, 0, 4 * (UPD_CTR_WORDS - UPD_CTR_A), st));
-  PRL_HIP_TRY(hipMemsetAsync(ws.dp, 0, 512, st));
-  // one all-reduce on the launch's stream first: RCCL's first collective on a communicator sets
-  // up its channels, which must not count against the launch's in-kernel wait budget
-  PRL_RCCL_TRY(g_rccl.all_reduce(ws.red2, ws.red2, count, ncclFloat32, ncclSum, c, st), "ncclAllReduce");
-  PRL_HIP_TRY(hipEventRecord(g_dp_ev[0], st));
-  void* kargs[] = {&args};
-  // cooperative here (unlike prl_ppo_update): with a plain launch the gate kernels on the second
-  // stream were never dispatched beside this launch and every step timed out (measured)
-  PRL_HIP_TRY(hipLaunchCooperativeKernel(kern, dim3(G), dim3(upd_nt(args.net)), kargs, (unsigned)lds, st));
-  PRL_HIP_TRY(hipStreamWaitEvent(g_dp_stream, g_dp_ev[0], 0));
-  const bool stand_in = dp_stand_in();
-  for (int64_t s = 0; s < total; ++s) {
-    float* buf = (s & 1) ? ws.red2 : ws.red;
-    hipLaunchKernelGGL(dp_gate_kernel, dim3(1), dim3(64), 0, g_dp_stream, ws.dp, ws.ctr, 0);
-    PRL_LAUNCH_CHECK("dp_gate");
-    if (stand_in) {
-      hipLaunchKernelGGL(dp_stand_in_kernel, dim3((unsigned)cdiv((int64_t)count, 256)), dim3(256), 0,
-                         g_dp_stream, buf, (int)count);
-      PRL_LAUNCH_CHECK("dp_stand_in");
-    } else {
-      PRL_RCCL_TRY(g_rccl.all_reduce(buf, buf, count, ncclFloat32, ncclSum, c, g_dp_stream), "ncclAllReduce");
-    }
-  }
-  hipLaunchKernelGGL(dp_gate_kernel, dim3(1), dim3(64), 0, g_dp_stream, ws.dp, ws.ctr, 1);
-  PRL_LAUNCH_CHECK("dp_gate");
-  PRL_HIP_TRY(hipEventRecord(g_dp_ev[1], g_dp_stream));
-  PRL_HIP_TRY(hipStreamWaitEvent(st, g_dp_ev[1], 0));
   return PRL_OK;
 }

@@ -69,9 +69,6 @@ SIGNATURES = {
     "prl_ppo_adam_step": [_P, _P, _P, _I32, _I32, _I32, _P, _I64] + [_F32] * 9 + [_P, _P],
     "prl_colsum_partial_floats": [_I64, _I32],
     "prl_colsum_f32": [_P, _I64, _I32, _P, _P, _I64, _P],
-    "prl_ppo_update_dp_persistent": [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64,
-                                     _I32, _I32, _I64, _P, _P] + [_F32] * 9 + [_P, _P, _I64, _P,
-                                                                               _P],
     "prl_ppo_grad_fold_step": [_P] * 7 + [_I64, _F32, _I32, _I32, _I32] + [_P] * 5
                               + [_I64, _I32, _I64] + [_F32] * 10 + [_P, _P, _P, _I64, _P],
 }
@@ -498,29 +495,6 @@ def ppo_update_dp(img_p, img_m, img_v, D, A, discrete, S, A_, old_logp, adv, ret
         beta2, eps, wd, max_norm, _dev(grad, torch.float32, "grad"),
         _dev(loss_out, torch.float32, "loss"), _dev(workspace, torch.uint8, "workspace"),
         workspace.numel(), comm, _stream()), "prl_ppo_update_dp")
-
-
-def ppo_update_dp_persistent(img_p, img_m, img_v, adam_step, D, A, discrete, S, A_, old_logp,
-                             adv, ret, mini_batch, k_epochs, counts, clip, vf_coef, ent_coef, lr,
-                             beta1, beta2, eps, wd, max_norm, loss_out, workspace, comm):
-    """The data-parallel loop as one persistent launch (prl_ppo_update_dp_persistent): the
-    per-step all-reduce runs on a second stream, enqueued up front, beside the launch."""
-    import numpy as np
-    cnt = np.ascontiguousarray(np.asarray(counts, dtype=np.int64))
-    cnt_dev = torch.from_numpy(cnt).to(img_p.device)
-    N = int(S.shape[0])
-    _check(lib().prl_ppo_update_dp_persistent(
-        _dev(img_p, torch.float32, "img_p"), _dev(img_m, torch.float32, "img_m"),
-        _dev(img_v, torch.float32, "img_v"), _dev(adam_step, torch.float32, "adam_step"),
-        int(D), int(A), int(bool(discrete)),
-        _dev(S, torch.float32, "S"), _dev(A_, torch.float32, "actions"),
-        _dev(old_logp, torch.float32, "old_logp"), _dev(adv, torch.float32, "adv"),
-        _dev(ret, torch.float32, "ret"), N, int(mini_batch), int(k_epochs), int(cnt.size),
-        cnt.ctypes.data_as(ctypes.c_void_p), _dev(cnt_dev, torch.int64, "counts"), clip, vf_coef,
-        ent_coef, lr, beta1, beta2, eps, wd, max_norm, _dev(loss_out, torch.float32, "loss"),
-        _dev(workspace, torch.uint8, "workspace"), workspace.numel(), comm, _stream()),
-        "prl_ppo_update_dp_persistent")
-    return cnt_dev   # keep alive until the launch has read it
 
 
 def ppo_image_floats(D, A, discrete) -> int:

@@ -496,49 +496,3 @@ def test_folded_step_equals_grad_then_adam(cont, D, A):
     assert float(p._engine.step.item()) == 2 * 5
 
 
-@pytest.mark.parametrize("cont", [False, True])
-@pytest.mark.parametrize("stand_in", ["0", "1"])
-def test_persistent_dp_launch_equals_python_loop(cont, stand_in, monkeypatch):
-    """prl_ppo_update_dp_persistent (the data-parallel loop as ONE persistent launch; each step's
-    all-reduce on a second stream behind one-lane gate kernels) gives
-    the same bits as the stepped Python loop: parameters, both moments, step count and loss.
-    stand_in = "1" runs a real kernel on the second stream in place of the (one-rank, launch-free)
-    RCCL all-reduce, so a kernel executes beside the persistent launch on this one GPU."""
-    import prl_native
-    from PPO import PPO
-    monkeypatch.setenv("PRL_DP_STAND_IN", stand_in)
-    monkeypatch.setenv("PRL_DP_PERSISTENT", "1")
-    N = 3000 + 7
-    data = _data(N, 3 if cont else 4, cont, seed=29)
-    D, A = (3, 1) if cont else (4, 2)
-    prl_native.dp_rccl_open()
-    comm = prl_native.dp_comm_init(prl_native.dp_unique_id(), 1, 0)
-    outs = []
-    try:
-        for native in (False, True):
-            torch.manual_seed(0)
-            p = PPO(cont, D, A, action_scaling=2.0 if cont else None, k_epochs=3, batch_size=64,
-                    mini_batch_size=512)
-            p.show_progress = False
-            p.memory.push_device(*data)
-            p._world = staticmethod(lambda: 1)
-            eng = p._fused_engine()
-            eng.events = []
-
-            def stepped_update(S, A_, old, adv, ret, n_ranks, p=p, native=native):
-                e = p._fused_engine()
-                p.last_loss = e.run_stepped(S, A_, old, adv, ret, p.k_epochs, n_ranks,
-                                            lambda t: t, comm=comm if native else None)
-            p._update = stepped_update
-            p.learn()
-            torch.cuda.synchronize()
-            names = {e[0] for e in eng.events}
-            assert names == ({"ppo_update_kernel_dp"} if native else {"ppo_grad_kernel"}), names
-            assert not getattr(eng, "_dp_pers_off", False)
-            outs.append((eng.flat.cpu(), eng.m.cpu(), eng.v.cpu(), float(eng.step.item()),
-                         float(p.last_loss)))
-    finally:
-        prl_native.dp_comm_destroy(comm)
-    (f0, m0, v0, s0, l0), (f1, m1, v1, s1, l1) = outs
-    assert torch.equal(f0, f1) and torch.equal(m0, m1) and torch.equal(v0, v1)
-    assert s0 == s1 == 3 * 6 and l0 == l1

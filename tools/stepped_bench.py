@@ -39,16 +39,10 @@ def _timed(fn):
 
 
 prl_native.ppo_update_dp = _timed(prl_native.ppo_update_dp)
-prl_native.ppo_update_dp_persistent = _timed(prl_native.ppo_update_dp_persistent)
 comm = prl_native.dp_comm_init(prl_native.dp_unique_id(), 1, 0)
 MODES = (("identity", lambda t: t, None, {}), ("rccl-1rank", dist.all_reduce, None, {}),
-         ("native-stepped-rccl-1rank", None, comm, {"PRL_DP_PERSISTENT": "0"}),
-         ("native-persistent-rccl-1rank", None, comm, {"PRL_DP_PERSISTENT": "1"}),
-         ("native-persistent-stand-in-kernel", None, comm,
-          {"PRL_DP_PERSISTENT": "1", "PRL_DP_STAND_IN": "1"}))
+         ("native-stepped-rccl-1rank", None, comm, {}))
 for label, ar, cm, env in MODES:
-    for key in ("PRL_DP_PERSISTENT", "PRL_DP_STAND_IN"):
-        os.environ.pop(key, None)
     os.environ.update(env)
     torch.manual_seed(0)
     p = PPO(False, 4, 2, lr=1e-3, k_epochs=k, batch_size=1, mini_batch_size=mb)
