@@ -12,19 +12,19 @@
 // tiny kernels; the graph-replayed PyTorch step costs ~180 us, almost all launch gaps.
 //
 // Decomposition (G workgroups of 256 threads, one per CU, co-resident: occupancy-checked plain launch):
-//   phase A  workgroup g takes rows [g*R, (g+1)*R) of the step's minibatch in chunks of RC = 8
-//            rows; forward + backward run out of LDS with the CURRENT parameters in LDS (every
+//   phase A  workgroup g takes rows [g*R, (g+1)*R) of the step's minibatch in 16-row tiles;
+//            forward + backward run out of LDS with the CURRENT parameters in LDS (every
 //            workgroup holds a full, bit-identical copy), accumulating this workgroup's partial
 //            gradient (and the loss partials) in LDS, then publishes it write-through (sc1
 //            16-B stores) to part[g] and bumps counter A;
 //   phase B  when all G partials are in, workgroup g sums its 1/G slice of the gradient over the
-//            G partials in workgroup order (deterministic), publishes the slice + its sum of
-//            squares (sc1) and bumps counter B;
-//   phase C  when all slices are in, EVERY workgroup reads the whole reduced gradient and the G
-//            squared-norm pieces (sc1 loads, same order everywhere), forms the clip coefficient
-//            and applies AdamW to its own copy of the parameters (LDS) and moments (a private
-//            global slab) — identical inputs, identical code, so every copy stays bit-identical
-//            and no parameter broadcast (third hand-off) is needed.
+//            G partials in workgroup order (deterministic), publishes the slice (sc1) and bumps
+//            counter B;
+//   phase C  when all slices are in, EVERY workgroup reads the whole reduced gradient (sc1
+//            loads), forms its squared norm in one fixed order and the clip coefficient, and
+//            applies AdamW to its own copy of the parameters (LDS) and moments (registers) —
+//            identical inputs, identical code, so every copy stays bit-identical and no
+//            parameter broadcast (third hand-off) is needed.
 // Hand-offs follow the MI355X guide's Guideline 16 (first row of the sc1 table): payload stored
 // sc1 and drained by every storing wave, one lane adds to the counter behind a workgroup
 // barrier, one lane polls it relaxed (bounded, s_sleep), every load of the payload is sc1.
@@ -1182,10 +1182,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     mark(2);   // wait A
     // ---- phase B: reduce this workgroup's slice over the G partials --------------------------
     {
-      float ssq = upd_slice_reduce(rs_part, rs_red, Qtot, Qp, g, G, scratch, NT);
-      // the slice's sum of squares as NW per-wave pieces (fixed DPP tree, lane 63 publishes)
-      ssq = wave_sum_f32_to63(ssq);
-      if ((t & 63) == 63) st_sc1f(args.sq + NW * g + (t >> 6), ssq);
+      (void)upd_slice_reduce(rs_part, rs_red, Qtot, Qp, g, G, scratch, NT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       mark(3);   // slice reduce
@@ -1207,12 +1204,23 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     }
     float clipc;
     {
-      // every wave of every workgroup sums the NW G pieces in the same order (no LDS, no barrier)
-      const int l = t & 63;
-      float piece = 0.f;
-      for (int i = l; i < NW * G; i += 64) piece += ld_sc1f(args.sq + i);
-      piece = wave_sum_f32_to63(piece);
-      const float tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(piece), 63));
+      // clip_grad_norm_'s norm from the reduced gradient this workgroup just loaded: per thread
+      // its quads in order, a fixed DPP tree per wave, the NW wave sums in wave order (LDS) — the
+      // same data, order and code in every workgroup, so every copy forms the same coefficient.
+      // (Round 1 summed per-slice pieces published by the slice owners instead: those 4-B words,
+      // eight workgroups' to a 128-B line, were read stale on some runs — a wrong clip
+      // coefficient, run-to-run differences; tools/exp/engine_determinism4.py.)
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i)
+        if (t + i * NT < Qp) acc += (gq[i].x * gq[i].x + gq[i].y * gq[i].y) + (gq[i].z * gq[i].z + gq[i].w * gq[i].w);
+      acc = wave_sum_f32_to63(acc);
+      float* s_nrm = hdr + 4;   // [NW]
+      if ((t & 63) == 63) s_nrm[t >> 6] = acc;
+      __syncthreads();
+      float tot = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) tot += s_nrm[w];
       const float coef = args.max_norm / (sqrtf(tot) + 1e-6f);
       clipc = coef < 1.0f ? coef : 1.0f;
       if (g == 0 && t == 0 && s + 1 == args.total_steps) {

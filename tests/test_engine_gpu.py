@@ -496,3 +496,37 @@ def test_folded_step_equals_grad_then_adam(cont, D, A):
     assert float(p._engine.step.item()) == 2 * 5
 
 
+
+
+@pytest.mark.parametrize("cont", [False, True])
+def test_engine_bit_reproducible(cont):
+    """The persistent engine is deterministic: learn() from the same seed and memory gives the
+    same bits twice, and re-running the engine from a restored state on learn()'s own inputs
+    (workspace refilled by a plain-store kernel in between) gives them again.  Round 1's engine
+    failed this: its clip coefficient came from 4-B norm pieces that workgroups sometimes read
+    stale (tools/exp/engine_determinism4.py); the norm is now formed from the reduced gradient."""
+    from PPO import PPO
+    N = 512 * 24 + 7
+    data = _data(N, 3 if cont else 4, cont, seed=41)
+    D, A = (3, 1) if cont else (4, 2)
+    flats = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        p = PPO(cont, D, A, action_scaling=2.0 if cont else None, k_epochs=3, batch_size=64,
+                mini_batch_size=512)
+        p.show_progress = False
+        eng = p._fused_engine()
+        init = [eng.flat.clone(), eng.m.clone(), eng.v.clone(), eng.step.clone()]
+        p.memory.push_device(*data)
+        p.learn()
+        torch.cuda.synchronize()
+        flats.append(eng.flat.cpu().clone())
+    assert torch.equal(flats[0], flats[1])
+    ins = [x.clone() for x in p._last_update_inputs]
+    for _ in range(3):
+        for dst, src in zip((eng.flat, eng.m, eng.v, eng.step), init):
+            dst.copy_(src)
+        eng.ws.fill_(0)
+        eng.run(*ins, 3)
+        torch.cuda.synchronize()
+        assert torch.equal(eng.flat.cpu(), flats[0])
