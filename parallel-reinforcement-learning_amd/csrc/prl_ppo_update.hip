@@ -272,15 +272,24 @@ __host__ __device__ inline int upd_scratch_floats(int D, int NW) {
          + NW * UPD_RT * 16          // Os  [NW][16][16]   assembled outputs per wave
          + NW * UPD_RT * 16          // dOs [NW][16][16]   d loss / d outputs per wave
          + UPD_RT * UPD_RIN          // Rin [16][12]       row inputs
-         + UPD_RT * UPD_ZS           // Fs  [16][80]       trunk output
+         + 2 * UPD_RT * UPD_ZS       // Fs  [2][16][80]    trunk output (double-buffered by tile)
          + UPD_MAXH * UPD_RT * UPD_ZS  // Zs [h][16][80]   head dZ
          + NW * UPD_RT * 16          // Ts  [NW][16][16]   per-wave transpose slot (G_h, dH0)
          + 16;
 }
 struct UpdScr {
   float *Xs, *Op, *Os, *dOs, *Rin, *Fs, *Zs, *Ts;
+  float* Fs2;   // the other trunk-output buffer: consecutive tiles of a step alternate (a tile's
+                // forward writes Fs before any barrier, while a slower wave may still read the
+                // previous tile's after that tile's barrier #2)
   int XS;
 };
+// the scratch view of the step's tile number c (odd tiles use the second trunk-output buffer)
+__device__ inline UpdScr upd_scr_tile(const UpdScr& s, int c) {
+  UpdScr r = s;
+  if (c & 1) r.Fs = s.Fs2;
+  return r;
+}
 __device__ inline UpdScr upd_scr(float* p, int D, int NW) {
   UpdScr s;
   s.XS = upd_xs(D);
@@ -290,6 +299,7 @@ __device__ inline UpdScr upd_scr(float* p, int D, int NW) {
   s.dOs = p; p += NW * UPD_RT * 16;
   s.Rin = p; p += UPD_RT * UPD_RIN;
   s.Fs = p; p += UPD_RT * UPD_ZS;
+  s.Fs2 = p; p += UPD_RT * UPD_ZS;
   s.Zs = p; p += UPD_MAXH * UPD_RT * UPD_ZS;
   s.Ts = p;
   return s;
@@ -623,12 +633,13 @@ __device__ inline void upd_tile_fwd(const UpdNet& n, const float* W, const UpdSc
   const int b = w & 3, hg = w >> 2;
   const int D = n.D, KS = (D + 3) >> 2;
   const int nh = upd_nh<KD>(n);
-  // trunk: H0^T block bb = W0[16bb .. 16bb+15][:] X^T  (A: W0 rows, B: inputs), then GN + SiLU
+  // trunk: H0^T block b = W0[16b .. 16b+15][:] X^T  (A: W0 rows, B: inputs), then GN + SiLU —
+  // this wave's block only; the four blocks meet in Fs (rows x channels) behind a barrier, and
+  // every wave reads all of them back as the heads' B operand (one 16-B read per block)
   upd_v4 F[4];
-#pragma unroll
-  for (int bb = 0; bb < 4; ++bb) {
+  {
     upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* wr = W + n.w0.lds + (16 * bb + x) * n.w0.stride;
+    const float* wr = W + n.w0.lds + (16 * b + x) * n.w0.stride;
 #pragma unroll
     for (int s = 0; s < KSM; ++s) {
       if (s < KS) {
@@ -636,16 +647,13 @@ __device__ inline void upd_tile_fwd(const UpdNet& n, const float* W, const UpdSc
         acc = upd_mma(d < D ? wr[d] : 0.0f, in.xin[s], acc);
       }
     }
-    upd_v4 xh;
-    float rs;
-    upd_gn_fwd_frag(acc, upd_ld4(W + n.g0.lds + 16 * bb + 4 * q), upd_ld4(W + n.b0.lds + 16 * bb + 4 * q),
-                    xh, rs, F[bb]);
-    if (bb == b) {
-      f.xh0 = xh;
-      f.r0 = rs;
-      f.Fw = F[bb];
-    }
+    upd_gn_fwd_frag(acc, upd_ld4(W + n.g0.lds + 16 * b + 4 * q), upd_ld4(W + n.b0.lds + 16 * b + 4 * q),
+                    f.xh0, f.r0, f.Fw);
+    if (hg == 0) upd_st4(sc.Fs + x * UPD_ZS + 16 * b + 4 * q, f.Fw);
   }
+  __syncthreads();   // #0: Fs
+#pragma unroll
+  for (int bb = 0; bb < 4; ++bb) F[bb] = upd_ld4(sc.Fs + x * UPD_ZS + 16 * bb + 4 * q);
   // heads: Z_h^T block b = W1_h[16b ..][:] F^T; K order per step (bb, i): lane q <-> input
   // channel 16 bb + 4 q + i, so F's C fragments are the B operand as they stand
   upd_v4 z[HPW];
@@ -823,8 +831,7 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
       upd_wave_sync();   // Tw reads done before the next head overwrites it
     }
   }
-  // trunk output and inputs, rows x channels, for the weight gradients
-  if (hg == 0) upd_st4(sc.Fs + x * UPD_ZS + 16 * b + 4 * q, f.Fw);
+  // inputs, rows x channels, for the weight gradients (the trunk output is in Fs already)
 #pragma unroll
   for (int s = 0; s < KSM; ++s)
     if (s < KS && (s % NW) == w) sc.Xs[x * sc.XS + 4 * s + q] = in.xin[s];
@@ -1140,10 +1147,10 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
         upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
                               myrow0 + c0 + UPD_RT, std::min(UPD_RT, myrows - c0 - UPD_RT), nin);
       if (c0 == 0)
-        upd_tile<KD, KA, true>(n, args, W, Ga, sc, cur, std::min(UPD_RT, myrows - c0), invB,
+        upd_tile<KD, KA, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0), invB,
                                reinterpret_cast<unsigned long long*>(hdr + 16));
       else
-        upd_tile<KD, KA, false>(n, args, W, Ga, sc, cur, std::min(UPD_RT, myrows - c0), invB,
+        upd_tile<KD, KA, false>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0), invB,
                                 reinterpret_cast<unsigned long long*>(hdr + 16));
     }
     __syncthreads();
@@ -1473,8 +1480,8 @@ __device__ __forceinline__ void ppo_grad_body(const UpdNet& n, const UpdArgs& ar
     UpdIn<upd_ksm<KA>()> in;
     upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
                           row0 + (int64_t)g * R + c0, rc, in);
-    if (c0 == 0) upd_tile<KD, KA, true>(n, args, W, Ga, sc, in, rc, inv_count, tm);
-    else upd_tile<KD, KA, false>(n, args, W, Ga, sc, in, rc, inv_count, tm);
+    if (c0 == 0) upd_tile<KD, KA, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), in, rc, inv_count, tm);
+    else upd_tile<KD, KA, false>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), in, rc, inv_count, tm);
   }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(grad_out);
