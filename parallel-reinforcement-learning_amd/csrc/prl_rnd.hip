@@ -16,6 +16,10 @@
 // row norms never leave the chip.  FLOPs per row: 512 * D (both nets, both layers).
 #include "prl_common.h"
 
+#include <stdlib.h>
+
+#include <algorithm>
+
 namespace prl {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
@@ -154,6 +158,208 @@ __global__ __launch_bounds__(256) void rnd_forward_kernel(const float* __restric
   if (tid < RB_M && row0 + tid < n) out[row0 + tid] = beta * sqrtf(s_rowsq[0][tid] + s_rowsq[1][tid]);
 }
 
+
+// ---- the persistent fast path (D % 4 == 0: 16-B row loads) -----------------------------------
+// Each workgroup (4 waves, one per SIMD, one workgroup per CU) loops over 128-row blocks.  The
+// first kernel above re-staged both nets' weights (~356 KB at D = 348) through LDS with 4-B
+// loads and two barriers per 64-row block, ~4x the bytes of its own rows; here the weights are
+// streamed per 128-row block in double-buffered chunks with 16-B loads (the next chunk in
+// registers while the current one feeds the MFMAs, one barrier per chunk), so every LDS fragment
+// read feeds 2-4 MFMAs and the weight traffic per row halves.
+//   layer 1: H[128 x 128] = X . [W1_target ; W1_pred]^T, K = D in 32-deep chunks; wave w owns
+//            rows 32w .. 32w+31 and all 128 hidden units (4 accumulators of 32 x 32);
+//   bias + GroupNorm + SiLU on the accumulators (a group = 8 consecutive lanes: DPP sums), into
+//            Z = [S_pred | -S_target] (LDS, 128 x 128);
+//   layer 2: Yp - Yt = Z . [W2_pred^T ; W2_target^T] + (b2_pred - b2_target) in 64-column chunks
+//            (2 accumulators per wave), squares accumulated per lane across all chunks and
+//            reduced over the 32 column lanes once per block.
+constexpr int RF_M = 128;         // rows per block
+constexpr int RF_KC = 32;         // layer-1 K chunk
+constexpr int RF_P1 = RF_KC + 4;  // pitch of the X / W1 chunks (16-B rows: ds_write_b128 staging;
+                                  // column reads see at most a 2-way bank conflict)
+constexpr int RF_CC = 64;         // layer-2 column chunk
+constexpr int RF_PZ = 129;        // pitch of Z (odd: conflict-free row-fragment reads)
+constexpr int RF_PW = 132;        // pitch of the W2 chunk (16-B rows)
+constexpr int RF_STAGE = 2 * 2 * RF_M * RF_P1;          // layer-1 double buffer: [2][X | W1]
+constexpr int RF_STAGE2 = 2 * RF_CC * RF_PW;            // layer-2 double buffer: [2][64][132]
+constexpr int RF_LDS = (RF_STAGE > RF_STAGE2 ? RF_STAGE : RF_STAGE2) + RF_M * RF_PZ + 2 * RF_M;
+
+// sum over the 8 consecutive lanes of a GroupNorm group (every lane gets the same bits)
+__device__ inline float rf_sum8(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));   // xor 1
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));   // xor 2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));  // half mirror
+  return v;
+}
+
+struct RfChunk {
+  float4 v[8];
+};
+// layer-1 chunk c of block rows [row0, row0 + 128): X[128][32] and [W1_t ; W1_p][128][32], thread
+// tid takes float4 slots tid + 256 i (i < 4) of each (row = slot >> 3, quad = slot & 7)
+__device__ inline void rf_load1(RfChunk& ch, const float* x, int64_t n, int D, int64_t row0, int k0,
+                                const float* wt, const float* wp) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int slot = tid + 256 * i, r = slot >> 3, k = k0 + 4 * (slot & 7);
+    const bool kin = k < D;
+    ch.v[i] = (kin && row0 + r < n) ? *reinterpret_cast<const float4*>(x + (row0 + r) * D + k)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* W = r < 64 ? wt : wp;
+    ch.v[4 + i] = kin ? *reinterpret_cast<const float4*>(W + (r & 63) * D + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+__device__ inline void rf_store1(const RfChunk& ch, float* buf) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int slot = tid + 256 * (i & 3), r = slot >> 3, k = 4 * (slot & 7);
+    *reinterpret_cast<float4*>(buf + (i >> 2) * RF_M * RF_P1 + r * RF_P1 + k) = ch.v[i];
+  }
+}
+// layer-2 chunk of output columns [col0, col0 + 64): W2cat[k][col] = k < 64 ? W2_p[col][k] :
+// W2_t[col][k - 64], stored [col][k]; thread tid takes slots tid + 256 i (i < 8): col = slot >> 5,
+// k = 4 (slot & 31)
+__device__ inline void rf_load2(RfChunk& ch, int D, int col0, const float* w2t, const float* w2p) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int slot = tid + 256 * i, c = slot >> 5, k = 4 * (slot & 31), col = col0 + c;
+    const float* W = k < 64 ? w2p : w2t;
+    ch.v[i] = col < D ? *reinterpret_cast<const float4*>(W + col * 64 + (k & 63)) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+__device__ inline void rf_store2(const RfChunk& ch, float* buf) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int slot = tid + 256 * i, c = slot >> 5, k = 4 * (slot & 31);
+    *reinterpret_cast<float4*>(buf + c * RF_PW + k) = ch.v[i];
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void rnd_forward_fast_kernel(const float* __restrict__ x, int64_t n,
+                                                                  int D, RndNet tn, RndNet pn, float beta,
+                                                                  float* __restrict__ out) {
+  extern __shared__ __align__(16) float rf_lds[];
+  float* stage = rf_lds;                                                       // layer 1 / 2 chunks
+  float* zs = rf_lds + (RF_STAGE > RF_STAGE2 ? RF_STAGE : RF_STAGE2);          // Z [128][129]
+  float* rsq = zs + RF_M * RF_PZ;                                              // [2][128]
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lr = lane & 31, lh = lane >> 5;
+  const int64_t nblocks = (n + RF_M - 1) / RF_M;
+  const int nk = (D + RF_KC - 1) / RF_KC, nc = (D + RF_CC - 1) / RF_CC;
+  // per-lane constants of the GroupNorm epilogue: hidden unit u = 32 j + lr of net (j >> 1)
+  RfChunk ch;   // the next chunk to stage, in registers (loaded one chunk ahead, also across the
+                // layer and block boundaries)
+  if ((int64_t)blockIdx.x < nblocks) rf_load1(ch, x, n, D, (int64_t)blockIdx.x * RF_M, 0, tn.w1, pn.w1);
+  for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    const int64_t row0 = blk * RF_M;
+    const bool more = blk + gridDim.x < nblocks;
+    // ---- layer 1 ----
+    f32x16 acc[4] = {};
+    rf_store1(ch, stage);
+    __syncthreads();
+    for (int c = 0; c < nk; ++c) {
+      if (c + 1 < nk) rf_load1(ch, x, n, D, row0, (c + 1) * RF_KC, tn.w1, pn.w1);
+      else rf_load2(ch, D, 0, tn.w2, pn.w2);   // layer 2's first chunk
+      const float* bx = stage + (c & 1) * 2 * RF_M * RF_P1;
+      const float* ax = bx + (32 * w + lr) * RF_P1 + lh;
+      const float* bw = bx + RF_M * RF_P1 + lr * RF_P1 + lh;
+      // every fragment of the chunk read up front (80 VGPRs): the MFMA chain then waits only on
+      // the first reads, instead of a read-wait bubble per k-pair at one wave per SIMD
+      float av[RF_KC / 2], bv[4][RF_KC / 2];
+#pragma unroll
+      for (int k = 0; k < RF_KC / 2; ++k) {
+        av[k] = ax[2 * k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bv[j][k] = bw[32 * j * RF_P1 + 2 * k];
+      }
+#pragma unroll
+      for (int k = 0; k < RF_KC / 2; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[k], bv[j][k], acc[j], 0, 0, 0);
+      if (c + 1 < nk) rf_store1(ch, stage + ((c + 1) & 1) * 2 * RF_M * RF_P1);
+      __syncthreads();
+    }
+    // ---- bias + GroupNorm(8 x 8) + SiLU, into Z = [S_pred | -S_target] ----
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const RndNet& nn = j < 2 ? tn : pn;
+      const int u = 32 * (j & 1) + lr;
+      const float bb = nn.b1[u], gw = nn.gw[u], gb = nn.gb[u];
+      const int zc = (j < 2 ? 64 : 0) + u;
+      const float sgn = j < 2 ? -1.0f : 1.0f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float v = acc[j][i] + bb;
+        const float mean = rf_sum8(v) * 0.125f;
+        const float d = v - mean;
+        const float var = rf_sum8(d * d) * 0.125f;
+        // hardware rsq / exp / rcp (~1 ulp each; the reward is checked at 2e-5 rel): IEEE
+        // division and libm expf cost ~40 VALU per value here, 64 values per lane per block
+        const float y = d * __builtin_amdgcn_rsqf(var + 1e-5f) * gw + gb;
+        zs[(32 * w + c_row(i, lane)) * RF_PZ + zc] = sgn * (y * __builtin_amdgcn_rcpf(1.0f + __expf(-y)));
+      }
+    }
+    // ---- layer 2 + squared differences ----
+    float rowsq[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) rowsq[i] = 0.f;
+    rf_store2(ch, stage);
+    __syncthreads();   // Z and the first W2 chunk
+    for (int c = 0; c < nc; ++c) {
+      if (c + 1 < nc) rf_load2(ch, D, (c + 1) * RF_CC, tn.w2, pn.w2);
+      else if (more) rf_load1(ch, x, n, D, (blk + gridDim.x) * RF_M, 0, tn.w1, pn.w1);   // next block
+      const float* bw2 = stage + (c & 1) * RF_CC * RF_PW;
+      const float* az = zs + (32 * w + lr) * RF_PZ + lh;
+      const float* b0 = bw2 + lr * RF_PW + lh;
+      f32x16 y0 = {}, y1 = {};
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 32) {   // fragments 16 k-steps at a time, read up front
+        float a[16], c0[16], c1[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          a[k] = az[k0 + 2 * k];
+          c0[k] = b0[k0 + 2 * k];
+          c1[k] = b0[32 * RF_PW + k0 + 2 * k];
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k], c0[k], y0, 0, 0, 0);
+          y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k], c1[k], y1, 0, 0, 0);
+        }
+      }
+      const int col_a = c * RF_CC + lr, col_b = col_a + 32;
+      const float bd_a = col_a < D ? pn.b2[col_a] - tn.b2[col_a] : 0.f;
+      const float bd_b = col_b < D ? pn.b2[col_b] - tn.b2[col_b] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float va = col_a < D ? y0[i] + bd_a : 0.f;
+        const float vb = col_b < D ? y1[i] + bd_b : 0.f;
+        rowsq[i] += va * va + vb * vb;
+      }
+      if (c + 1 < nc) rf_store2(ch, stage + ((c + 1) & 1) * RF_CC * RF_PW);
+      __syncthreads();
+    }
+    // ---- reduce over the 32 column lanes of each half-wave, write beta * sqrt ----
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float v = rowsq[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+      v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+      v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+      v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));
+      if (lr == 0) rsq[32 * w + c_row(i, lane)] = v;
+    }
+    __syncthreads();
+    if (tid < RF_M && row0 + tid < n) out[row0 + tid] = beta * sqrtf(rsq[tid]);
+    // (the next block stages into `stage` first: the loop's last barrier has passed every read of
+    // it; rsq is rewritten only after that block's own barriers)
+  }
+}
+
 }  // namespace prl
 
 using namespace prl;
@@ -171,8 +377,28 @@ extern "C" int prl_rnd_forward(const float* x, int64_t n, int32_t D, const float
               "prl_rnd_forward: null pointer");
   PRL_REQUIRE(cdiv(n, RB_M) < (int64_t)0x7fffffff, "prl_rnd_forward: n too large");
   RndNet tn{t_w1, t_b1, t_gw, t_gb, t_w2, t_b2}, pn{p_w1, p_b1, p_gw, p_gb, p_w2, p_b2};
-  hipLaunchKernelGGL(rnd_forward_kernel, dim3((unsigned)cdiv(n, RB_M)), dim3(256), 0,
-                     as_stream(stream), x, n, (int)D, tn, pn, beta, out);
+  hipStream_t st = as_stream(stream);
+  const bool fast = (D % 4) == 0 && aligned16(x) && aligned16(t_w1) && aligned16(p_w1) &&
+                    aligned16(t_w2) && aligned16(p_w2) && getenv("PRL_RND_GENERIC") == nullptr;
+  if (fast) {
+    // persistent: one workgroup per CU (LDS-bound), each over its share of 128-row blocks
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      PRL_HIP_TRY(hipGetDevice(&dev));
+      PRL_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(rnd_forward_fast_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(RF_LDS * sizeof(float))));
+    }
+    const int64_t nblocks = cdiv(n, RF_M);
+    const unsigned grid = (unsigned)std::min<int64_t>(nblocks, cus);
+    hipLaunchKernelGGL(rnd_forward_fast_kernel, dim3(grid), dim3(256), RF_LDS * sizeof(float), st, x, n,
+                       (int)D, tn, pn, beta, out);
+    PRL_LAUNCH_CHECK("rnd_forward_fast");
+    return PRL_OK;
+  }
+  hipLaunchKernelGGL(rnd_forward_kernel, dim3((unsigned)cdiv(n, RB_M)), dim3(256), 0, st, x, n, (int)D,
+                     tn, pn, beta, out);
   PRL_LAUNCH_CHECK("rnd_forward");
   return PRL_OK;
 }

@@ -212,6 +212,33 @@ def test_rnd_forward_ragged_rows():
                                    rtol=3e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("D,n", [(348, 70001), (348, 257), (12, 33000), (4, 1)])
+def test_rnd_forward_persistent_blocks(D, n, monkeypatch):
+    """The persistent fast kernel (D % 4 == 0: 128-row blocks, every workgroup looping over
+    several when n > 128 x CUs, chunks prefetched across the layer and block boundaries) against
+    the oracle on a row subset and against the round-1 kernel (PRL_RND_GENERIC=1) on all rows."""
+    N = native()
+    rng = np.random.default_rng(D + n)
+    nets_np, nets = [], []
+    for _ in range(2):
+        p = dict(w1=rng.normal(0, .1, (64, D)), b1=rng.normal(0, .01, 64), gw=rng.normal(1, .1, 64),
+                 gb=rng.normal(0, .1, 64), w2=rng.normal(0, .1, (D, 64)), b2=rng.normal(0, .01, D))
+        p = {k: v.astype(np.float32) for k, v in p.items()}
+        nets_np.append(p)
+        nets.append([T(p[k]) for k in ("w1", "b1", "gw", "gb", "w2", "b2")])
+    x = rng.normal(size=(n, D)).astype(np.float32)
+    fast = torch.empty(n, dtype=torch.float32, device=DEV)
+    N.rnd_forward(T(x), nets[0], nets[1], 0.001, fast)
+    monkeypatch.setenv("PRL_RND_GENERIC", "1")
+    gen = torch.empty(n, dtype=torch.float32, device=DEV)
+    N.rnd_forward(T(x), nets[0], nets[1], 0.001, gen)
+    f, gn = fast.cpu().numpy(), gen.cpu().numpy()
+    np.testing.assert_allclose(f, gn, rtol=2e-5, atol=1e-9)
+    sub = np.unique(np.r_[np.arange(0, n, max(1, n // 997)), n - 1])
+    np.testing.assert_allclose(f[sub], O.rnd_forward(x[sub], nets_np[0], nets_np[1], 0.001),
+                               rtol=2e-5, atol=1e-9)
+
+
 # ---------------------------------------------------------------------------------- envs
 def _make_env_state(kind, E, seeds, D):
     N = native()
