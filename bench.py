@@ -245,6 +245,9 @@ def main():
     for name in ("adv_normalize", "surrogate_fwd", "surrogate_bwd"):
         setattr(ppo._ops, name, getattr(prl_native, name))
     ppo._ops.gae = gae_call
+    # ... and the RND forward's (RND.compute_intrinsic_reward calls prl_native.rnd_forward)
+    rnd_call = LastCall(prl_native.rnd_forward)
+    prl_native.rnd_forward = rnd_call
 
     def iteration():
         t0 = time.perf_counter()
@@ -341,6 +344,23 @@ def main():
                     "transitions_per_launch": int(n_gae),
                     "bytes_per_transition": GAE_BYTES_PER_TRANSITION}
 
+    roofline_rnd = None
+    if rnd_call.args is not None:
+        a, k = rnd_call.args
+        n_rnd, D_rnd = int(a[0].shape[0]), int(a[0].shape[1])
+        f = rnd_call.fn
+        cold_med, _ = time_kernel(lambda: f(*a, **k), cold=True)
+        warm_med, _ = time_kernel(lambda: f(*a, **k), cold=False)
+        flops = 512.0 * D_rnd * n_rnd     # both nets, both layers
+        ach = flops / (cold_med * 1e-3) / 1e12
+        roofline_rnd = {"kernel": "prl_rnd_forward: rnd_forward_fast_kernel (persistent, both nets, "
+                                  "f32 MFMA)",
+                        "bound": "mfma", "achieved": round(ach, 2), "peak": F32_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(ach / F32_PEAK_TFLOPS, 4), "traffic": None,
+                        "avg_launch_us": round(cold_med * 1e3, 2), "cache": "cold (512 MiB read-only flush)",
+                        "warm_launch_us": round(warm_med * 1e3, 2), "rows_per_launch": n_rnd,
+                        "D": D_rnd, "flops_per_row": 512 * D_rnd}
+
     roofline_env = None
     if cfg["env"] in ENV_STEP_BYTES and runner._traj is not None:
         env, tr, spec_ = runner.env, runner._traj, runner.env.spec
@@ -422,6 +442,7 @@ def main():
             "roofline": roofline,
             "roofline_gae": roofline_gae,
             "roofline_env": roofline_env,
+            "roofline_rnd": roofline_rnd,
             "learn_fixed_2p20": fixed,
             "cpu_baseline": cpu,
         }
