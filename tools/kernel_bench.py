@@ -95,7 +95,11 @@ if __name__ == "__main__":
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--gae-n", type=int, default=0, help="only the GAE scan at this size")
     ap.add_argument("--gae-file", default=None, help="only the GAE scan on bench.py --dump-gae")
+    ap.add_argument("--env-e", type=int, default=0, help="only the CartPole rollout step at E envs")
     a = ap.parse_args()
+    if a.env_e:
+        print(json.dumps(cartpole_step_case(a.env_e, reps=a.reps)), flush=True)
+        sys.exit(0)
     if a.gae_file:
         print(json.dumps(gae_file_case(a.gae_file, reps=a.reps)), flush=True)
         sys.exit(0)
