@@ -107,8 +107,8 @@ class FusedUpdate:
         trunk, heads, outs = self.D * H, nh * H * H, nout * H
         return 2 * (trunk + heads + outs) * 2 + 2 * (heads + outs)
 
-    PHASES = ("forward+backward", "publish", "gather partials", "slice reduce", "gather reduced",
-              "norm", "AdamW")
+    PHASES = ("forward+backward", "publish", "wait A", "slice reduce", "wait B", "norm",
+              "AdamW")
 
     CHUNK_STAGES = ("forward", "barrier 1", "loss", "heads bwd + dW2", "barrier 2", "dW1",
                     "dF + trunk bwd", "dW0 + biases")
