@@ -19,16 +19,16 @@
 // Work decomposition (single pass, ONE launch, no host-side memset):
 //   * tile = 256 threads x 8 consecutive elements = 2048 elements, 16-B vector loads; delta_t and
 //     c_t are formed elementwise and staged in LDS;
-//   * each thread finishes everything at or left of the LAST break in its own chunk, then
-//     resolves its tail from the nearest chunk to the right that has a break (LDS), re-evaluating
-//     break-free chunks in between sequentially;
-//   * workgroup b owns tile ntiles-1-b (reverse), so a tile's successor is normally already
-//     running.  A tile publishes its carry-out g[first element] as one 8-byte {epoch, value}
-//     granule with one agent-scope store (data = flag, MI355X guide Guideline 16 R2) as soon as
-//     it is known, before it ever waits.  A tile whose tail runs into the next tile polls that
-//     granule for a bounded time; if it does not appear (the successor was not dispatched yet —
-//     HIP promises no dispatch order), the tile computes the carry itself by look-ahead: the same
-//     sequential chain over the successor's head segment, so the result is bit-identical and
+//   * each thread finishes everything at or left of the LAST break in its own chunk; the carries
+//     between chunks are chained once per RUN of break-free chunks (gae_kernel), the runs listed
+//     in LDS and walked by the lowest threads, packed into the fewest waves;
+//   * tiles are taken in reverse, in R interleaved streams (gae_kernel): a tile's successor was
+//     dispatched one round of resident workgroups earlier.  A tile publishes its carry-out
+//     g[first element] as one 8-byte {epoch, value} granule with one agent-scope store (data =
+//     flag, MI355X guide Guideline 16 R2) as soon as it is known, before it ever waits; the tile
+//     to its left reads it.  A stream's first tile computes its successor's carry itself (that
+//     tile runs last); a tile that still finds no granule after a bounded poll computes the carry
+//     by a scalar look-ahead — the same sequential chain, so the result is bit-identical and
 //     correctness never depends on placement or order.  No ticket atomic: a single contended word
 //     caps at ~88 ops/us on MI355X (guide: dequeue row), i.e. ~73 us at 6400 tiles.
 //   * statistics: when adv is requested each tile stores {sum adv, sum adv^2} (f64) to its slot;
@@ -46,6 +46,9 @@ namespace prl {
 // file); empty in the product build.
 #ifndef PRL_GAE_MARK
 #define PRL_GAE_MARK(i)
+#endif
+#ifndef PRL_GAE_MARK_TAIL   // same, recorded by the tail-run thread (255)
+#define PRL_GAE_MARK_TAIL(i)
 #endif
 
 constexpr int GAE_THREADS = 256;
@@ -222,29 +225,20 @@ __device__ inline unsigned gae_tag(const GaeWs& ws) {
   return t ? t : 1u;
 }
 
+// Stage one tile: load its r / d / V (16-B vector loads when aligned and full), form delta_t and
+// c_t in the reference's order into LDS, run every chunk's recurrence at or left of its last
+// break, and publish the wave's break ballot to s_mask; g0 = g at the chunk's first element
+// when it has a break (pb >= 0).  No barrier inside.
 template <bool VEC>
-__global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
-    const float* __restrict__ r, const float* __restrict__ d, const float* __restrict__ V,
-    const float* __restrict__ next_value, int64_t n, float gf, float glf, float* __restrict__ ret,
-    float* __restrict__ adv, GaeWs ws, int64_t ntiles, double* __restrict__ sums_out) {
-  __shared__ __attribute__((aligned(16))) float s_delta[GAE_TILE];
-  __shared__ __attribute__((aligned(16))) float s_c[GAE_TILE];
-  __shared__ float s_out[GAE_THREADS];
-  __shared__ unsigned long long s_mask[GAE_THREADS / 64];
-  __shared__ float s_cin[GAE_THREADS];
-  __shared__ unsigned s_tag;
-
+__device__ inline void gae_stage(const float* __restrict__ r, const float* __restrict__ d,
+                                 const float* __restrict__ V, int64_t n, float nv_end, float gf,
+                                 float glf, int64_t tile, float* s_delta, float* s_c,
+                                 unsigned long long* s_mask, float (&vv)[GAE_EPT],
+                                 float& g0, int& pb) {
   const int tid = threadIdx.x;
-  PRL_GAE_MARK(0);
-  if (tid == 0) {
-    s_tag = gae_tag(ws);
-  }
-  const int64_t tile = ntiles - 1 - (int64_t)blockIdx.x;
   const int64_t i0 = tile * GAE_TILE + (int64_t)tid * GAE_EPT;
-
-  float rr[GAE_EPT], dd[GAE_EPT], vv[GAE_EPT];
-  const bool full = (i0 + GAE_EPT <= n);
-  if (VEC && full) {
+  float rr[GAE_EPT], dd[GAE_EPT];
+  if (VEC && i0 + GAE_EPT <= n) {
     const float4* r4 = reinterpret_cast<const float4*>(r + i0);
     const float4* d4 = reinterpret_cast<const float4*>(d + i0);
     const float4* v4 = reinterpret_cast<const float4*>(V + i0);
@@ -263,11 +257,8 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
     }
   }
   PRL_GAE_MARK(1);
-  // nv for the final element (PPO.py:188: next_value = V[-1]) and for this chunk's last element
-  const float nv_end = next_value ? *next_value : V[n - 1];
   const int64_t inext = i0 + GAE_EPT;
   const float vnext = (inext < n) ? V[inext] : nv_end;
-
   float dl[GAE_EPT], cc[GAE_EPT];
 #pragma unroll
   for (int k = 0; k < GAE_EPT; ++k) {
@@ -285,27 +276,93 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
     sc4[0] = float4{cc[0], cc[1], cc[2], cc[3]};
     sc4[1] = float4{cc[4], cc[5], cc[6], cc[7]};
   }
-  // local phase: everything at or left of the last break of this chunk
-  int pb = -1;
+  pb = -1;
 #pragma unroll
   for (int k = 0; k < GAE_EPT; ++k)
     if (cc[k] == 0.0f) pb = k;
-  float g[GAE_EPT];
-  {
-    float gg = 0.0f;
+  float gg = 0.0f;
 #pragma unroll
-    for (int k = GAE_EPT - 1; k >= 0; --k) {
-      if (k <= pb) {
-        gg = dl[k] + cc[k] * gg;
-        g[k] = gg;
+  for (int k = GAE_EPT - 1; k >= 0; --k)
+    if (k <= pb) gg = dl[k] + cc[k] * gg;
+  g0 = gg;
+  const unsigned long long bal = __ballot(pb >= 0);   // chunks of this wave with a break
+  if ((tid & 63) == 0) s_mask[tid >> 6] = bal;
+}
+
+// Tile order.  Dispatch index b runs tile ntiles-1-t', t' = (b % R) * Q + b / R: R streams of
+// Q consecutive tiles each, stream r's tiles one ROUND (R dispatches) apart.  A tile's successor
+// (the tile to its right, whose carry-out it needs) was therefore dispatched a round earlier and
+// has normally published long before — with t' = b the successor was the block dispatched just
+// before, still walking its own first run, so every tile waited out a whole run (trained
+// CartPole: 500 steps) before its tail walk could start.  A stream's first tile (q = 0) has its
+// successor at the END of the order; it computes that carry itself: it stages the successor tile
+// first and walks its first run (bit-identical to what the successor publishes).
+template <bool VEC>
+__global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
+    const float* __restrict__ r, const float* __restrict__ d, const float* __restrict__ V,
+    const float* __restrict__ next_value, int64_t n, float gf, float glf, float* __restrict__ ret,
+    float* __restrict__ adv, GaeWs ws, int64_t ntiles, int64_t R, int64_t Q,
+    double* __restrict__ sums_out) {
+  __shared__ __attribute__((aligned(16))) float s_delta[GAE_TILE];
+  __shared__ __attribute__((aligned(16))) float s_c[GAE_TILE];
+  __shared__ unsigned long long s_mask[GAE_THREADS / 64];
+  __shared__ float s_cin[GAE_THREADS];
+  __shared__ float s_pre;
+  __shared__ int s_run_hi[GAE_THREADS], s_run_lo[GAE_THREADS];   // the tile's runs (below)
+  __shared__ float s_run_g[GAE_THREADS];
+  __shared__ unsigned s_tag;
+
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int64_t q = b / R;
+  const int64_t tp = (b - q * R) * Q + q;
+  if (tp >= ntiles) return;   // past the last stream's end (the whole block: no barrier yet)
+  const int64_t tile = ntiles - 1 - tp;
+  const int64_t i0 = tile * GAE_TILE + (int64_t)tid * GAE_EPT;
+  PRL_GAE_MARK(0);
+  if (tid == 0) s_tag = gae_tag(ws);
+  // nv for the final element (PPO.py:188: next_value = V[-1])
+  const float nv_end = next_value ? *next_value : V[n - 1];
+  const bool has_succ = tile + 1 < ntiles;
+  const bool pre = has_succ && q == 0;   // the successor is run at the end: compute its carry
+  float vv[GAE_EPT], g0;
+  int pb;
+  if (pre) {
+    // stage tiles tile+1, tile+2, ... until one has a break (normally the first): its first run
+    // gives its carry-out; then every break-free tile back to tile+1 is walked whole
+    int64_t tb = tile + 1;
+    int F = -1;   // first chunk of tile tb with a break
+    for (;;) {
+      gae_stage<VEC>(r, d, V, n, nv_end, gf, glf, tb, s_delta, s_c, s_mask, vv, g0, pb);
+      __syncthreads();
+      for (int w2 = 0; w2 < GAE_THREADS / 64; ++w2) {
+        const unsigned long long mk = s_mask[w2];
+        if (mk) {
+          F = w2 * 64 + __builtin_ctzll(mk);
+          break;
+        }
       }
+      if (F >= 0 || tb + 1 >= ntiles) break;
+      __syncthreads();   // everyone has read s_mask before the next stage rewrites it
+      ++tb;
+    }
+    if (F >= 0) {
+      if (tid == F) s_pre = chunk_walk(s_delta, s_c, s_cin, F - 1, 0, -1, g0);
+    } else if (tid == 0) {   // the array's last tile, no break: the chain starts at gae = 0
+      s_pre = chunk_walk(s_delta, s_c, s_cin, GAE_THREADS - 1, 0, -1, 0.0f);
+    }
+    __syncthreads();
+    for (int64_t tw = tb - 1; tw > tile; --tw) {   // break-free tiles (rare): whole-tile walks
+      gae_stage<VEC>(r, d, V, n, nv_end, gf, glf, tw, s_delta, s_c, s_mask, vv, g0, pb);
+      __syncthreads();
+      if (tid == 0) s_pre = chunk_walk(s_delta, s_c, s_cin, GAE_THREADS - 1, 0, -1, s_pre);
+      __syncthreads();
     }
   }
-  s_out[tid] = (pb >= 0) ? g[0] : 0.0f;
-  {
-    const unsigned long long bal = __ballot(pb >= 0);   // chunks of this wave with a break
-    if ((tid & 63) == 0) s_mask[tid >> 6] = bal;
-  }
+  // the successor's granule, polled early (a round old, so normally there)
+  unsigned long long gw = 0ull;
+  if (tid == GAE_THREADS - 1 && has_succ && !pre) gw = ld_sc1(&ws.gran[tile + 1]);
+  gae_stage<VEC>(r, d, V, n, nv_end, gf, glf, tile, s_delta, s_c, s_mask, vv, g0, pb);
   __syncthreads();
   PRL_GAE_MARK(2);
   const unsigned tag = s_tag;
@@ -314,79 +371,107 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
     st_sc1(&ws.gran[tile], ((unsigned long long)tag << 32) | __float_as_uint(carry_out));
   };
   // chunk 0 with a break: the tile's carry-out is local — publish before anything else
-  if (tid == 0 && hb) publish(g[0]);
+  if (tid == 0 && hb) publish(g0);
 
-  // Carries between chunks, each chained ONCE: the thread of every chunk with a break owns the
-  // run of break-free chunks to its left (down to, and including as a carry target, the previous
-  // chunk with a break) and walks it right to left, writing each chunk's carry-in (g at the
-  // first element of the chunk to its right).  Thread 255 owns the run at the tile's end, which
-  // starts from the successor tile's carry.  Same recurrence order as the reference throughout.
+  // Carries between chunks, each chained ONCE.  A RUN is the stretch of break-free chunks left
+  // of a chunk with a break (down to, and including as a carry target, the previous chunk with a
+  // break), walked right to left from that chunk's g at its first element, writing each chunk's
+  // carry-in (g at the first element of the chunk to its right) to s_cin; the run at the tile's
+  // end starts from the successor tile's carry.  The runs are listed in LDS in chunk order and
+  // walked by threads 0, 1, ... — packed into the fewest waves: a walk keeps one lane of its
+  // wave busy, so with every chunk walking its own run (one lane in each of four waves) the
+  // walks of trained 500-step episodes filled the SIMDs' issue slots four times over.
+  // Same recurrence order as the reference throughout.
   const int lane = tid & 63, wv = tid >> 6;
+  int nb = 0;   // chunks with a break
+#pragma unroll
+  for (int w2 = 0; w2 < GAE_THREADS / 64; ++w2) nb += __popcll(s_mask[w2]);
   if (hb) {
+    int rank = __popcll(s_mask[wv] & ((1ull << lane) - 1ull));
+    for (int w2 = 0; w2 < wv; ++w2) rank += __popcll(s_mask[w2]);
     int p = -1;   // previous chunk with a break
-    {
-      const unsigned long long below = lane == 0 ? 0ull : (s_mask[wv] << (64 - lane));
-      if (below) {
-        p = tid - 1 - __builtin_clzll(below);
-      } else {
-        for (int w2 = wv - 1; w2 >= 0; --w2) {
-          const unsigned long long mk = s_mask[w2];
-          if (mk) {
-            p = w2 * 64 + 63 - __builtin_clzll(mk);
-            break;
-          }
+    const unsigned long long below = lane == 0 ? 0ull : (s_mask[wv] << (64 - lane));
+    if (below) {
+      p = tid - 1 - __builtin_clzll(below);
+    } else {
+      for (int w2 = wv - 1; w2 >= 0; --w2) {
+        const unsigned long long mk = s_mask[w2];
+        if (mk) {
+          p = w2 * 64 + 63 - __builtin_clzll(mk);
+          break;
         }
       }
     }
-    const float carry = chunk_walk(s_delta, s_c, s_cin, tid - 1, p < 0 ? 0 : p, p, g[0]);
-    if (p < 0 && tid > 0) publish(carry);   // walked to chunk 0: carry = g(tile start)
+    s_run_hi[rank] = tid - 1;
+    s_run_lo[rank] = p;
+    s_run_g[rank] = g0;
   }
+  // the tail run exists when chunk 255 has no break at all (a break that is not its last
+  // element leaves only that chunk's own tail, fed by s_cin[255])
+  const bool tail_run = (s_mask[GAE_THREADS / 64 - 1] >> 63) == 0ull && s_c[GAE_TILE - 1] != 0.0f;
   if (tid == GAE_THREADS - 1 && pb != GAE_EPT - 1) {
     float cin = 0.0f;  // beyond the last element: gae = 0 (PPO.py:110)
-    if (tile + 1 < ntiles) {
+    PRL_GAE_MARK_TAIL(8);
+    if (pre) {
+      cin = s_pre;
+    } else if (has_succ) {
       unsigned spins = 0;
       bool got = false;
       for (;;) {
-        const unsigned long long w = ld_sc1(&ws.gran[tile + 1]);
-        if ((unsigned)(w >> 32) == tag) {
-          cin = __uint_as_float((unsigned)(w & 0xffffffffull));
+        if ((unsigned)(gw >> 32) == tag) {
+          cin = __uint_as_float((unsigned)(gw & 0xffffffffull));
           got = true;
           break;
         }
         if (++spins >= GAE_SPIN_LIMIT) break;
         __builtin_amdgcn_s_sleep(1);
+        gw = ld_sc1(&ws.gran[tile + 1]);
       }
       if (!got) {
         cin = gae_lookahead(r, d, V, nv_end, n, gf, glf, (tile + 1) * (int64_t)GAE_TILE);
         __hip_atomic_fetch_add(&ws.ctrs[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    int L = -1;   // last chunk with a break
-    for (int w2 = GAE_THREADS / 64 - 1; w2 >= 0; --w2) {
-      const unsigned long long mk = s_mask[w2];
-      if (mk) {
-        L = w2 * 64 + 63 - __builtin_clzll(mk);
-        break;
+    PRL_GAE_MARK_TAIL(9);
+    if (tail_run) {
+      int L = -1;   // last chunk with a break
+      for (int w2 = GAE_THREADS / 64 - 1; w2 >= 0; --w2) {
+        const unsigned long long mk = s_mask[w2];
+        if (mk) {
+          L = w2 * 64 + 63 - __builtin_clzll(mk);
+          break;
+        }
       }
+      s_run_hi[nb] = GAE_THREADS - 1;
+      s_run_lo[nb] = L;
+      s_run_g[nb] = cin;
+    } else {
+      s_cin[GAE_THREADS - 1] = cin;
     }
-    const float carry = chunk_walk(s_delta, s_c, s_cin, GAE_THREADS - 1, L < 0 ? 0 : L, L, cin);
-    if (L < 0) publish(carry);               // no break in the tile
   }
   __syncthreads();
+  if (tid < nb + (tail_run ? 1 : 0)) {
+    const int hi = s_run_hi[tid], lo = s_run_lo[tid];
+    const float carry = chunk_walk(s_delta, s_c, s_cin, hi, lo < 0 ? 0 : lo, lo, s_run_g[tid]);
+    if (lo < 0 && hi >= 0) publish(carry);   // walked to chunk 0: g(tile start)
+  }
+  if (tid == GAE_THREADS - 1) PRL_GAE_MARK_TAIL(10);
+  __syncthreads();
   PRL_GAE_MARK(3);
-  // every chunk's elements after its last break, from its carry-in (delta / c re-read from LDS:
-  // not keeping them in registers across the walk keeps the kernel at 8 waves per SIMD)
-  if (pb != GAE_EPT - 1) {
+  // the chunk's outputs: g at or left of its last break again (the local recurrence, recomputed
+  // rather than kept in registers across the walks), then after it from its carry-in; delta / c
+  // re-read from LDS
+  float g[GAE_EPT];
+  {
     const ChunkDC x = chunk_load(s_delta, s_c, tid);
     const float dl2[GAE_EPT] = {x.da.x, x.da.y, x.da.z, x.da.w, x.db.x, x.db.y, x.db.z, x.db.w};
     const float cc2[GAE_EPT] = {x.ca.x, x.ca.y, x.ca.z, x.ca.w, x.cb.x, x.cb.y, x.cb.z, x.cb.w};
-    float carry = s_cin[tid];
+    float carry = pb != GAE_EPT - 1 ? s_cin[tid] : 0.0f;
 #pragma unroll
     for (int k = GAE_EPT - 1; k >= 0; --k) {
-      if (k > pb) {
-        carry = dl2[k] + cc2[k] * carry;
-        g[k] = carry;
-      }
+      if (k == pb) carry = 0.0f;   // the local chain starts from gae = 0 at the last break
+      carry = dl2[k] + cc2[k] * carry;
+      g[k] = carry;
     }
   }
 
@@ -398,7 +483,7 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
     rt[k] = g[k] + vv[k];
     av[k] = rt[k] - vv[k];
   }
-  if (VEC && full) {
+  if (VEC && i0 + GAE_EPT <= n) {
     float4* o4 = reinterpret_cast<float4*>(ret + i0);
     o4[0] = float4{rt[0], rt[1], rt[2], rt[3]};
     o4[1] = float4{rt[4], rt[5], rt[6], rt[7]};
@@ -502,6 +587,25 @@ using namespace prl;
 
 int64_t prl_gae_workspace_bytes(int64_t n) { return gae_ws_bytes(n); }
 
+namespace {
+// workgroups of the scan resident at once on the current device (cached per device)
+int64_t gae_resident_blocks() {
+  static int cached[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] == 0) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(gae_kernel<true>), GAE_THREADS, 0) != hipSuccess ||
+        cus <= 0 || per_cu <= 0)
+      return 1792;
+    cached[dev] = cus * per_cu;
+  }
+  return cached[dev];
+}
+}  // namespace
+
 extern "C" int prl_gae(const float* r, const float* d, const float* V, const float* next_value,
                        int64_t n, double gamma, double lam, float* ret, float* adv,
                        double* sums_out, void* workspace, int64_t workspace_bytes, void* stream) {
@@ -524,12 +628,19 @@ extern "C" int prl_gae(const float* r, const float* d, const float* V, const flo
   const float glf = (float)(gamma * lam);
   const bool vec = aligned16(r) && aligned16(d) && aligned16(V) && aligned16(ret) &&
                    (!adv || aligned16(adv));
+  // R streams (gae_kernel's tile order): about one round of resident workgroups, but at least
+  // 4 tiles per stream (a stream's first tile also stages its successor: <= 1/4 extra reads)
+  // (measured on trained 500-step segments: R = 1/2 or 3/4 of a round 10-20 % slower, 1.5 or 2
+  // rounds 4 % slower)
+  const int64_t R = std::max<int64_t>(1, std::min<int64_t>(gae_resident_blocks(), (nt + 3) / 4));
+  const int64_t Q = (nt + R - 1) / R;
+  const unsigned grid = (unsigned)(R * Q);
   if (vec)
-    hipLaunchKernelGGL(gae_kernel<true>, dim3((unsigned)nt), dim3(GAE_THREADS), 0, s, r, d, V,
-                       next_value, n, gf, glf, ret, adv, ws, nt, sums_out);
+    hipLaunchKernelGGL(gae_kernel<true>, dim3(grid), dim3(GAE_THREADS), 0, s, r, d, V,
+                       next_value, n, gf, glf, ret, adv, ws, nt, R, Q, sums_out);
   else
-    hipLaunchKernelGGL(gae_kernel<false>, dim3((unsigned)nt), dim3(GAE_THREADS), 0, s, r, d, V,
-                       next_value, n, gf, glf, ret, adv, ws, nt, sums_out);
+    hipLaunchKernelGGL(gae_kernel<false>, dim3(grid), dim3(GAE_THREADS), 0, s, r, d, V,
+                       next_value, n, gf, glf, ret, adv, ws, nt, R, Q, sums_out);
   PRL_LAUNCH_CHECK("gae");
   hipLaunchKernelGGL(gae_fold_kernel, dim3(1), dim3(GAE_FOLD_THREADS), 0, s, ws, nt,
                      adv ? 1 : 0, sums_out);

@@ -51,13 +51,19 @@ def test_gae_bit_exact_vs_reference_fixture(golden, case):
 
 @pytest.mark.parametrize("n,pd,seed", [(1, 1.0, 0), (7, 0.3, 1), (2048, 0.05, 2), (2049, 0.05, 3),
                                        (100_003, 0.05, 4), (1 << 20, 0.05, 5), (300_000, 0.0, 6),
-                                       (250_000, 0.002, 7), (65_536 * 200 // 8, -1, 8)])
+                                       (250_000, 0.002, 7), (65_536 * 200 // 8, -1, 8),
+                                       (2048 * 37, 0.0, 10), (2048 * 300 + 5, -5000, 11),
+                                       (2048 * 3000, -500, 12)])
 def test_gae_bit_exact_vs_oracle(n, pd, seed):
+    """Random breaks, none at all (a full last tile: the chain starts at gae = 0 past the end),
+    fixed segments of 200 (Pendulum), 500 (trained CartPole, > 1 round of tiles) and 5000 steps
+    (runs over break-free tiles: the stream heads' multi-tile look-ahead)."""
     N = native()
     rng = np.random.default_rng(seed)
-    if pd < 0:                                 # Pendulum-like: fixed 200-step segments
+    if pd < 0:                                 # fixed segments (-1: Pendulum's 200 steps)
+        seg = 200 if pd == -1 else int(-pd)
         d = np.zeros(n, np.float32)
-        d[199::200] = 1
+        d[seg - 1::seg] = 1
     else:
         d = (rng.random(n) < pd).astype(np.float32)
     r = rng.normal(1, 0.5, n).astype(np.float32)

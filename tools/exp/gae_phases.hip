@@ -4,9 +4,16 @@
 #include <stdint.h>
 __device__ unsigned long long* g_gae_prof;
 #define PRL_GAE_MARK(i) \
-  do { if (threadIdx.x == 0) g_gae_prof[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+  do { if (threadIdx.x == 0) g_gae_prof[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define PRL_GAE_MARK_TAIL(i) \
+  do { g_gae_prof[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #include "../../parallel-reinforcement-learning_amd/csrc/prl_gae.hip"
 
 extern "C" int gae_prof_set(unsigned long long* buf) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_gae_prof), &buf, sizeof(buf));
 }
+
+// the product library's error slot is not linked into this experiment
+namespace prl {
+int set_error(int code, const char* fmt, ...) { (void)fmt; return code; }
+}  // namespace prl

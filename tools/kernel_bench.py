@@ -94,6 +94,7 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--gae-n", type=int, default=0, help="only the GAE scan at this size")
+    ap.add_argument("--gae-seg", type=int, default=0, help="with --gae-n: fixed segment length")
     ap.add_argument("--gae-file", default=None, help="only the GAE scan on bench.py --dump-gae")
     ap.add_argument("--env-e", type=int, default=0, help="only the CartPole rollout step at E envs")
     a = ap.parse_args()
@@ -104,7 +105,7 @@ if __name__ == "__main__":
         print(json.dumps(gae_file_case(a.gae_file, reps=a.reps)), flush=True)
         sys.exit(0)
     if a.gae_n:
-        print(json.dumps(gae_case(a.gae_n, reps=a.reps)), flush=True)
+        print(json.dumps(gae_case(a.gae_n, seg=a.gae_seg or None, reps=a.reps)), flush=True)
         sys.exit(0)
     out = []
     sizes = [1 << 20] if a.quick else [1 << 20, 2_300_000, 65536 * 200]
