@@ -146,12 +146,21 @@ __device__ inline float chunk_apply(const ChunkDC& x, float carry) {
   return carry;
 }
 // Walk chunks hi, hi-1, ..., lo: write each one's carry-in (g at the first element of the chunk to
-// its right) to s_cin, and apply every chunk > stop to the carry.  The next chunk's delta / c are
-// read from LDS while the current one is applied (the walk is the kernel's serial path: ~500
-// dependent mul/add pairs for a trained CartPole episode, 13 us per tile without the prefetch).
+// its right) to s_cin, and apply every chunk > stop to the carry.  The walk is the kernel's serial
+// path (~500 dependent mul/add pairs for a trained CartPole episode); two chunks' LDS reads are
+// issued together, so one LDS latency is exposed per two chunks (a prefetch carried across the
+// loop's back edge was sunk back behind its branch by the compiler; four chunks cost occupancy).
 __device__ inline float chunk_walk(const float* s_delta, const float* s_c, float* s_cin, int hi,
                                    int lo, int stop, float carry) {
-  for (int k = hi; k >= lo; --k) {
+  int k = hi;
+  for (; k - 1 > stop && k - 1 >= lo; k -= 2) {   // two chunks' reads in flight at once
+    const ChunkDC x0 = chunk_load(s_delta, s_c, k), x1 = chunk_load(s_delta, s_c, k - 1);
+    s_cin[k] = carry;
+    carry = chunk_apply(x0, carry);
+    s_cin[k - 1] = carry;
+    carry = chunk_apply(x1, carry);
+  }
+  for (; k >= lo; --k) {
     s_cin[k] = carry;
     if (k > stop) carry = chunk_apply(chunk_load(s_delta, s_c, k), carry);
   }
