@@ -306,6 +306,9 @@ def main():
         achieved = flops / (avg_ms * 1e-3) / 1e12
         what = {"ppo_update_kernel": "persistent fused PPO update: the whole k_epochs x "
                                      "minibatch loop in one launch",
+                "ppo_update_kernel_dp": "data-parallel persistent engine: the whole loop in one "
+                                        "launch per rank, each step's gradient summed across "
+                                        "ranks inside it over IPC-mapped peer memory",
                 "ppo_update_dp": "data-parallel engine: the whole loop enqueued natively, per "
                                  "step gradient kernel -> RCCL all-reduce -> AdamW kernel; "
                                  "time = events around the loop",

@@ -306,6 +306,35 @@ int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, int32_t D, 
                       float* grad, float* loss_out, void* workspace, int64_t workspace_bytes,
                       void* comm, void* stream);
 
+/* ---- data-parallel persistent update (world > 1, opt-in PRL_DP_PERSISTENT=1): PPO.py:216-255
+ * per rank as ONE launch of the persistent engine (prl_ppo_update) per rank, the cross-rank sum
+ * done inside it: after each step's in-GPU slice reduction, workgroup g publishes its rank's
+ * slice in its own slice buffer, raises a per-step flag, waits for workgroup g of every rank and
+ * sums their slices in rank order (float32) over IPC-mapped peer memory — no RCCL call, no
+ * host work per step.  nb_union = minibatches of the union (max over ranks); inv_count = device
+ * [nb_union], float(1 / rows of union minibatch j); xbufs = host array of `world` slice-buffer
+ * pointers (this rank's own, and the others' opened with prl_dp_ipc_open), each
+ * prl_dp_xbuf_bytes long, allocated by prl_dp_xbuf_alloc (zeroed once).  seq0 = the exchange
+ * sequence number of this launch's first step: 0 for the first launch on a buffer set, then
+ * advanced by nb_union x k_epochs per launch, the same on every rank (the flags only grow, so
+ * one buffer set serves every later launch).  All ranks' launches must be resident together.
+ * No reference counterpart (the reference is single-process). */
+int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step,
+                       int32_t D, int32_t A, int32_t discrete, const float* S,
+                       const float* actions, const float* old_logp, const float* adv,
+                       const float* ret, int64_t N, int32_t mini_batch, int32_t k_epochs,
+                       int32_t nb_union, const float* inv_count, float clip, float vf_coef,
+                       float ent_coef, float lr, float beta1, float beta2, float eps,
+                       float weight_decay, float max_norm, float* loss_out, int32_t world,
+                       int32_t rank, void* const* xbufs, int64_t seq0, void* workspace,
+                       int64_t workspace_bytes, void* stream);
+int64_t prl_dp_xbuf_bytes(int32_t D, int32_t A, int32_t discrete, int32_t mini_batch);
+int prl_dp_xbuf_alloc(int64_t bytes, void** out);
+int prl_dp_xbuf_free(void* p);
+int prl_dp_ipc_handle(void* p, uint8_t* out, int64_t out_bytes);   /* out: 64 bytes */
+int prl_dp_ipc_open(const uint8_t* handle, int64_t bytes, void** out);
+int prl_dp_ipc_close(void* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -310,7 +310,9 @@ class PPO:
                     comm = eng.dp_comm()
                     self.last_loss = eng.run_stepped(S, A, old_logp, adv, returns, self.k_epochs,
                                                      n_ranks, self.all_reduce, comm=comm).clone()
-                    self.last_update_path = "fused-dp" + ("-native" if comm is not None else "")
+                    self.last_update_path = ("fused-dp" + ("-native" if comm is not None else "")
+                                             + ("-persistent" if getattr(eng, "_xbufs", None)
+                                                else ""))
                 self.last_graph_replays = 0
                 return
         self.last_update_path = "graph" if self.use_graphs else "eager"

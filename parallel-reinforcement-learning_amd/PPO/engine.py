@@ -191,12 +191,167 @@ class FusedUpdate:
 
     def close(self):
         """Destroy this engine's own RCCL communicator (if one was built) once the device is
-        idle; call before torch.distributed.destroy_process_group()."""
+        idle, and its data-parallel slice buffers (after every rank is idle: a peer may still be
+        reading them); call on every rank before torch.distributed.destroy_process_group()."""
         comm = getattr(self, "_comm", None)
         if comm:
             torch.cuda.synchronize()
             prl_native.dp_comm_destroy(comm)
         self._comm = None
+        xb = getattr(self, "_xbufs", None)
+        if xb:
+            import torch.distributed as tdist
+            torch.cuda.synchronize()
+            tdist.barrier()
+            for r, ptr in enumerate(xb):
+                if r != self._dp_rank:
+                    prl_native.dp_ipc_close(ptr)
+            tdist.barrier()
+            prl_native.dp_xbuf_free(self._xbuf_own)
+        self._xbufs, self._xb_tried = None, False
+
+    # ---------------------------------- data-parallel persistent launch (world > 1, opt-in)
+    def dp_slices(self):
+        """Every rank's slice buffer for prl_ppo_update_dpx (this rank's own allocation and the
+        peers' opened through IPC handles exchanged over torch.distributed), built once; None
+        when PRL_DP_PERSISTENT=0, world > 8, or any rank could not build them or failed the
+        self-test (a vote; then run_stepped's loop runs).  All ranks call it together.
+        The self-test is one small launch on scratch copies of the optimizer state: it must end
+        without an in-kernel timeout and leave bit-identical parameters on every rank.  Its
+        2-rank GPU test runs both ranks on ONE GPU (IPC maps of the same device); on a node the
+        maps are other GPUs' memory over xGMI, which the self-test checks before first use."""
+        if getattr(self, "_xb_tried", False):
+            return self._xbufs
+        self._xb_tried, self._xbufs = True, None
+        if os.environ.get("PRL_DP_PERSISTENT", "1") != "1":
+            return None
+        import torch.distributed as tdist
+        if not (tdist.is_available() and tdist.is_initialized()):
+            return None
+        world, rank = tdist.get_world_size(), tdist.get_rank()
+        own, handle = None, b""
+        if 1 < world <= 8:
+            try:
+                own = prl_native.dp_xbuf_alloc(
+                    prl_native.dp_xbuf_bytes(self.D, self.A, self.discrete, self.mini_batch))
+                handle = prl_native.dp_ipc_handle(own)
+            except (RuntimeError, ValueError) as e:
+                warnings.warn(f"data-parallel slice buffer unavailable ({e})")
+                own, handle = None, b""
+        handles = [None] * world
+        tdist.all_gather_object(handles, handle)
+        ptrs, ok = [], all(len(h) > 0 for h in handles)
+        if ok:
+            try:
+                ptrs = [own if r == rank else prl_native.dp_ipc_open(h) for r, h in enumerate(handles)]
+            except RuntimeError as e:
+                warnings.warn(f"data-parallel peer slice buffers unavailable ({e})")
+                ok = False
+        votes = [None] * world
+        tdist.all_gather_object(votes, ok)
+        if not all(votes):
+            for r, ptr in enumerate(ptrs):
+                if r != rank:
+                    prl_native.dp_ipc_close(ptr)
+            tdist.barrier()
+            prl_native.dp_xbuf_free(own)
+            return None
+        self._xbuf_own, self._xbufs, self._dp_rank, self._dp_seq = own, ptrs, rank, 0
+        ok = self._dp_selftest(world)
+        votes = [None] * world
+        tdist.all_gather_object(votes, ok)
+        if not all(votes):
+            warnings.warn("data-parallel persistent engine failed its self-test; using the "
+                          "stepped loop")
+            self.close()
+            self._xb_tried = True
+            return None
+        return ptrs
+
+    def _dp_checksum(self, flat) -> float:
+        return float(flat.double().sum().item()) + float((flat.double() ** 2).sum().item())
+
+    def _dp_selftest(self, world) -> bool:
+        """One small prl_ppo_update_dpx launch (2 minibatches per rank, k 1) on scratch copies
+        of the state: no in-kernel timeout and the same parameters on every rank."""
+        import torch.distributed as tdist
+        try:
+            mb = self.mini_batch
+            n = 2 * mb
+            dev = self.flat.device
+            g = torch.Generator(device=dev).manual_seed(7 + self._dp_rank)
+            S = torch.randn(n, self.D, device=dev, generator=g) * 0.5
+            if self.discrete:
+                A = (torch.rand(n, device=dev, generator=g) * self.A).floor().reshape(-1, 1)
+            else:
+                A = torch.randn(n, self.A, device=dev, generator=g) * 0.3
+            old = torch.randn(n, device=dev, generator=g) * 0.1 - 0.7
+            adv, ret = torch.randn(n, device=dev, generator=g), torch.randn(n, device=dev, generator=g)
+            flat, m, v, step = self.flat.clone(), self.m.clone(), self.v.clone(), self.step.clone()
+            loss = torch.zeros(1, dtype=torch.float32, device=dev)
+            group = self.ppo.optimizer.param_groups[0]
+            inv = torch.full((2,), 1.0 / (n // 2 * world), dtype=torch.float32, device=dev)
+            prl_native.ppo_update_dpx(
+                flat, m, v, step, self.D, self.A, self.discrete, S, A, old, adv, ret, mb, 1, 2,
+                inv, self.ppo.policy_clip, self.ppo.value_coef, self.ppo.entropy_coef,
+                group["lr"], group["betas"][0], group["betas"][1], group["eps"],
+                group["weight_decay"], 2.0, loss, world, self._dp_rank, self._xbufs,
+                self._dp_seq, self.ws)
+            self._dp_seq += 2
+            torch.cuda.synchronize()
+            status = max(prl_native.ppo_update_status(self.ws).tolist())
+            if status != 0:
+                # the sticky word stays set: clear the workspace so the engine's own runs start clean
+                self.ws.zero_()
+                return False
+            sums = [None] * world
+            tdist.all_gather_object(sums, self._dp_checksum(flat))
+            return len(set(sums)) == 1 and all(x == x for x in sums)
+        except RuntimeError as e:
+            warnings.warn(f"data-parallel persistent self-test failed ({e})")
+            return False
+
+    def run_dp_persistent(self, S, A, old_logp, adv, ret, k_epochs: int, n_ranks):
+        """run() as one data-parallel rank: ONE persistent launch for the whole loop; each step's
+        gradient is summed over the ranks inside it (union minibatch j = every rank's rows
+        j*mb .. (j+1)*mb, weighted 1 / union rows, as run_stepped)."""
+        import torch.distributed as tdist
+        xb = self.dp_slices()
+        if not self.bound():
+            self._bind()
+        group = self.ppo.optimizer.param_groups[0]
+        beta1, beta2 = group["betas"]
+        mb = self.mini_batch
+        nb = max(-(-n // mb) for n in n_ranks)
+        counts = [sum(min(mb, max(0, n - j * mb)) for n in n_ranks) for j in range(nb)]
+        inv = torch.tensor([1.0 / c for c in counts], dtype=torch.float32, device=S.device)
+        A2 = A if A.dim() == 2 else A.reshape(-1, 1)
+        if self.events is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        prl_native.ppo_update_dpx(
+            self.flat, self.m, self.v, self.step, self.D, self.A, self.discrete,
+            S.contiguous(), A2.contiguous(), old_logp.contiguous(), adv.contiguous(),
+            ret.contiguous(), mb, k_epochs, nb, inv, self.ppo.policy_clip, self.ppo.value_coef,
+            self.ppo.entropy_coef, group["lr"], beta1, beta2, group["eps"],
+            group["weight_decay"], 2.0, self.loss, tdist.get_world_size(), self._dp_rank, xb,
+            self._dp_seq, self.ws)
+        self._dp_seq += int(k_epochs) * nb
+        if self.events is not None:
+            ev[1].record()
+            self.events.append(("ppo_update_kernel_dp", ev[0], ev[1],
+                                int(S.shape[0]) * int(k_epochs), int(k_epochs) * nb))
+        self._sync_optimizer_state()
+        status = max(prl_native.ppo_update_status(self.ws).tolist())
+        if status != 0:
+            raise RuntimeError(f"prl_ppo_update_dpx: in-kernel timeout (status {status}); the "
+                               "policy parameters are undefined")
+        # the ranks must still hold the same parameters (one scalar per rank per learn())
+        sums = [None] * tdist.get_world_size()
+        tdist.all_gather_object(sums, self._dp_checksum(self.flat))
+        if len(set(sums)) != 1:
+            raise RuntimeError(f"prl_ppo_update_dpx: ranks diverged (parameter checksums {sums})")
+        return self.loss.reshape(())
 
     def run_stepped(self, S, A, old_logp, adv, ret, k_epochs: int, n_ranks, all_reduce,
                     comm=None):
@@ -211,6 +366,8 @@ class FusedUpdate:
         ncclAllReduce on torch's stream); otherwise it runs here, calling `all_reduce` on the
         gradient image every step.  Both give the same bits."""
         import ctypes
+        if k_epochs > 0 and comm is None and self.dp_slices() is not None:
+            return self.run_dp_persistent(S, A, old_logp, adv, ret, k_epochs, n_ranks)
         if not self.bound():
             self._bind()
         group = self.ppo.optimizer.param_groups[0]

@@ -53,6 +53,7 @@ constexpr int UPD_HS = 68;        // LDS row stride of [*][64] arrays
 constexpr int UPD_MAXH = 3;       // heads
 constexpr int UPD_MAXD = 64;      // max observation dim on the fused path
 constexpr int UPD_MAXA = 8;       // max action dim on the fused path
+constexpr int UPD_MAX_RANKS = 8;   // data-parallel ranks of one persistent launch (one node)
 constexpr unsigned UPD_SPIN_LIMIT = 1u << 22;  // ~0.1-0.3 s of s_sleep polls: never expected
 
 struct UpdTensor {
@@ -140,6 +141,14 @@ struct UpdArgs {
   unsigned long long* prof;  // [8] workgroup 0's time per phase (100 MHz ticks, summed over steps)
   unsigned grad_target;      // ppo_grad_kernel: arrivals on ctr[0] that end its hand-off
   int profile;               // 1: workgroup 0 records its phase / tile-stage times (PRL_UPD_PROFILE)
+  // data-parallel persistent launch (prl_ppo_update_dpx; world == 1: the single-GPU engine)
+  int world, rank;
+  const float* inv_count;    // [nb] 1 / rows of union minibatch j over all ranks (null: 1 / B)
+  unsigned long long dp_seq0;   // exchange sequence number of this launch's first step
+  float* xbuf[UPD_MAX_RANKS];             // rank r's [2][Qtot * 4] slice buffers (peer mappings)
+  unsigned long long* xflag[UPD_MAX_RANKS];   // rank r's [G] per-workgroup step flags
+  float* xbuf_self;                       // == xbuf[rank] (no dynamic kernarg indexing)
+  unsigned long long* xflag_self;         // == xflag[rank]
 };
 
 // ---- sc1 (write-through / L1-bypassing) accessors -------------------------------------------
@@ -150,18 +159,29 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 __device__ inline __amdgpu_buffer_rsrc_t upd_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
-__device__ inline float4 ld4_sc1(__amdgpu_buffer_rsrc_t rs, size_t float_off) {
-  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(float_off * 4), 0, 16);
+// cache policy of the 16-B buffer accesses: sc1 = device scope (the hand-offs inside one GPU);
+// sc0 sc1 = system scope (the data-parallel slices other ranks' kernels read through IPC maps)
+constexpr int UPD_AUX_SC1 = 16, UPD_AUX_SYS = 17;
+template <int AUX>
+__device__ inline float4 ld4_aux(__amdgpu_buffer_rsrc_t rs, size_t float_off) {
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(float_off * 4), 0, AUX);
   return float4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
                 __uint_as_float(v.w)};
 }
-__device__ inline void st4_sc1(__amdgpu_buffer_rsrc_t rs, size_t float_off, float4 x) {
+template <int AUX>
+__device__ inline void st4_aux(__amdgpu_buffer_rsrc_t rs, size_t float_off, float4 x) {
   v4u v;
   v.x = __float_as_uint(x.x);
   v.y = __float_as_uint(x.y);
   v.z = __float_as_uint(x.z);
   v.w = __float_as_uint(x.w);
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (unsigned)(float_off * 4), 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (unsigned)(float_off * 4), 0, AUX);
+}
+__device__ inline float4 ld4_sc1(__amdgpu_buffer_rsrc_t rs, size_t float_off) {
+  return ld4_aux<UPD_AUX_SC1>(rs, float_off);
+}
+__device__ inline void st4_sc1(__amdgpu_buffer_rsrc_t rs, size_t float_off, float4 x) {
+  st4_aux<UPD_AUX_SC1>(rs, float_off, x);
 }
 __device__ inline float ld_sc1f(const float* p) {
   return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
@@ -1027,14 +1047,16 @@ __device__ __forceinline__ float adam_loss(const float* grad, int Lp, float inv_
 // cancel across workgroups), publishes the slice (sc1) and returns this thread's share of the
 // slice's sum of squares (parameter quads only).  Uses scratch as [spl][nq] double4.
 __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_red,
-                                         int Qtot, int Qp, int g, int G, float* scratch, int NT) {
+                                         int Qtot, int Qp, int g, int G, float* scratch, int NT,
+                                         int aux = UPD_AUX_SC1) {
   const int t = threadIdx.x;
   const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
   const int nq = qhi - qlo;
   float ssq = 0.f;
   auto fin = [&](int qi, double ax, double ay, double az, double aw) {
     const float4 r = float4{(float)ax, (float)ay, (float)az, (float)aw};
-    st4_sc1(rs_red, (size_t)(qlo + qi) * 4, r);
+    if (aux == UPD_AUX_SYS) st4_aux<UPD_AUX_SYS>(rs_red, (size_t)(qlo + qi) * 4, r);
+    else st4_aux<UPD_AUX_SC1>(rs_red, (size_t)(qlo + qi) * 4, r);
     if (qlo + qi < Qp) ssq += r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w;
   };
   if (nq > NT / 2) {
@@ -1069,8 +1091,71 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
   return ssq;
 }
 
+// Data-parallel ranks (world > 1, one persistent launch per rank): this workgroup's slice of the
+// step's gradient summed over ranks.  Workgroup g of every rank has just written its rank-local
+// slice into its own xbuf[par] (system-scope stores, drained); it raises its flag to the step's
+// exchange sequence number + 1 (the caller continues the sequence from launch to launch, so the
+// flags only grow and are never reset), waits until workgroup
+// g of every rank has, then sums the world slices in rank order (float32, as the stepped path's
+// all-reduce) into red, where phase C reads the reduced gradient.  xbuf is double-buffered by
+// step parity: a rank rewrites xbuf[par] two steps later, by which time every rank has raised
+// the flag of the step in between, i.e. has finished reading this one.
+__device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t rs_red, int Qtot,
+                                   int g, int G, unsigned long long gstep, int par, int* s_abort) {
+  const int t = threadIdx.x, NT = blockDim.x;
+  const unsigned long long want = gstep + 1ull;
+  if (t == 0) __hip_atomic_store(args.xflag_self + g, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t < 64) {
+    unsigned long long* fl = args.xflag[0];   // lane r polls rank r (selected, not indexed)
+#pragma unroll
+    for (int r = 1; r < UPD_MAX_RANKS; ++r)
+      if (t == r) fl = args.xflag[r];
+    bool ok = true;
+    for (unsigned spins = 0;; ++spins) {
+      const bool ready = t >= args.world ||
+                         __hip_atomic_load(fl + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= want;
+      if (__ballot(!ready) == 0ull) break;
+      if (ld_sc1u(args.ctr + 2) != 0u) { ok = false; break; }
+      if (spins > UPD_SPIN_LIMIT) {
+        if (t == 0) {
+          __hip_atomic_store(args.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(args.ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_or(args.ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (t == 0) *s_abort = ok ? 0 : 1;
+  }
+  __syncthreads();
+  if (*s_abort) return false;
+  const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
+  const size_t base = (size_t)par * Qtot * 4;
+  for (int q = qlo + t; q < qhi; q += NT) {
+    float4 acc = ld4_aux<UPD_AUX_SYS>(upd_rsrc(args.xbuf[0] + base), (size_t)q * 4);
+#pragma unroll
+    for (int r = 1; r < UPD_MAX_RANKS; ++r) {
+      if (r < args.world) {
+        const float4 x = ld4_aux<UPD_AUX_SYS>(upd_rsrc(args.xbuf[r] + base), (size_t)q * 4);
+        acc.x += x.x;
+        acc.y += x.y;
+        acc.z += x.z;
+        acc.w += x.w;
+      }
+    }
+    st4_sc1(rs_red, (size_t)q * 4, acc);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  return true;
+}
+
 // NQ = parameter quads per thread (ceil(Lp / 4 / 256)): AdamW's moments live in registers.
-template <int NQ, int KD, int KA>
+// DP: the data-parallel form (prl_ppo_update_dpx): union-minibatch row weights and the
+// cross-rank slice sum; a separate instantiation, so the single-GPU kernel carries none of it.
+template <int NQ, int KD, int KA, bool DP>
 __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& args) {
   constexpr int NW = upd_nw<KD, KA>(), NT = 64 * NW;
   extern __shared__ __align__(16) float upd_lds[];
@@ -1130,7 +1215,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     const int j = s % args.nb;
     const int64_t mb0 = (int64_t)j * args.mb;
     const int B = (int)std::min<int64_t>(args.mb, args.N - mb0);
-    const float invB = 1.0f / (float)B;
+    const float invB = DP ? args.inv_count[j] : 1.0f / (float)B;
     // profile mode 2 (PRL_UPD_PROFILE=2, diagnostics only): no rows, i.e. the exchange alone
     const int myrows = args.profile == 2 ? 0 : std::max(0, std::min(R, B - g * R));
     const int64_t myrow0 = mb0 + (int64_t)g * R;
@@ -1189,9 +1274,14 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     mark(2);   // wait A
     // ---- phase B: reduce this workgroup's slice over the G partials --------------------------
     {
-      (void)upd_slice_reduce(rs_part, rs_red, Qtot, Qp, g, G, scratch, NT);
+      constexpr bool dp = DP;
+      const unsigned long long gstep = args.dp_seq0 + (unsigned long long)s;
+      const int par = (int)(gstep & 1ull);
+      (void)upd_slice_reduce(rs_part, dp ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
+                             Qtot, Qp, g, G, scratch, NT, dp ? UPD_AUX_SYS : UPD_AUX_SC1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (dp && !upd_dp_union_slice(args, rs_red, Qtot, g, G, gstep, par, s_abort)) return;
       mark(3);   // slice reduce
       if (t < 64) {
         if (t == 0) upd_arrive(args.ctr, UPD_CTR_B, g);
@@ -1304,13 +1394,13 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
 
 // KDIM > 0: the observation dim is a compile-time constant and the whole parameter layout folds
 // into immediates (the specialised shapes); KDIM = 0: runtime layout from the kernel argument.
-template <int NQ, int KD, int KA, int KDIM>
+template <int NQ, int KD, int KA, int KDIM, bool DP = false>
 __global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_update_kernel(UpdArgs args) {
   if constexpr (KDIM > 0) {
     constexpr UpdNet N = upd_make(KDIM, KA, KD);
-    ppo_update_body<NQ, KD, KA>(N, args);
+    ppo_update_body<NQ, KD, KA, DP>(N, args);
   } else {
-    ppo_update_body<NQ, KD, KA>(args.net, args);
+    ppo_update_body<NQ, KD, KA, DP>(args.net, args);
   }
 }
 
@@ -1599,7 +1689,15 @@ bool upd_force_generic() {
   const char* e = getenv("PRL_UPD_GENERIC");
   return e && e[0] == '1';
 }
-const void* upd_kernel_for(const UpdNet& n) {
+const void* upd_kernel_for(const UpdNet& n, bool dp = false) {
+  if (dp) {
+    const int nq = upd_nq(n);
+    if (upd_force_generic()) return nq <= 20 ? reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0, true>) : nullptr;
+    if (n.discrete && n.A == 2 && n.D == 4 && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4, true>);
+    if (!n.discrete && n.A == 1 && n.D == 3 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3, true>);
+    if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0, true>);
+    return nullptr;
+  }
   const int nq = upd_nq(n);
   if (upd_force_generic()) return nq <= 20 ? reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0>) : nullptr;
   if (n.discrete && n.A == 2 && n.D == 4 && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4>);
@@ -1689,14 +1787,24 @@ extern "C" int prl_ppo_update_info(int32_t D, int32_t A, int32_t discrete, int64
   return (upd_lds_bytes(n) <= 160 * 1024 && upd_kernel_for(n)) ? PRL_OK : PRL_ERR_ARG;
 }
 
-extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step,
-                              int32_t D, int32_t A, int32_t discrete, const float* S,
-                              const float* actions, const float* old_logp, const float* adv,
-                              const float* ret, int64_t N, int32_t mini_batch, int32_t k_epochs,
-                              float clip, float vf_coef, float ent_coef, float lr, float beta1,
-                              float beta2, float eps, float weight_decay, float max_norm,
-                              float* loss_out, void* workspace, int64_t workspace_bytes,
-                              void* stream) {
+namespace {
+// the data-parallel part of a persistent launch (prl_ppo_update_dpx)
+struct UpdDp {
+  int world, rank, nb;
+  const float* inv_count;
+  void* const* xbufs;
+  int64_t seq0;
+};
+// the slice buffers [2][Qtot * 4] f32, then the per-workgroup step flags [G] u64
+size_t upd_xbuf_flags_off(const UpdNet& n) { return (((size_t)n.Lp / 4 + 1) * 32 + 255) & ~(size_t)255; }
+
+int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, int32_t D,
+            int32_t A, int32_t discrete, const float* S, const float* actions,
+            const float* old_logp, const float* adv, const float* ret, int64_t N,
+            int32_t mini_batch, int32_t k_epochs, float clip, float vf_coef, float ent_coef,
+            float lr, float beta1, float beta2, float eps, float weight_decay, float max_norm,
+            float* loss_out, void* workspace, int64_t workspace_bytes, void* stream,
+            const UpdDp* dp) {
   UpdArgs args{};
   PRL_REQUIRE(upd_layout(D, A, discrete, args.net), "prl_ppo_update: D=%d A=%d not supported", D, A);
   PRL_REQUIRE(N > 0 && mini_batch > 0 && k_epochs >= 0, "prl_ppo_update: bad sizes");
@@ -1707,7 +1815,8 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
   const size_t need = upd_ws_carve(args.net, G, reinterpret_cast<char*>(workspace), &ws);
   PRL_REQUIRE((size_t)workspace_bytes >= need, "prl_ppo_update: workspace %lld < %zu bytes",
               (long long)workspace_bytes, need);
-  const int64_t nb = cdiv(N, (int64_t)mini_batch);
+  const int64_t nb = dp ? (int64_t)dp->nb : cdiv(N, (int64_t)mini_batch);
+  PRL_REQUIRE(nb >= cdiv(N, (int64_t)mini_batch), "prl_ppo_update_dpx: nb < this rank's minibatches");
   PRL_REQUIRE(nb * (int64_t)k_epochs < (int64_t)(1u << 31) / 256, "prl_ppo_update: too many steps");
   if (k_epochs == 0) return PRL_OK;
   args.S = S;
@@ -1745,10 +1854,29 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
   args.ctr = ws.ctr;
   args.prof = ws.prof;
   args.profile = upd_profile_enabled();
+  args.world = 1;
+  if (dp) {
+    PRL_REQUIRE(dp->world >= 1 && dp->world <= UPD_MAX_RANKS && dp->rank >= 0 && dp->rank < dp->world,
+                "prl_ppo_update_dpx: world %d / rank %d (at most %d ranks)", dp->world, dp->rank,
+                UPD_MAX_RANKS);
+    PRL_REQUIRE(dp->inv_count && dp->xbufs, "prl_ppo_update_dpx: null pointer");
+    args.world = dp->world;
+    args.rank = dp->rank;
+    args.inv_count = dp->inv_count;
+    args.dp_seq0 = (unsigned long long)dp->seq0;
+    const size_t fo = upd_xbuf_flags_off(args.net);
+    for (int r = 0; r < dp->world; ++r) {
+      PRL_REQUIRE(dp->xbufs[r], "prl_ppo_update_dpx: null slice buffer of rank %d", r);
+      args.xbuf[r] = reinterpret_cast<float*>(dp->xbufs[r]);
+      args.xflag[r] = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(dp->xbufs[r]) + fo);
+    }
+    args.xbuf_self = args.xbuf[dp->rank];
+    args.xflag_self = args.xflag[dp->rank];
+  }
   const size_t lds = upd_lds_bytes(args.net);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_update: %zu B of LDS needed", lds);
   hipStream_t st = as_stream(stream);
-  const void* kern = upd_kernel_for(args.net);
+  const void* kern = upd_kernel_for(args.net, dp != nullptr);
   PRL_REQUIRE(kern, "prl_ppo_update: %d parameter quads per thread not built", upd_nq(args.net));
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
@@ -1762,6 +1890,83 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
   hipLaunchKernelGGL(ppo_image_kernel, dim3(img_grid), dim3(UPD_THREADS), 0, st, args.net, params,
                      exp_avg, exp_avg_sq, img_p, img_m, img_v, 0);
   PRL_LAUNCH_CHECK("ppo_image");
+  return PRL_OK;
+}
+}  // namespace
+
+extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step,
+                              int32_t D, int32_t A, int32_t discrete, const float* S,
+                              const float* actions, const float* old_logp, const float* adv,
+                              const float* ret, int64_t N, int32_t mini_batch, int32_t k_epochs,
+                              float clip, float vf_coef, float ent_coef, float lr, float beta1,
+                              float beta2, float eps, float weight_decay, float max_norm,
+                              float* loss_out, void* workspace, int64_t workspace_bytes,
+                              void* stream) {
+  return upd_run(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp,
+                 adv, ret, N, mini_batch, k_epochs, clip, vf_coef, ent_coef, lr, beta1, beta2, eps,
+                 weight_decay, max_norm, loss_out, workspace, workspace_bytes, stream, nullptr);
+}
+
+extern "C" int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_sq,
+                                  float* adam_step, int32_t D, int32_t A, int32_t discrete,
+                                  const float* S, const float* actions, const float* old_logp,
+                                  const float* adv, const float* ret, int64_t N,
+                                  int32_t mini_batch, int32_t k_epochs, int32_t nb_union,
+                                  const float* inv_count, float clip, float vf_coef,
+                                  float ent_coef, float lr, float beta1, float beta2, float eps,
+                                  float weight_decay, float max_norm, float* loss_out,
+                                  int32_t world, int32_t rank, void* const* xbufs, int64_t seq0,
+                                  void* workspace, int64_t workspace_bytes, void* stream) {
+  PRL_REQUIRE(nb_union > 0 && seq0 >= 0, "prl_ppo_update_dpx: nb_union <= 0 or seq0 < 0");
+  const UpdDp dp{world, rank, nb_union, inv_count, xbufs, seq0};
+  return upd_run(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp,
+                 adv, ret, N, mini_batch, k_epochs, clip, vf_coef, ent_coef, lr, beta1, beta2, eps,
+                 weight_decay, max_norm, loss_out, workspace, workspace_bytes, stream, &dp);
+}
+
+extern "C" int64_t prl_dp_xbuf_bytes(int32_t D, int32_t A, int32_t discrete, int32_t mini_batch) {
+  UpdNet net{};
+  if (!upd_layout(D, A, discrete, net) || mini_batch <= 0) return -1;
+  return (int64_t)(upd_xbuf_flags_off(net) + (size_t)upd_grid(mini_batch) * 8);
+}
+
+extern "C" int prl_dp_xbuf_alloc(int64_t bytes, void** out) {
+  PRL_REQUIRE(bytes > 0 && out, "prl_dp_xbuf_alloc: bad arguments");
+  void* p = nullptr;
+  PRL_HIP_TRY(hipMalloc(&p, (size_t)bytes));   // its own allocation: shareable by IPC handle
+  const hipError_t e = hipMemset(p, 0, (size_t)bytes);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    PRL_HIP_TRY(e);
+  }
+  *out = p;
+  return PRL_OK;
+}
+
+extern "C" int prl_dp_xbuf_free(void* p) {
+  if (p) PRL_HIP_TRY(hipFree(p));
+  return PRL_OK;
+}
+
+extern "C" int prl_dp_ipc_handle(void* p, uint8_t* out, int64_t out_bytes) {
+  PRL_REQUIRE(p && out && out_bytes >= (int64_t)sizeof(hipIpcMemHandle_t),
+              "prl_dp_ipc_handle: need %zu bytes", sizeof(hipIpcMemHandle_t));
+  hipIpcMemHandle_t h;
+  PRL_HIP_TRY(hipIpcGetMemHandle(&h, p));
+  memcpy(out, &h, sizeof(h));
+  return PRL_OK;
+}
+
+extern "C" int prl_dp_ipc_open(const uint8_t* handle, int64_t bytes, void** out) {
+  PRL_REQUIRE(handle && out && bytes >= (int64_t)sizeof(hipIpcMemHandle_t), "prl_dp_ipc_open: bad arguments");
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  PRL_HIP_TRY(hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess));
+  return PRL_OK;
+}
+
+extern "C" int prl_dp_ipc_close(void* p) {
+  if (p) PRL_HIP_TRY(hipIpcCloseMemHandle(p));
   return PRL_OK;
 }
 

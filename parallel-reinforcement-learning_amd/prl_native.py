@@ -61,6 +61,14 @@ SIGNATURES = {
     "prl_dp_comm_destroy": [_P],
     "prl_ppo_update_dp": [_P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I32,
                           _I64, _P, _I64] + [_F32] * 9 + [_P, _P, _P, _I64, _P, _P],
+    "prl_ppo_update_dpx": [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32,
+                           _I32, _I32, _P] + [_F32] * 9 + [_P, _I32, _I32, _P, _I64, _P, _I64, _P],
+    "prl_dp_xbuf_bytes": [_I32, _I32, _I32, _I32],
+    "prl_dp_xbuf_alloc": [_I64, _P],
+    "prl_dp_xbuf_free": [_P],
+    "prl_dp_ipc_handle": [_P, _P, _I64],
+    "prl_dp_ipc_open": [_P, _I64, _P],
+    "prl_dp_ipc_close": [_P],
     "prl_ppo_evaluate": [_P, _I32, _I32, _I32, _P, _P, _I64, _P, _P, _P, _P],
     "prl_ppo_image_floats": [_I32, _I32, _I32],
     "prl_ppo_image": [_I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32, _P],
@@ -72,7 +80,7 @@ SIGNATURES = {
     "prl_ppo_grad_fold_step": [_P] * 7 + [_I64, _F32, _I32, _I32, _I32] + [_P] * 5
                               + [_I64, _I32, _I64] + [_F32] * 10 + [_P, _P, _P, _I64, _P],
 }
-_RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64,
+_RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,
              "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
 
 _lib = None
@@ -495,6 +503,71 @@ def ppo_update_dp(img_p, img_m, img_v, D, A, discrete, S, A_, old_logp, adv, ret
         beta2, eps, wd, max_norm, _dev(grad, torch.float32, "grad"),
         _dev(loss_out, torch.float32, "loss"), _dev(workspace, torch.uint8, "workspace"),
         workspace.numel(), comm, _stream()), "prl_ppo_update_dp")
+
+
+# -------------------------------------- data-parallel persistent engine (IPC slice buffers)
+IPC_HANDLE_BYTES = 64
+
+
+def dp_xbuf_bytes(D, A, discrete, mini_batch) -> int:
+    n = int(lib().prl_dp_xbuf_bytes(int(D), int(A), int(bool(discrete)), int(mini_batch)))
+    if n <= 0:
+        raise ValueError(f"prl_dp_xbuf_bytes: shape D={D} A={A} not on the fused engine")
+    return n
+
+
+def dp_xbuf_alloc(nbytes: int) -> ctypes.c_void_p:
+    """A zeroed device allocation of its own (shareable by IPC handle)."""
+    p = ctypes.c_void_p()
+    _check(lib().prl_dp_xbuf_alloc(int(nbytes), ctypes.byref(p)), "prl_dp_xbuf_alloc")
+    return p
+
+
+def dp_xbuf_free(p):
+    if p:
+        _check(lib().prl_dp_xbuf_free(p), "prl_dp_xbuf_free")
+
+
+def dp_ipc_handle(p) -> bytes:
+    buf = ctypes.create_string_buffer(IPC_HANDLE_BYTES)
+    _check(lib().prl_dp_ipc_handle(p, ctypes.cast(buf, ctypes.c_void_p), IPC_HANDLE_BYTES),
+           "prl_dp_ipc_handle")
+    return buf.raw
+
+
+def dp_ipc_open(handle: bytes) -> ctypes.c_void_p:
+    buf = ctypes.create_string_buffer(bytes(handle), IPC_HANDLE_BYTES)
+    p = ctypes.c_void_p()
+    _check(lib().prl_dp_ipc_open(ctypes.cast(buf, ctypes.c_void_p), IPC_HANDLE_BYTES,
+                                 ctypes.byref(p)), "prl_dp_ipc_open")
+    return p
+
+
+def dp_ipc_close(p):
+    if p:
+        _check(lib().prl_dp_ipc_close(p), "prl_dp_ipc_close")
+
+
+def ppo_update_dpx(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp,
+                   adv, ret, mini_batch, k_epochs, nb_union, inv_count, clip, vf_coef, ent_coef,
+                   lr, beta1, beta2, eps, weight_decay, max_norm, loss_out, world, rank, xbufs,
+                   seq0, workspace):
+    """The persistent engine as one data-parallel rank: the cross-rank gradient sum runs inside
+    the launch over the ranks' IPC-mapped slice buffers `xbufs` (rank order)."""
+    N = int(S.shape[0])
+    arr = (ctypes.c_void_p * len(xbufs))(*[ctypes.c_void_p(getattr(x, "value", x)) for x in xbufs])
+    _check(lib().prl_ppo_update_dpx(
+        _dev(params, torch.float32, "params"), _dev(exp_avg, torch.float32, "exp_avg"),
+        _dev(exp_avg_sq, torch.float32, "exp_avg_sq"), _dev(adam_step, torch.float32, "adam_step"),
+        int(D), int(A), int(bool(discrete)), _dev(S, torch.float32, "S"),
+        _dev(actions, torch.float32, "actions"), _dev(old_logp, torch.float32, "old_logp"),
+        _dev(adv, torch.float32, "adv"), _dev(ret, torch.float32, "ret"), N, int(mini_batch),
+        int(k_epochs), int(nb_union), _dev(inv_count, torch.float32, "inv_count"), float(clip),
+        float(vf_coef), float(ent_coef), float(lr), float(beta1), float(beta2), float(eps),
+        float(weight_decay), float(max_norm), _dev(loss_out, torch.float32, "loss_out"),
+        int(world), int(rank), ctypes.cast(arr, ctypes.c_void_p), int(seq0),
+        _dev(workspace, torch.uint8, "workspace"), workspace.numel(), _stream()),
+        "prl_ppo_update_dpx")
 
 
 def ppo_image_floats(D, A, discrete) -> int:

@@ -30,7 +30,7 @@ def _make_ppo(mb, k):
 
 def _worker(rank, world, port, mb, nb, k, out_dir, fused):
     sys.path[:0] = PATHS
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PRL_DP_PERSISTENT="0")
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
@@ -87,6 +87,83 @@ def test_two_ranks_graphed_equal_one_process_on_the_union(tmp_path, fused):
     assert p.last_graph_replays == k * nb - 2
     for key in ref:
         np.testing.assert_allclose(outs[0][key], ref[key], rtol=0, atol=2e-5, err_msg=key)
+
+
+def _dpx_worker(rank, world, port, mb, nb, k, out_dir):
+    sys.path[:0] = PATHS
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PRL_DP_PERSISTENT="1")
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        p = _make_ppo(mb, k)
+        S, A, R, D = _shard(rank, mb, nb)
+        if rank == 1:   # unequal shards: rank 1 has one minibatch less (zero rows in the last)
+            S, A, R, D = (x[:-mb] for x in (S, A, R, D))
+        p.memory.push_device(*(torch.from_numpy(x).cuda() for x in (S, A, R, D)))
+        p.learn()
+        p.learn()       # a second launch on the same slice buffers (flags carry global steps)
+        torch.cuda.synchronize()
+        sd = {kk: v.cpu().numpy() for kk, v in p.policy.state_dict().items()}
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **sd, _path=np.array(p.last_update_path),
+                 _loss=np.float32(p.last_loss.item()))
+        p._engine.close()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def _stepped_worker(rank, world, port, mb, nb, k, out_dir):
+    sys.path[:0] = PATHS
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PRL_DP_PERSISTENT="0")
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        p = _make_ppo(mb, k)
+        S, A, R, D = _shard(rank, mb, nb)
+        if rank == 1:
+            S, A, R, D = (x[:-mb] for x in (S, A, R, D))
+        p.memory.push_device(*(torch.from_numpy(x).cuda() for x in (S, A, R, D)))
+        p.learn()
+        p.learn()
+        torch.cuda.synchronize()
+        sd = {kk: v.cpu().numpy() for kk, v in p.policy.state_dict().items()}
+        np.savez(os.path.join(out_dir, f"stepped{rank}.npz"), **sd,
+                 _path=np.array(p.last_update_path))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_two_ranks_persistent_dp_engine(tmp_path):
+    """prl_ppo_update_dpx on 2 ranks sharing cuda:0 (opt-in PRL_DP_PERSISTENT=1): one persistent
+    launch per rank per learn(), the per-step gradient summed across the ranks INSIDE the
+    kernels over IPC-mapped slice buffers.  Unequal shards, two learn() calls.  Both ranks end
+    bit-identical, and equal the stepped data-parallel loop (grad kernel -> all-reduce -> AdamW
+    per step) in function space: the two sum the gradient norm in different orders
+    (test_stepped_engine_matches_persistent), so bits are not expected to match."""
+    import random
+    mb, nb, k = 64, 5, 3
+    port = 29960 + random.randint(0, 30)
+    mp.spawn(_dpx_worker, args=(2, port, mb, nb, k, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_stepped_worker, args=(2, port + 40, mb, nb, k, str(tmp_path)), nprocs=2, join=True)
+    outs = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(2)]
+    ref = np.load(os.path.join(tmp_path, "stepped0.npz"))
+    assert str(outs[0]["_path"]) == "fused-dp-persistent"
+    assert str(ref["_path"]) == "fused-dp"
+    keys = [kk for kk in outs[0].files if not kk.startswith("_")]
+    for key in keys:
+        np.testing.assert_array_equal(outs[0][key], outs[1][key], err_msg=key)
+    assert np.isfinite(outs[0]["_loss"])
+    import copy
+    import types
+    p = _make_ppo(mb, k)
+    q1 = types.SimpleNamespace(policy=copy.deepcopy(p.policy))
+    q2 = types.SimpleNamespace(policy=copy.deepcopy(p.policy))
+    q1.policy.load_state_dict({kk: torch.from_numpy(outs[0][kk]) for kk in keys})
+    q2.policy.load_state_dict({kk: torch.from_numpy(ref[kk]) for kk in keys})
+    S, A, _, _ = _shard(0, mb, nb)
+    from test_engine_gpu import _outputs
+    (l1, v1), (l2, v2) = (_outputs(q, torch.from_numpy(S[:256]).cuda(),
+                                   torch.from_numpy(A[:256]).cuda()) for q in (q1, q2))
+    assert float((l1 - l2).abs().max()) <= 1e-4 and float((v1 - v2).abs().max()) <= 1e-4
 
 
 def _nccl_one_rank_worker(port, out_dir):
@@ -172,8 +249,8 @@ C5 = dict(env="SyntheticHumanoid-v0", E=16384, cont=True, D=348, A=17, mb=65536,
 @pytest.mark.parametrize("name,cfg", [("c4", C4), ("c5", C5)])
 def test_two_ranks_at_config_per_rank_shape(tmp_path, name, cfg):
     """C4 / C5 per-rank shapes end to end on 2 ranks: independent rollouts (different envs and
-    sampling keys per rank), one data-parallel learn() (C4: stepped engine + all-reduce per
-    step; C5: graphed per-step path + RND update_pred with its gradient all-reduced); both ranks
+    sampling keys per rank), one data-parallel learn() (C4: the data-parallel persistent engine,
+    the default; C5: graphed per-step path + RND update_pred with its gradient all-reduced); both ranks
     end with bit-identical policy (and predictor) weights and finite losses."""
     import random
     port = 29800 + random.randint(0, 150)
@@ -182,7 +259,7 @@ def test_two_ranks_at_config_per_rank_shape(tmp_path, name, cfg):
     assert int(outs[0]["_key"]) != int(outs[1]["_key"])              # rank-mixed sampling keys
     assert not np.array_equal(outs[0]["_head"], outs[1]["_head"])    # different rollouts
     assert min(int(o["_n"]) for o in outs) >= cfg["E"]               # >= one step per env
-    assert str(outs[0]["_path"]) == ("fused-dp" if name == "c4" else "graph")
+    assert str(outs[0]["_path"]) == ("fused-dp-persistent" if name == "c4" else "graph")
     for key in outs[0].files:
         if not key.startswith("_"):
             np.testing.assert_array_equal(outs[0][key], outs[1][key], err_msg=key)
