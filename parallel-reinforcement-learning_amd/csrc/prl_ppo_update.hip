@@ -1932,8 +1932,15 @@ extern "C" int64_t prl_dp_xbuf_bytes(int32_t D, int32_t A, int32_t discrete, int
 
 extern "C" int prl_dp_xbuf_alloc(int64_t bytes, void** out) {
   PRL_REQUIRE(bytes > 0 && out, "prl_dp_xbuf_alloc: bad arguments");
+  // Its own allocation (shareable by IPC handle), UNCACHED: other GPUs read it over xGMI while
+  // this GPU writes it, and coarse-grained memory is not coherent across devices inside a
+  // kernel (RCCL keeps its cross-GPU flags and FIFOs in uncached / fine-grained memory too).
   void* p = nullptr;
-  PRL_HIP_TRY(hipMalloc(&p, (size_t)bytes));   // its own allocation: shareable by IPC handle
+  if (hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached) != hipSuccess) {
+    (void)hipGetLastError();
+    p = nullptr;
+    PRL_HIP_TRY(hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocFinegrained));
+  }
   const hipError_t e = hipMemset(p, 0, (size_t)bytes);
   if (e != hipSuccess) {
     (void)hipFree(p);
