@@ -383,6 +383,62 @@ def test_native_dp_loop_equals_python_loop(cont):
     assert s0 == s1 == 3 * 6 and l0 == l1
 
 
+@pytest.mark.parametrize("cont", [False, True])
+def test_dpx_one_rank_equals_engine(cont):
+    """The data-parallel persistent kernel (prl_ppo_update_dpx) with ONE rank — its own slice
+    buffer, inv_count = float(1 / rows) — gives the single-GPU engine's bits (parameters, both
+    moments, step count, loss) over two learn() calls on one buffer set: its in-GPU part is the
+    engine's, the cross-rank phase adds only the rank-order sum."""
+    import prl_native
+    from PPO import PPO
+    N = 3000 + 7
+    data = _data(N, 3 if cont else 4, cont, seed=31)
+    D, A = (3, 1) if cont else (4, 2)
+    outs = []
+    for dpx in (False, True):
+        torch.manual_seed(0)
+        p = PPO(cont, D, A, action_scaling=2.0 if cont else None, k_epochs=3, batch_size=64,
+                mini_batch_size=512)
+        p.show_progress = False
+        state = {"xb": None, "seq": 0}
+        if dpx:
+            def upd(S, A_, old, adv, ret, n_ranks, p=p, state=state):
+                eng = p._fused_engine()
+                if state["xb"] is None:
+                    state["xb"] = prl_native.dp_xbuf_alloc(
+                        prl_native.dp_xbuf_bytes(eng.D, eng.A, eng.discrete, eng.mini_batch))
+                n, mb = int(S.shape[0]), eng.mini_batch
+                nb = -(-n // mb)
+                inv = torch.tensor([1.0 / min(mb, n - j * mb) for j in range(nb)],
+                                   dtype=torch.float32, device=S.device)
+                group = p.optimizer.param_groups[0]
+                prl_native.ppo_update_dpx(
+                    eng.flat, eng.m, eng.v, eng.step, D, A, eng.discrete, S.contiguous(),
+                    (A_ if A_.dim() == 2 else A_.reshape(-1, 1)).contiguous(), old.contiguous(),
+                    adv.contiguous(), ret.contiguous(), mb, p.k_epochs, nb, inv, p.policy_clip,
+                    p.value_coef, p.entropy_coef, group["lr"], group["betas"][0],
+                    group["betas"][1], group["eps"], group["weight_decay"], 2.0, eng.loss, 1, 0,
+                    [state["xb"]], state["seq"], eng.ws)
+                state["seq"] += p.k_epochs * nb
+                eng._sync_optimizer_state()
+                p.last_loss = eng.loss.reshape(()).clone()
+                p.last_update_path = "dpx1"
+            p._update = upd
+        for _ in range(2):
+            p.memory.push_device(*data)
+            p.learn()
+        torch.cuda.synchronize()
+        eng = p._engine
+        assert max(prl_native.ppo_update_status(eng.ws).tolist()) == 0
+        outs.append((eng.flat.cpu(), eng.m.cpu(), eng.v.cpu(), float(eng.step.item()),
+                     float(p.last_loss)))
+        if state["xb"] is not None:
+            prl_native.dp_xbuf_free(state["xb"])
+    (f0, m0, v0, s0, l0), (f1, m1, v1, s1, l1) = outs
+    assert torch.equal(f0, f1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+    assert s0 == s1 == 2 * 3 * 6 and l0 == l1
+
+
 @pytest.mark.parametrize("cont,D,A", [(False, 6, 3), (True, 5, 2)])
 def test_generic_shape_engine_gradient(cont, D, A):
     """Shapes outside the specialised kernels run the runtime-layout engine (KD = -1): one step at
