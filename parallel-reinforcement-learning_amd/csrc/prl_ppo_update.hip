@@ -286,7 +286,10 @@ constexpr int UPD_RIN = 12;       // row-input record: act[8], old_logp, adv, re
 constexpr int UPD_MAXO = 16;      // outputs of all heads together (one 16-row MFMA tile)
 
 __host__ __device__ inline int upd_xs(int D) { return D <= 16 ? 16 : UPD_ZS; }
-__host__ __device__ inline int upd_scratch_floats(int D, int NW) {
+// transpose slots per wave: one per head for the two-head (discrete) nets, so both heads'
+// backward chains interleave; the three-head (continuous) nets share one slot (LDS is short)
+__host__ __device__ constexpr int upd_ts(const UpdNet& n) { return n.discrete ? 2 : 1; }
+__host__ __device__ inline int upd_scratch_floats(int D, int NW, int TS) {
   return UPD_RT * upd_xs(D)          // Xs  [16][XS]       tile inputs (rows x features)
          + NW * UPD_RT * 16          // Op  [NW][16][16]   output-layer partial per wave
          + NW * UPD_RT * 16          // Os  [NW][16][16]   assembled outputs per wave
@@ -294,7 +297,7 @@ __host__ __device__ inline int upd_scratch_floats(int D, int NW) {
          + UPD_RT * UPD_RIN          // Rin [16][12]       row inputs
          + 2 * UPD_RT * UPD_ZS       // Fs  [2][16][80]    trunk output (double-buffered by tile)
          + UPD_MAXH * UPD_RT * UPD_ZS  // Zs [h][16][80]   head dZ
-         + NW * UPD_RT * 16          // Ts  [NW][16][16]   per-wave transpose slot (G_h, dH0)
+         + NW * TS * UPD_RT * 16     // Ts  [NW][TS][16][16] per-wave transpose slots (G_h; dH0 in 0)
          + 16;
 }
 struct UpdScr {
@@ -808,21 +811,34 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
   }
   upd_wave_sync();
   UPD_CMARK(2)
-  float* Tw = sc.Ts + w * UPD_RT * 16;   // this wave's [16 rows][16 ch] transpose slot
+  // this wave's [16 rows][16 ch] transpose slots (upd_ts): with one per head, every head stores
+  // its G first, then ONE wave sync, so the heads' backward chains below are independent and
+  // interleave; with one shared slot each head waits for the previous head's reads
+  const int TS = upd_ts(n);
+  float* Tw = sc.Ts + w * TS * UPD_RT * 16;
+#pragma unroll
+  for (int hs = 0; hs < HPW; ++hs)
+    if (hs < TS && upd_head<NW>(hs, hg) < nh) upd_st4(Tw + hs * UPD_RT * 16 + x * 16 + 4 * q, f.G[hs]);
+  upd_wave_sync();
 #pragma unroll
   for (int hs = 0; hs < HPW; ++hs) {
     const int h = upd_head<NW>(hs, hg);
     if (h < nh) {
       const UpdHead hi = upd_head_info(n, h);
       const int oc = hi.oc, no = hi.no;
-      // dW2_h[j][16b + x] += sum_rows dO[row][oc + j] G_h[row][ch]  (G_h transposed via Tw)
-      upd_st4(Tw + x * 16 + 4 * q, f.G[hs]);
-      upd_wave_sync();
+      const int slot = TS == 1 ? 0 : hs;
+      if (hs >= TS) {   // the shared slot is free once the previous head has read it
+        upd_wave_sync();
+        upd_st4(Tw + x * 16 + 4 * q, f.G[hs]);
+        upd_wave_sync();
+      }
+      const float* Th = Tw + slot * UPD_RT * 16;
+      // dW2_h[j][16b + x] += sum_rows dO[row][oc + j] G_h[row][ch]  (G_h transposed via Th)
       upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const float a = x < no ? dOw[(4 * s + q) * 16 + oc + x] : 0.0f;
-        acc = upd_mma(a, Tw[(4 * s + q) * 16 + x], acc);
+        acc = upd_mma(a, Th[(4 * s + q) * 16 + x], acc);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -848,7 +864,6 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
       for (int i = 0; i < 4; ++i) dyx[i] = dy[i] * f.xh[hs][i];
       upd_colsum_add(dyx, Ga + hi.g1 + 16 * b + 4 * q, x == 0, first);
       upd_colsum_add(dy, Ga + hi.b1 + 16 * b + 4 * q, x == 0, first);
-      upd_wave_sync();   // Tw reads done before the next head overwrites it
     }
   }
   // inputs, rows x channels, for the weight gradients (the trunk output is in Fs already)
@@ -1168,7 +1183,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
   // 64 KB so every scratch address folds into the ds instructions' 16-bit offset field (no base
   // registers kept live across the step loop)
   float* scratch = upd_lds + UPD_HDR;                                   // tile activations
-  float* W = scratch + ((upd_scratch_floats(n.D, NW) + 3) & ~3);         // [Lp]
+  float* W = scratch + ((upd_scratch_floats(n.D, NW, upd_ts(n)) + 3) & ~3);         // [Lp]
   float* Ga = W + Lp;                                                    // [Lp + 4]
   const UpdScr sc = upd_scr(scratch, n.D, NW);
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
@@ -1415,7 +1430,7 @@ __device__ __forceinline__ void ppo_evaluate_body(const UpdNet& n, const UpdArgs
   extern __shared__ __align__(16) float upd_lds[];
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   float* scratch = upd_lds + UPD_HDR;
-  float* W = scratch + ((upd_scratch_floats(n.D, NW) + 3) & ~3);
+  float* W = scratch + ((upd_scratch_floats(n.D, NW, upd_ts(n)) + 3) & ~3);
   const UpdScr sc = upd_scr(scratch, n.D, NW);
   for (int k = t; k < n.Lp; k += NT) {
     const int f = upd_flat_of(n, k);
@@ -1547,7 +1562,7 @@ __device__ __forceinline__ void ppo_grad_body(const UpdNet& n, const UpdArgs& ar
   const int Lp = n.Lp, Qp = Lp / 4, Qtot = Qp + 1;
   float* hdr = upd_lds;
   float* scratch = upd_lds + UPD_HDR;
-  float* W = scratch + ((upd_scratch_floats(n.D, NW) + 3) & ~3);
+  float* W = scratch + ((upd_scratch_floats(n.D, NW, upd_ts(n)) + 3) & ~3);
   float* Ga = W + Lp;
   const UpdScr sc = upd_scr(scratch, n.D, NW);
   float* s_ssq = hdr + 4;
@@ -1738,7 +1753,7 @@ hipError_t upd_launch_resident(const void* kern, int G, int threads, size_t lds,
 }
 
 size_t upd_lds_bytes(const UpdNet& n) {
-  return sizeof(float) * (size_t)(UPD_HDR + 2 * n.Lp + 4 + ((upd_scratch_floats(n.D, upd_nw_host(n)) + 3) & ~3));
+  return sizeof(float) * (size_t)(UPD_HDR + 2 * n.Lp + 4 + ((upd_scratch_floats(n.D, upd_nw_host(n), upd_ts(n)) + 3) & ~3));
 }
 
 struct UpdWs {
@@ -1989,7 +2004,7 @@ extern "C" int prl_ppo_evaluate(const float* params, int32_t D, int32_t A, int32
   args.S = S;
   args.act = actions;
   args.N = N;
-  const size_t lds = sizeof(float) * (size_t)(UPD_HDR + args.net.Lp + ((upd_scratch_floats(D, upd_nw_host(args.net)) + 3) & ~3));
+  const size_t lds = sizeof(float) * (size_t)(UPD_HDR + args.net.Lp + ((upd_scratch_floats(D, upd_nw_host(args.net), upd_ts(args.net)) + 3) & ~3));
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_evaluate: %zu B of LDS needed", lds);
   const unsigned grid = (unsigned)std::min<int64_t>(cdiv(N, UPD_RT), 2 * 256);
   const void* kern = upd_eval_kernel_for(args.net);
