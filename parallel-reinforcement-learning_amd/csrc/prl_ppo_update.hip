@@ -722,7 +722,8 @@ __device__ inline void upd_tile_fwd(const UpdNet& n, const float* W, const UpdSc
 }
 
 // After the barrier that publishes Op: lanes q == 0 of every wave assemble row x's outputs
-// (the NW partials in wave order, then the bias) into Os[w][x][*]; returns the pointer.  A head's
+// (the NW partials in wave order, then the bias) into Os[w][x][*]; returns the pointer.  Every
+// caller reads a row only from the lane that wrote it, so no wave sync follows.  A head's
 // output gets exact zeros from the other head group's waves, so 4 and 8 waves give equal bits.
 template <int NW>
 __device__ inline const float* upd_tile_outputs(const UpdNet& n, const float* W, const UpdScr& sc) {
@@ -747,7 +748,6 @@ __device__ inline const float* upd_tile_outputs(const UpdNet& n, const float* W,
       upd_st4(Orow + 4 * j4, v);
     }
   }
-  upd_wave_sync();
   return Orow;
 }
 
@@ -968,7 +968,7 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
       if (tl_ == 0) upd_gadd(Ga + n.Lp + k, s, first);
     }
   }
-  upd_wave_sync();   // Tw reads done before the next tile
+  // (the next tile rewrites Tw only after its barrier #0)
   UPD_CMARK(7)
 #undef UPD_CMARK
 }
