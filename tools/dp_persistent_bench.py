@@ -54,11 +54,14 @@ def _worker(rank, world, port, n, out):
                 e.synchronize()
                 ts.append(s.elapsed_time(e))
             res[name] = round(min(ts) * 1e3 / steps, 2)
+            if os.environ.get("PRL_UPD_PROFILE") == "1" and (name == "dpx" or rank == 0):
+                res[name + "_phases"] = eng.profile()
         torch.distributed.barrier()
         if rank == 0:
             with open(out, "w") as f:
                 json.dump({"world": world, "rows_per_rank": n, "steps": steps,
-                           "us_per_step_dpx": res["dpx"], "us_per_step_single_engine": res["single"]}, f)
+                           "us_per_step_dpx": res["dpx"], "us_per_step_single_engine": res["single"],
+                           **{k: v for k, v in res.items() if k.endswith("_phases")}}, f)
         eng.close()
     finally:
         torch.distributed.destroy_process_group()
