@@ -268,6 +268,25 @@ int prl_ppo_grad_fold_step(const float* in_p, const float* in_m, const float* in
                            float ent_coef, float lr, float beta1, float beta2, float eps,
                            float weight_decay, float max_norm, float* loss_out, float* grad_out,
                            void* workspace, int64_t workspace_bytes, void* stream);
+/* ---- wide-net optimizer step (shapes outside the persistent engine: D <= 352, <= 48 outputs) -- */
+/* Host call: parameter count, partial-gradient scratch floats and grid of prl_ppo_wide_grad for
+ * ActorCritic(is_continuous = !discrete, D, A) at mini_batch; PRL_ERR_ARG (outputs 0) for shapes
+ * outside it.  Replaces, for those shapes, the per-step forward + loss + backward of
+ * PPO/PPO.py:219-249 (get_evaluate, the surrogate, loss.mean().backward()). */
+int prl_ppo_wide_info(int32_t D, int32_t A, int32_t discrete, int64_t mini_batch,
+                      int64_t* n_params, int64_t* part_floats, int32_t* grid);
+/* One optimizer step's gradient: minibatch j = *cursor (device int64; rows [j*mb, min((j+1)*mb, N))
+ * of S [N][D], actions [N][discrete ? 1 : A], old_logp, adv, ret), loss = mean(-min(surr1,
+ * surr2)) + vf_coef * SmoothL1(V, ret) - ent_coef * H (PPO.py:225-245; H detached) times
+ * scales[j] (device f32, null = 1), its gradient w.r.t. params (flat f32, torch parameters()
+ * order) into grad [n_params], the loss into loss_out[0] (nullable).  part: prl_ppo_wide_info's
+ * part_floats of scratch.  Two launches on `stream`, no host synchronisation (graph-capturable);
+ * deterministic (fixed summation order). */
+int prl_ppo_wide_grad(const float* params, int32_t D, int32_t A, int32_t discrete, const float* S,
+                      const float* actions, const float* old_logp, const float* adv,
+                      const float* ret, int64_t N, int64_t mini_batch, const int64_t* cursor,
+                      const float* scales, float clip, float vf_coef, float ent_coef, float* grad,
+                      float* loss_out, float* part, int64_t part_floats, void* stream);
 /* Column sums out[c] = sum_r x[r][c] of a row-major f32 matrix (cols >= 1): the bias
  * gradient of a Linear over a large batch (nn.Linear backward, reached from PPO.py:249 /
  * RND.py:112).  Two deterministic passes; `partial` holds prl_colsum_partial_floats(rows, cols)

@@ -339,6 +339,10 @@ class PPO:
                 loss = graphed.loss_out
                 pbar.update(sum(counts[:j0]))
             for j in range(j0, nb):
+                if graphed is not None and graphed.wide is not None and world == 1:
+                    loss = graphed.wide_step(j)
+                    pbar.update(counts[j])
+                    continue
                 out = self._eager_step(S, A, old_logp, adv, returns, j, counts[j], world)
                 loss = out if out is not None else loss
                 pbar.update(counts[j])

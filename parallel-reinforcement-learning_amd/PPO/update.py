@@ -15,6 +15,8 @@ run through PPO._eager_step.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -53,9 +55,47 @@ class GraphedUpdate:
         self.graph = None
         self.replays = 0
         prl_native.reserve_workspace(mb, dev)
+        # wide nets (outside the persistent engine, e.g. C5's D = 348, A = 17): the step's
+        # forward + loss + backward is prl_ppo_wide_grad (two HIP launches reading the minibatch
+        # in place) instead of ~60 PyTorch / hipBLASLt kernels; PRL_WIDE=0 keeps the autograd step
+        self.wide = None
+        info = (prl_native.ppo_wide_info(S.shape[1], ppo.action_dim, not ppo.is_continuous, mb)
+                if os.environ.get("PRL_WIDE", "1") == "1" else None)
+        if info is not None and info[0] == sum(self.sizes) == sum(
+                p.numel() for p in ppo.policy.parameters()):
+            self.wide = info
+            self.pflat = torch.empty(info[0], dtype=torch.float32, device=dev)
+            self.part = torch.empty(info[1], dtype=torch.float32, device=dev)
+            self.cursor_e = torch.zeros(1, dtype=torch.int64, device=dev)
+            self.sources[1] = self.sources[1].float().contiguous()
+
+    def _wide_grad(self, cursor, scales):
+        """Gradient of minibatch `cursor` into the flat gradient buffer (p.grad views) or, on
+        data-parallel ranks, into self.flat (the all-reduce buffer); loss into loss_out."""
+        ppo = self.ppo
+        grads = ppo._ensure_flat_grads()
+        torch.cat([p.detach().reshape(-1) for p in self.params], out=self.pflat)
+        S, A2, old, adv, ret = self.sources
+        prl_native.ppo_wide_grad(self.pflat, S.shape[1], ppo.action_dim, not ppo.is_continuous,
+                                 S, A2, old, adv, ret, self.mb, cursor, scales, ppo.policy_clip,
+                                 ppo.value_coef, ppo.entropy_coef,
+                                 self.flat if scales is not None else grads, self.loss_out,
+                                 self.part)
+
+    def wide_step(self, j: int):
+        """One eager optimizer step on minibatch j through the wide kernel (single rank: the
+        ragged last minibatch of an epoch)."""
+        self.cursor_e.fill_(j)
+        self._wide_grad(self.cursor_e, None)
+        nn.utils.clip_grad_norm_(self.params, 2.0)
+        self.ppo.optimizer.step()
+        return self.loss_out
 
     def _forward_backward(self):
         ppo = self.ppo
+        if self.wide is not None:
+            self._wide_grad(self.cursor, self.scales)
+            return
         self.gather()
         logp, V, H = ppo.policy.get_evaluate(self.S_mb, self.A_eval)
         loss = self.SurrogateLoss.apply(logp, self.old_mb, self.adv_mb, V, self.ret_mb, H,

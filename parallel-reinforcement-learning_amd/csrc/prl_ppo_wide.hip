@@ -1,0 +1,881 @@
+// prl_ppo_wide.hip — one optimizer step's gradient for the wide nets the persistent engine cannot
+// hold (observation dim D up to 352, up to 48 head outputs: C5's D = 348 synthetic Humanoid with
+// A = 17, i.e. mu 17 + log_std 17 + critic 1).  Forward (ActorCritic.get_evaluate,
+// PPO/ActorCritic.py:118-146) -> clipped surrogate + 0.5 SmoothL1 (PPO/PPO.py:225-245; entropy
+// detached) -> backward of the whole net for the minibatch of `cursor`, in ONE kernel, then a
+// deterministic fold of the per-workgroup partial gradients (second kernel).  clip_grad_norm_ and
+// AdamW stay torch's (capturable, fused) on the flat gradient, as in the graphed per-step path.
+//
+// Why its own kernel: the persistent engine keeps the parameters AND the gradient image in one
+// CU's LDS (~2 x 150 KB for C5: does not fit), and C5's per-step graph was ~60 kernels, 1.3 ms per
+// 65,536-row step.  Here the minibatch is wide (65,536 rows = 4,096 16-row tiles), so there is no
+// hand-off inside the step: workgroup g walks tiles g, g + G, ... and accumulates ITS gradient in
+// registers (MFMA accumulators), writes it once to part[g], and a second kernel sums part[0..G)
+// in workgroup order.
+//
+// Per workgroup (256 threads = 4 waves, one per SIMD; wave w owns channel block w = channels
+// 16w .. 16w+15 of every 64-wide layer; activations live in v_mfma_f32_16x16x4_f32 C fragments,
+// lane (x = l & 15, q = l >> 4) register i = [row x][channel 16w + 4q + i]):
+//   registers: W0 block w as A fragments (KSM k-steps, read once), dW0 block w (KSM / 4 16-column
+//              accumulators), dW1 / dW2 blocks, GroupNorm gamma / beta gradient quads;
+//   LDS:       the heads' parameters (W1, GN, W2, b2, trunk GN), the tile's inputs (double
+//              buffered: the next tile stages while a slower wave still reads this one's), trunk
+//              output F, head outputs G, the outputs O / dO, head dZ, per-wave transpose slots.
+// Per 16-row tile, 5 workgroup barriers: stage X | trunk fwd -> F | heads fwd -> G | output layer
+// -> O | row loss -> dO | heads bwd (dW2, dZ) | dW1, dF, trunk GN bwd, dW0.
+#include "prl_common.h"
+
+#include <float.h>
+
+#include <algorithm>
+
+namespace prl {
+namespace {
+
+constexpr int WD_THREADS = 256;
+constexpr int WD_H = 64;
+constexpr int WD_HS = 68;      // LDS row stride of the [*][64] weight matrices
+constexpr int WD_RT = 16;      // rows per tile
+constexpr int WD_MAXH = 3;
+constexpr int WD_MAXO = 48;    // outputs of all heads (three 16-row output tiles)
+constexpr int WD_MAXHO = 32;   // outputs of one head (two 16-row tiles)
+constexpr int WD_MAXA = 32;
+constexpr int WD_FS = 80;      // row stride of F and dZ tiles [16][64]
+constexpr int WD_GS = 196;     // row stride of the head outputs [16][3 * 64] (== 4 mod 64)
+constexpr int WD_OS = 52;      // row stride of O / dO [16][48]
+constexpr int WD_RS = 36;      // row-input record: act[32], old_logp, adv, ret, pad
+constexpr int WD_GRID_MAX = 256;
+
+struct WdNet {
+  int D, A, nh, discrete, nout, P, Pq;      // Pq: P rounded up to 4 (loss slots at Pq .. Pq+2)
+  int out[WD_MAXH], ocol[WD_MAXH];
+  // flat offsets (torch parameters() order: model.0.weight, model.1.{weight,bias}, then every
+  // head's 0.weight, 1.weight, 1.bias, 3.weight, 3.bias)
+  int w0, g0, b0, w1[WD_MAXH], g1[WD_MAXH], b1[WD_MAXH], w2[WD_MAXH], b2[WD_MAXH];
+  // LDS offsets of the head parameter image (floats)
+  int Lg0, Lb0, Lw1[WD_MAXH], Lg1[WD_MAXH], Lb1[WD_MAXH], Lw2[WD_MAXH], Lb2[WD_MAXH], Lp;
+};
+
+bool wd_layout(int D, int A, int discrete, WdNet& n) {
+  n = WdNet{};
+  if (D < 1 || A < 1 || A > WD_MAXA) return false;
+  n.D = D;
+  n.A = A;
+  n.discrete = discrete ? 1 : 0;
+  n.nh = discrete ? 2 : 3;
+  int flat = 0, lds = 0;
+  auto lds_add = [&](int floats) {
+    const int o = lds;
+    lds += (floats + 3) & ~3;
+    return o;
+  };
+  n.w0 = flat; flat += WD_H * D;
+  n.g0 = flat; flat += WD_H;
+  n.b0 = flat; flat += WD_H;
+  n.Lg0 = lds_add(WD_H);
+  n.Lb0 = lds_add(WD_H);
+  int col = 0;
+  for (int h = 0; h < n.nh; ++h) {
+    const int out = (h == n.nh - 1) ? 1 : A;
+    if (out > WD_MAXHO) return false;
+    n.out[h] = out;
+    n.ocol[h] = col;
+    col += out;
+    n.w1[h] = flat; flat += WD_H * WD_H;
+    n.g1[h] = flat; flat += WD_H;
+    n.b1[h] = flat; flat += WD_H;
+    n.w2[h] = flat; flat += out * WD_H;
+    n.b2[h] = flat; flat += out;
+    n.Lw1[h] = lds_add(WD_H * WD_HS);
+    n.Lg1[h] = lds_add(WD_H);
+    n.Lb1[h] = lds_add(WD_H);
+    n.Lw2[h] = lds_add(out * WD_HS);
+    n.Lb2[h] = lds_add(out);
+  }
+  n.nout = col;
+  if (n.nout > WD_MAXO) return false;
+  n.P = flat;
+  n.Pq = (flat + 3) & ~3;
+  n.Lp = lds;
+  return true;
+}
+
+// tile scratch after the parameter image (floats)
+__host__ __device__ inline int wd_xs(int KSM) { return 4 * KSM + 4; }   // X row stride (== 4 mod 32)
+__host__ __device__ inline int wd_scratch_floats(int KSM) {
+  return 2 * WD_RT * wd_xs(KSM)      // Xs  [2][16][XS]   tile inputs (double-buffered)
+         + 2 * WD_RT * WD_RS         // Rin [2][16][36]   row inputs (double-buffered)
+         + WD_RT * WD_FS             // Fs  [16][80]      trunk output
+         + WD_RT * WD_GS             // Gs  [16][196]     head outputs (3 x 64 channels)
+         + 2 * WD_RT * WD_OS         // Os, dOs [16][52]  outputs, d loss / d outputs
+         + WD_MAXH * WD_RT * WD_FS   // Zs  [3][16][80]   head dZ
+         + 4 * WD_RT * 16;           // Tw  [4][16][16]   per-wave dH0 transpose slot
+}
+inline size_t wd_lds_bytes(const WdNet& n, int KSM) {
+  return sizeof(float) * (size_t)(n.Lp + wd_scratch_floats(KSM));
+}
+
+struct WdArgs {
+  WdNet net;
+  const float* params;     // flat, torch parameters() order
+  const float* S;          // [N][D]
+  const float* act;        // [N][Aw]
+  const float* old_logp;   // [N]
+  const float* adv;        // [N]
+  const float* ret;        // [N]
+  const int64_t* cursor;   // device: minibatch index j (rows j*mb .. min((j+1)*mb, N))
+  const float* scales;     // device [nb] loss scale per minibatch (data-parallel ranks) or null
+  int64_t N, mb;
+  float clip, vf_coef;
+  float* part;             // [G][Pq + 4]
+  int G;
+};
+
+typedef float wd_v4 __attribute__((ext_vector_type(4)));
+__device__ inline wd_v4 wd_mma(float a, float b, wd_v4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ inline wd_v4 wd_ld4(const float* p) {
+  const float4 v = *reinterpret_cast<const float4*>(p);
+  return wd_v4{v.x, v.y, v.z, v.w};
+}
+__device__ inline void wd_st4(float* p, wd_v4 v) {
+  *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
+}
+__device__ inline void wd_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ inline float wd_exp(float x) { return __expf(x); }
+__device__ inline float wd_log(float x) { return __logf(x); }
+__device__ inline float wd_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ inline float wd_sigmoid(float y) { return wd_rcp(1.0f + wd_exp(-y)); }
+template <int CTRL>
+__device__ inline float wd_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// sum over the 16 lanes of a DPP row (the tile's 16 rows, for one channel quad)
+__device__ inline float wd_rsum16(float v) {
+  v += wd_dpp<0xB1>(v);
+  v += wd_dpp<0x4E>(v);
+  v += wd_dpp<0x141>(v);
+  v += wd_dpp<0x140>(v);
+  return v;
+}
+// v + the partner lane l ^ 16's v (the other 4 channels of the lane's GroupNorm group)
+__device__ inline float wd_pair_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// GroupNorm(8 groups of 8, eps 1e-5) + SiLU on a C fragment (PPO/ActorCritic.py:19-22)
+__device__ inline void wd_gn_fwd(wd_v4 z, wd_v4 gw, wd_v4 gb, wd_v4& xh, float& rstd, wd_v4& y) {
+  const float s4 = (z[0] + z[1]) + (z[2] + z[3]);
+  const float mean = wd_pair_sum(s4) * 0.125f;
+  wd_v4 d;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d[i] = z[i] - mean;
+  const float q4 = (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+  rstd = __builtin_amdgcn_rsqf(wd_pair_sum(q4) * 0.125f + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    xh[i] = d[i] * rstd;
+    const float u = xh[i] * gw[i] + gb[i];
+    y[i] = u * wd_sigmoid(u);
+  }
+}
+__device__ inline wd_v4 wd_gn_bwd(wd_v4 go, wd_v4 xh, wd_v4 gw, wd_v4 gb, float rstd, wd_v4& dy) {
+  wd_v4 dxh;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float u = xh[i] * gw[i] + gb[i];
+    const float sg = wd_sigmoid(u);
+    dy[i] = go[i] * (sg * (1.0f + u * (1.0f - sg)));
+    dxh[i] = dy[i] * gw[i];
+  }
+  const float a4 = (dxh[0] + dxh[1]) + (dxh[2] + dxh[3]);
+  const float b4 = (dxh[0] * xh[0] + dxh[1] * xh[1]) + (dxh[2] * xh[2] + dxh[3] * xh[3]);
+  const float m1 = wd_pair_sum(a4) * 0.125f;
+  const float m2 = wd_pair_sum(b4) * 0.125f;
+  wd_v4 dx;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dx[i] = rstd * (dxh[i] - m1 - xh[i] * m2);
+  return dx;
+}
+
+// head h's offsets, selected over compile-time indices (no dynamic indexing of the kernarg struct)
+struct WdHead {
+  int Lw1, Lg1, Lb1, Lw2, Lb2, oc, no;
+};
+__device__ inline WdHead wd_head(const WdNet& n, int h) {
+  WdHead r{n.Lw1[0], n.Lg1[0], n.Lb1[0], n.Lw2[0], n.Lb2[0], n.ocol[0], n.out[0]};
+#pragma unroll
+  for (int k = 1; k < WD_MAXH; ++k)
+    if (h == k) r = WdHead{n.Lw1[k], n.Lg1[k], n.Lb1[k], n.Lw2[k], n.Lb2[k], n.ocol[k], n.out[k]};
+  return r;
+}
+
+// Row loss (the persistent engine's upd_row_loss arithmetic, for up to 32 actions, reading the
+// outputs from LDS): writes dO[0 .. 48) (zeros past nout) and returns {-min(s1,s2), SmoothL1, H}.
+__device__ inline void wd_row_loss(const WdNet& n, const float* O, const float* rin, float invB,
+                                   float clip, float vf_coef, float* dO, float (&lp)[3]) {
+  const int A = n.A;
+  const bool discrete = n.discrete != 0;
+  const int vcol = discrete ? A : 2 * A;
+  float logp = 0.f, H = 0.f;
+  // discrete: softmax then torch's Categorical(probs) renormalisation + clamped log
+  float mx = 0.f, rs = 1.f, rS2 = 1.f, qa = 1.f;
+  int ai = 0;
+  if (discrete) {
+    mx = O[0];
+    for (int k = 1; k < A; ++k) mx = fmaxf(mx, O[k]);
+    float s = 0.f;
+    for (int k = 0; k < A; ++k) s += wd_exp(O[k] - mx);
+    rs = wd_rcp(s);
+    float S2 = 0.f;
+    for (int k = 0; k < A; ++k) S2 += wd_exp(O[k] - mx) * rs;
+    rS2 = wd_rcp(S2);
+    ai = (int)rin[0];
+    const bool bad = ai < 0 || ai >= A;
+    float la = 0.f;
+    for (int k = 0; k < A; ++k) {
+      const float qk = (wd_exp(O[k] - mx) * rs) * rS2;
+      const float c = qk < FLT_EPSILON ? FLT_EPSILON : (qk > 1.0f - FLT_EPSILON ? 1.0f - FLT_EPSILON : qk);
+      const float l = wd_log(c);
+      H += l * qk;
+      if (k == ai) { la = l; qa = qk; }
+    }
+    H = -H;
+    logp = bad ? __builtin_nanf("") : la;
+    // S2 is needed below through rS2 only
+  } else {
+    const float half_log_2pi = 0.91893853320467274f;
+    for (int k = 0; k < A; ++k) {
+      const float mu = O[k];
+      const float lsr = O[A + k];
+      const float lsc = lsr < -2.0f ? -2.0f : (lsr > 2.0f ? 2.0f : lsr);
+      const float sd = wd_log(1.0f + wd_exp(lsc));
+      const float dd = rin[k] - mu;
+      const float lsd = wd_log(sd);
+      logp += -(dd * dd) * wd_rcp(2.0f * (sd * sd)) - lsd - half_log_2pi;
+      H += 0.5f + half_log_2pi + lsd;
+    }
+  }
+  const float V = O[vcol];
+  const float diff = logp - rin[32];
+  const float cl = diff < -20.0f ? -20.0f : (diff > 20.0f ? 20.0f : diff);
+  const float ratio = wd_exp(cl);
+  const float adv = rin[33];
+  const float s1 = ratio * adv;
+  const float lo = 1.0f - clip, hi = 1.0f + clip;
+  const float rcl = ratio < lo ? lo : (ratio > hi ? hi : ratio);
+  const float s2 = rcl * adv;
+  const float m = (s1 != s1 || s2 != s2) ? __builtin_nanf("") : fminf(s1, s2);
+  float w1, w2;
+  if (s1 < s2) { w1 = 1.0f; w2 = 0.0f; }
+  else if (s2 < s1) { w1 = 0.0f; w2 = 1.0f; }
+  else { w1 = 0.5f; w2 = 0.5f; }
+  const float in_clip = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
+  const float in_20 = (diff >= -20.0f && diff <= 20.0f) ? 1.0f : 0.0f;
+  const float dlogp = -invB * (w1 * adv + w2 * adv * in_clip) * ratio * in_20;
+  const float x = V - rin[34];
+  const float ax = fabsf(x);
+  const float sl = ax < 1.0f ? 0.5f * ax * ax : ax - 0.5f;
+  const float gx = ax < 1.0f ? x : (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f));
+  lp[0] = -m;
+  lp[1] = sl;
+  lp[2] = H;
+  for (int j = 0; j < WD_MAXO; ++j) dO[j] = 0.f;
+  dO[vcol] = vf_coef * invB * gx;
+  if (discrete) {
+    const float mk = (qa >= FLT_EPSILON && qa <= 1.0f - FLT_EPSILON) ? 1.0f : 0.0f;
+    const float gq = (logp != logp) ? logp : dlogp * mk;
+    const float rqa = wd_rcp(qa);
+    // dp_k = gq (1[k = a] / qa - 1) / S2;  dO_k = p_k (dp_k - sum_k' p_k' dp_k')
+    float dot = 0.f;
+    for (int k = 0; k < A; ++k) {
+      const float pk = wd_exp(O[k] - mx) * rs;
+      dot += pk * (gq * (((k == ai) ? rqa : 0.0f) - 1.0f) * rS2);
+    }
+    for (int k = 0; k < A; ++k) {
+      const float pk = wd_exp(O[k] - mx) * rs;
+      const float dpk = gq * (((k == ai) ? rqa : 0.0f) - 1.0f) * rS2;
+      dO[k] = pk * (dpk - dot);
+    }
+  } else {
+    for (int k = 0; k < A; ++k) {
+      const float mu = O[k];
+      const float lsr = O[A + k];
+      const float lsc = lsr < -2.0f ? -2.0f : (lsr > 2.0f ? 2.0f : lsr);
+      const float sd = wd_log(1.0f + wd_exp(lsc));
+      const float d = rin[k] - mu;
+      const float var = sd * sd;
+      const float rvar = wd_rcp(var), rsd = wd_rcp(sd);
+      dO[k] = dlogp * (d * rvar);
+      const float dsd = dlogp * ((d * d) * (rvar * rsd) - rsd);
+      const float pass = (lsr >= -2.0f && lsr <= 2.0f) ? 1.0f : 0.0f;
+      dO[A + k] = dsd * wd_sigmoid(lsc) * pass;
+    }
+  }
+}
+
+// Stage tile rows [row0, row0 + rc) of S into Xs (rows >= rc and columns >= D stay / become 0)
+// and the row records into Rin.
+__device__ inline void wd_stage(const WdNet& n, const WdArgs& a, int64_t row0, int rc, int XS,
+                                float* Xs, float* Rin) {
+  const int t = threadIdx.x, D = n.D;
+  const float* src = a.S + row0 * D;
+  const int tot = WD_RT * D, have = rc * D;
+  if ((D & 3) == 0 && ((reinterpret_cast<uintptr_t>(a.S) & 15u) == 0)) {
+    for (int f = 4 * t; f < tot; f += 4 * WD_THREADS) {
+      const int r = f / D, d = f - r * D;
+      const float4 v = f < have ? *reinterpret_cast<const float4*>(src + f) : float4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<float4*>(Xs + r * XS + d) = v;
+    }
+  } else {
+    for (int f = t; f < tot; f += WD_THREADS) {
+      const int r = f / D, d = f - r * D;
+      Xs[r * XS + d] = f < have ? src[f] : 0.f;
+    }
+  }
+  const int Aw = n.discrete ? 1 : n.A;
+  for (int e = t; e < WD_RT * WD_RS; e += WD_THREADS) {
+    const int r = e / WD_RS, k = e - r * WD_RS;
+    float v = 0.f;
+    if (r < rc) {
+      const int64_t row = row0 + r;
+      if (k < WD_MAXA) v = k < Aw ? a.act[row * Aw + k] : 0.f;
+      else if (k == 32) v = a.old_logp[row];
+      else if (k == 33) v = a.adv[row];
+      else if (k == 34) v = a.ret[row];
+    }
+    Rin[e] = v;
+  }
+}
+
+template <int KSM>
+__global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) {
+  constexpr int KE = KSM / 4;          // 16-column blocks of dW0
+  extern __shared__ float4 wd_lds4[];
+  float* lds = reinterpret_cast<float*>(wd_lds4);
+  const WdNet& n = a.net;
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  const int D = n.D, nh = n.nh;
+  const int XS = wd_xs(KSM);
+  float* W = lds;
+  float* p = lds + n.Lp;
+  float* Xs0 = p; p += 2 * WD_RT * XS;
+  float* Rin0 = p; p += 2 * WD_RT * WD_RS;
+  float* Fs = p; p += WD_RT * WD_FS;
+  float* Gs = p; p += WD_RT * WD_GS;
+  float* Os = p; p += WD_RT * WD_OS;
+  float* dOs = p; p += WD_RT * WD_OS;
+  float* Zs = p; p += WD_MAXH * WD_RT * WD_FS;
+  float* Tw = p + w * WD_RT * 16;
+
+  // ---- minibatch of this step
+  const int64_t j = *a.cursor;
+  const int64_t row_lo = j * a.mb;
+  const int64_t rows = row_lo < a.N ? (a.N - row_lo < a.mb ? a.N - row_lo : a.mb) : 0;
+  const float invB = rows > 0 ? (a.scales ? a.scales[j] : 1.0f) / (float)rows : 0.f;
+  const int ntile = (int)((rows + WD_RT - 1) / WD_RT);
+
+  // ---- head parameters -> LDS (padding entries 0); both X buffers' pad columns -> 0
+  for (int k = t; k < n.Lp; k += WD_THREADS) W[k] = 0.f;
+  for (int k = t; k < 2 * WD_RT * XS; k += WD_THREADS) Xs0[k] = 0.f;
+  __syncthreads();
+  for (int k = t; k < WD_H; k += WD_THREADS) {
+    W[n.Lg0 + k] = a.params[n.g0 + k];
+    W[n.Lb0 + k] = a.params[n.b0 + k];
+  }
+#pragma unroll
+  for (int h = 0; h < WD_MAXH; ++h) {
+    if (h < nh) {
+      const WdHead hi = wd_head(n, h);
+      int fw1 = n.w1[0], fg1 = n.g1[0], fb1 = n.b1[0], fw2 = n.w2[0], fb2 = n.b2[0];
+      if (h == 1) { fw1 = n.w1[1]; fg1 = n.g1[1]; fb1 = n.b1[1]; fw2 = n.w2[1]; fb2 = n.b2[1]; }
+      if (h == 2) { fw1 = n.w1[2]; fg1 = n.g1[2]; fb1 = n.b1[2]; fw2 = n.w2[2]; fb2 = n.b2[2]; }
+      for (int k = t; k < WD_H * WD_H; k += WD_THREADS)
+        W[hi.Lw1 + (k >> 6) * WD_HS + (k & 63)] = a.params[fw1 + k];
+      for (int k = t; k < WD_H; k += WD_THREADS) {
+        W[hi.Lg1 + k] = a.params[fg1 + k];
+        W[hi.Lb1 + k] = a.params[fb1 + k];
+      }
+      for (int k = t; k < hi.no * WD_H; k += WD_THREADS)
+        W[hi.Lw2 + (k >> 6) * WD_HS + (k & 63)] = a.params[fw2 + k];
+      for (int k = t; k < hi.no; k += WD_THREADS) W[hi.Lb2 + k] = a.params[fb2 + k];
+    }
+  }
+  // trunk weight block w: rows 16w + x of W0, read per tile from L2 as 16-B A fragments (K order
+  // permuted so a lane's four k-steps of a 16-column group are 4 consecutive columns: step
+  // (sg, i) <-> column 16 sg + 4 q + i, the same permutation on the X side); registers hold the
+  // dW0 accumulators instead
+  const float* w0row = a.params + n.w0 + (int64_t)(16 * w + x) * D;
+  const bool w0vec = (D & 3) == 0 && ((reinterpret_cast<uintptr_t>(a.params) & 15u) == 0);
+  // gradient accumulators
+  wd_v4 gW0[KE];
+  wd_v4 gW1[WD_MAXH][4];
+  wd_v4 gW2[WD_MAXH][2];
+  wd_v4 gg1[WD_MAXH], gb1[WD_MAXH], gg0, gb0;
+  const wd_v4 z4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < KE; ++e) gW0[e] = z4;
+#pragma unroll
+  for (int h = 0; h < WD_MAXH; ++h) {
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) gW1[h][bb] = z4;
+    gW2[h][0] = z4;
+    gW2[h][1] = z4;
+    gg1[h] = z4;
+    gb1[h] = z4;
+  }
+  gg0 = z4;
+  gb0 = z4;
+  double gbias = 0.0;                 // wave 3, lane l < nout: output bias l
+  double lpacc[3] = {0.0, 0.0, 0.0};  // wave 0, lanes x < 16, q == 0: loss terms of row x
+
+  int it = 0;
+  for (int tile = blockIdx.x; tile < ntile; tile += a.G, ++it) {
+    const int64_t row0 = row_lo + (int64_t)tile * WD_RT;
+    const int rc = (int)(rows - (int64_t)tile * WD_RT < WD_RT ? rows - (int64_t)tile * WD_RT : WD_RT);
+    float* Xs = Xs0 + (it & 1) * WD_RT * XS;
+    float* Rin = Rin0 + (it & 1) * WD_RT * WD_RS;
+    wd_stage(n, a, row0, rc, XS, Xs, Rin);
+    __syncthreads();   // #1: Xs, Rin (and, on the first tile, the parameter image)
+
+    // ---- trunk: H0^T block w = W0 block w X^T, GroupNorm + SiLU
+    wd_v4 xh0, Fw;
+    float r0;
+    {
+      wd_v4 acc[4] = {z4, z4, z4, z4};
+#pragma unroll
+      for (int sg = 0; sg < KSM / 4; ++sg) {
+        const int d0 = 16 * sg + 4 * q;
+        if (16 * sg < D) {
+          float4 wv;
+          if (w0vec) {
+            wv = d0 < D ? *reinterpret_cast<const float4*>(w0row + d0) : float4{0.f, 0.f, 0.f, 0.f};
+          } else {
+            wv.x = d0 < D ? w0row[d0] : 0.f;
+            wv.y = d0 + 1 < D ? w0row[d0 + 1] : 0.f;
+            wv.z = d0 + 2 < D ? w0row[d0 + 2] : 0.f;
+            wv.w = d0 + 3 < D ? w0row[d0 + 3] : 0.f;
+          }
+          const float4 xv = *reinterpret_cast<const float4*>(Xs + x * XS + d0);
+          acc[0] = wd_mma(wv.x, xv.x, acc[0]);
+          acc[1] = wd_mma(wv.y, xv.y, acc[1]);
+          acc[2] = wd_mma(wv.z, xv.z, acc[2]);
+          acc[3] = wd_mma(wv.w, xv.w, acc[3]);
+        }
+      }
+      wd_v4 z;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) z[i] = (acc[0][i] + acc[1][i]) + (acc[2][i] + acc[3][i]);
+      wd_gn_fwd(z, wd_ld4(W + n.Lg0 + 16 * w + 4 * q), wd_ld4(W + n.Lb0 + 16 * w + 4 * q), xh0, r0, Fw);
+      wd_st4(Fs + x * WD_FS + 16 * w + 4 * q, Fw);
+    }
+    __syncthreads();   // #2: Fs
+    // ---- heads: Z_h^T block w = W1_h block w F^T, GroupNorm + SiLU -> G_h
+    wd_v4 F[4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) F[bb] = wd_ld4(Fs + x * WD_FS + 16 * bb + 4 * q);
+    wd_v4 xhh[WD_MAXH], Gh[WD_MAXH];
+    float rh[WD_MAXH];
+#pragma unroll
+    for (int h = 0; h < WD_MAXH; ++h) {
+      xhh[h] = z4;
+      Gh[h] = z4;
+      rh[h] = 0.f;
+      if (h < nh) {
+        const WdHead hi = wd_head(n, h);
+        wd_v4 z = z4;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const wd_v4 wa = wd_ld4(W + hi.Lw1 + (16 * w + x) * WD_HS + 16 * bb + 4 * q);
+          z = wd_mma(wa[0], F[bb][0], z);
+          z = wd_mma(wa[1], F[bb][1], z);
+          z = wd_mma(wa[2], F[bb][2], z);
+          z = wd_mma(wa[3], F[bb][3], z);
+        }
+        wd_gn_fwd(z, wd_ld4(W + hi.Lg1 + 16 * w + 4 * q), wd_ld4(W + hi.Lb1 + 16 * w + 4 * q),
+                  xhh[h], rh[h], Gh[h]);
+        wd_st4(Gs + x * WD_GS + 64 * h + 16 * w + 4 * q, Gh[h]);
+      }
+    }
+    __syncthreads();   // #3: Gs
+    // ---- output layer: wave m < 3 forms outputs 16m .. 16m+15 of every row (K = each
+    //      overlapping head's 64 channels): lane (x = row, q) reg i = O[row x][16m + 4q + i]
+    if (w < 3 && 16 * w < n.nout) {
+      const int jA = 16 * w + x;   // the A row this lane supplies
+      wd_v4 o = z4;
+#pragma unroll
+      for (int h = 0; h < WD_MAXH; ++h) {
+        if (h < nh) {
+          const WdHead hi = wd_head(n, h);
+          if (hi.oc < 16 * w + 16 && hi.oc + hi.no > 16 * w) {
+            const bool mine = jA >= hi.oc && jA < hi.oc + hi.no;
+            const float* wr = W + hi.Lw2 + (mine ? jA - hi.oc : 0) * WD_HS;
+            const float* gr = Gs + x * WD_GS + 64 * h;
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+              o = wd_mma(mine ? wr[4 * s + q] : 0.f, gr[4 * s + q], o);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int jo = 16 * w + 4 * q + i;
+        float bias = 0.f;
+#pragma unroll
+        for (int h = 0; h < WD_MAXH; ++h) {
+          if (h < nh) {
+            const WdHead hi = wd_head(n, h);
+            if (jo >= hi.oc && jo < hi.oc + hi.no) bias = W[hi.Lb2 + jo - hi.oc];
+          }
+        }
+        o[i] += bias;
+      }
+      wd_st4(Os + x * WD_OS + 16 * w + 4 * q, o);
+    }
+    __syncthreads();   // #4: Os
+    // ---- per-row loss and dO (wave 0, lanes q == 0: row x)
+    if (w == 0 && q == 0) {
+      float* dOr = dOs + x * WD_OS;
+      if (x < rc) {
+        float lp[3];
+        wd_row_loss(n, Os + x * WD_OS, Rin + x * WD_RS, invB, a.clip, a.vf_coef, dOr, lp);
+        lpacc[0] += (double)lp[0];
+        lpacc[1] += (double)lp[1];
+        lpacc[2] += (double)lp[2];
+      } else {
+        for (int jj = 0; jj < WD_MAXO; ++jj) dOr[jj] = 0.f;
+      }
+    }
+    __syncthreads();   // #5: dOs
+    // ---- heads backward (block w): dW2, dG -> GroupNorm bwd -> dZ (to Zs), dgamma / dbeta
+#pragma unroll
+    for (int h = 0; h < WD_MAXH; ++h) {
+      if (h < nh) {
+        const WdHead hi = wd_head(n, h);
+        const int oc = hi.oc, no = hi.no;
+        // dW2_h[16mt + 4q + i][16w + x] += sum_rows dO[row][oc + 16mt + x'] G_h[row][16w + x]
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          if (16 * mt < no) {
+            const int jj = 16 * mt + x;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const int r = 4 * s + q;
+              gW2[h][mt] = wd_mma(jj < no ? dOs[r * WD_OS + oc + jj] : 0.f,
+                                  Gs[r * WD_GS + 64 * h + 16 * w + x], gW2[h][mt]);
+            }
+          }
+        }
+        // dG_h^T block w = W2_h^T dO_h^T (K = the head's outputs)
+        wd_v4 dg = z4;
+#pragma unroll
+        for (int s = 0; s < WD_MAXHO / 4; ++s) {
+          if (4 * s < no) {
+            const int jj = 4 * s + q;
+            const float av = jj < no ? W[hi.Lw2 + jj * WD_HS + 16 * w + x] : 0.f;
+            const float bv = jj < no ? dOs[x * WD_OS + oc + jj] : 0.f;
+            dg = wd_mma(av, bv, dg);
+          }
+        }
+        wd_v4 dy;
+        const wd_v4 dz = wd_gn_bwd(dg, xhh[h], wd_ld4(W + hi.Lg1 + 16 * w + 4 * q),
+                                   wd_ld4(W + hi.Lb1 + 16 * w + 4 * q), rh[h], dy);
+        wd_st4(Zs + h * WD_RT * WD_FS + x * WD_FS + 16 * w + 4 * q, dz);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          gg1[h][i] += wd_rsum16(dy[i] * xhh[h][i]);
+          gb1[h][i] += wd_rsum16(dy[i]);
+        }
+      }
+    }
+    if (w == 3 && l < n.nout) {   // output biases: f64 row sums (softmax dO cancel across rows)
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < WD_RT; ++r) s += (double)dOs[r * WD_OS + l];
+      gbias += s;
+    }
+    __syncthreads();   // #6: Zs
+    // ---- dW1_h[16w + 4q + i][16bb + x] += sum_rows dZ_h[row][16w + ..] F[row][16bb + x]
+#pragma unroll
+    for (int h = 0; h < WD_MAXH; ++h) {
+      if (h < nh) {
+        const float* Zh = Zs + h * WD_RT * WD_FS;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int r = 4 * s + q;
+          const float av = Zh[r * WD_FS + 16 * w + x];
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb) gW1[h][bb] = wd_mma(av, Fs[r * WD_FS + 16 * bb + x], gW1[h][bb]);
+        }
+      }
+    }
+    // ---- dF^T block w = sum_h W1_h^T dZ_h^T (K permuted: step s, lane q <-> channel
+    //      16 (s & 3) + 4 q + (s >> 2)), trunk GroupNorm backward -> dH0
+    wd_v4 dF;
+    {
+      wd_v4 d0 = z4, d1 = z4;
+#pragma unroll
+      for (int h = 0; h < WD_MAXH; ++h) {
+        if (h < nh) {
+          const WdHead hi = wd_head(n, h);
+          const float* Zh = Zs + h * WD_RT * WD_FS + x * WD_FS;
+          const float* Wh = W + hi.Lw1 + 16 * w + x;
+#pragma unroll
+          for (int s = 0; s < 16; ++s) {
+            const int o = 16 * (s & 3) + 4 * q + (s >> 2);
+            if (s & 1) d1 = wd_mma(Wh[o * WD_HS], Zh[o], d1);
+            else d0 = wd_mma(Wh[o * WD_HS], Zh[o], d0);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dF[i] = d0[i] + d1[i];
+    }
+    wd_v4 dy0;
+    const wd_v4 dH0 = wd_gn_bwd(dF, xh0, wd_ld4(W + n.Lg0 + 16 * w + 4 * q),
+                                wd_ld4(W + n.Lb0 + 16 * w + 4 * q), r0, dy0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      gg0[i] += wd_rsum16(dy0[i] * xh0[i]);
+      gb0[i] += wd_rsum16(dy0[i]);
+    }
+    // ---- dW0[16w + 4q + i][16e + x] += sum_rows dH0[row][ch] X[row][16e + x]
+    wd_st4(Tw + x * 16 + 4 * q, dH0);
+    wd_wave_sync();
+    {
+      float ta[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) ta[s] = Tw[(4 * s + q) * 16 + x];
+#pragma unroll
+      for (int e = 0; e < KE; ++e) {
+        if (16 * e < D) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) gW0[e] = wd_mma(ta[s], Xs[(4 * s + q) * XS + 16 * e + x], gW0[e]);
+        }
+      }
+    }
+    wd_wave_sync();   // Tw is rewritten by the next tile only after its barriers; keep order
+  }
+
+  // ---- this workgroup's partial gradient -> part[g] (flat order; every entry written once)
+  float* out = a.part + (int64_t)blockIdx.x * (n.Pq + 4);
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    const int d = 16 * e + x;
+    if (d < D) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[n.w0 + (16 * w + 4 * q + i) * D + d] = gW0[e][i];
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < WD_MAXH; ++h) {
+    if (h < nh) {
+      int fw1 = n.w1[0], fg1 = n.g1[0], fb1 = n.b1[0], fw2 = n.w2[0], no = n.out[0];
+      if (h == 1) { fw1 = n.w1[1]; fg1 = n.g1[1]; fb1 = n.b1[1]; fw2 = n.w2[1]; no = n.out[1]; }
+      if (h == 2) { fw1 = n.w1[2]; fg1 = n.g1[2]; fb1 = n.b1[2]; fw2 = n.w2[2]; no = n.out[2]; }
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) out[fw1 + (16 * w + 4 * q + i) * WD_H + 16 * bb + x] = gW1[h][bb][i];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int jj = 16 * mt + 4 * q + i;
+          if (jj < no) out[fw2 + jj * WD_H + 16 * w + x] = gW2[h][mt][i];
+        }
+      if (x == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          out[fg1 + 16 * w + 4 * q + i] = gg1[h][i];
+          out[fb1 + 16 * w + 4 * q + i] = gb1[h][i];
+        }
+      }
+    }
+  }
+  if (x == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      out[n.g0 + 16 * w + 4 * q + i] = gg0[i];
+      out[n.b0 + 16 * w + 4 * q + i] = gb0[i];
+    }
+  }
+  if (w == 3 && l < n.nout) {
+    int fb = n.b2[0] + l;
+#pragma unroll
+    for (int h = 1; h < WD_MAXH; ++h)
+      if (h < nh && l >= n.ocol[h]) fb = (h == 1 ? n.b2[1] : n.b2[2]) + (l - n.ocol[h]);
+    out[fb] = (float)gbias;
+  }
+  if (w == 0) {   // loss terms: lanes 0..15 (q == 0) hold rows' sums; lanes q > 0 hold 0
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float s = wd_rsum16((float)lpacc[k]);
+      if (l == 0) out[n.Pq + k] = s;
+    }
+    if (l == 0) out[n.Pq + 3] = 0.f;
+  }
+}
+
+// grad[k] = sum_g part[g][k] in workgroup order (f64), k < P; loss = (L0 + vf L1 - ent L2) / B.
+// Block = 64 quads x 4 workgroup slots; slot s sums workgroups s, s + 4, ... and the 4 slot
+// sums are added in slot order.
+constexpr int WR_QUADS = 64;
+__global__ __launch_bounds__(256) void ppo_wide_reduce_kernel(const float* __restrict__ part, int G,
+                                                              int P, int Pq, float* __restrict__ grad,
+                                                              float* __restrict__ loss_out,
+                                                              const int64_t* cursor,
+                                                              const float* scales, int64_t N,
+                                                              int64_t mb, float vf_coef,
+                                                              float ent_coef) {
+  __shared__ double4 acc_s[4][WR_QUADS];
+  const int t = threadIdx.x, slot = t >> 6, qi = t & 63;
+  const int quad = blockIdx.x * WR_QUADS + qi;
+  const int stride = Pq + 4;
+  const int nq = stride / 4;
+  double4 acc = {0.0, 0.0, 0.0, 0.0};
+  if (quad < nq) {
+    const float4* src = reinterpret_cast<const float4*>(part) + quad;
+    int g = slot;
+    for (; g + 12 < G; g += 16) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = src[(int64_t)(g + 4 * u) * nq];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x += v[u].x;
+        acc.y += v[u].y;
+        acc.z += v[u].z;
+        acc.w += v[u].w;
+      }
+    }
+    for (; g < G; g += 4) {
+      const float4 v = src[(int64_t)g * nq];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+  }
+  acc_s[slot][qi] = acc;
+  __syncthreads();
+  if (slot == 0 && quad < nq) {
+    double4 s = acc_s[0][qi];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const double4 o = acc_s[k][qi];
+      s.x += o.x;
+      s.y += o.y;
+      s.z += o.z;
+      s.w += o.w;
+    }
+    const int k0 = 4 * quad;
+    if (k0 < P) {
+      grad[k0] = (float)s.x;
+      if (k0 + 1 < P) grad[k0 + 1] = (float)s.y;
+      if (k0 + 2 < P) grad[k0 + 2] = (float)s.z;
+      if (k0 + 3 < P) grad[k0 + 3] = (float)s.w;
+    } else if (k0 == Pq && loss_out) {
+      const int64_t j = *cursor;
+      const int64_t lo = j * mb;
+      const int64_t rows = lo < N ? (N - lo < mb ? N - lo : mb) : 0;
+      const float inv = rows > 0 ? (scales ? scales[j] : 1.0f) / (float)rows : 0.f;
+      loss_out[0] = (float)s.x * inv + vf_coef * ((float)s.y * inv) - ent_coef * ((float)s.z * inv);
+    }
+  }
+}
+
+// KSM instantiated for D <= 128 and D <= 352
+int wd_ksm(int D) { return D <= 128 ? 32 : (D <= 352 ? 88 : 0); }
+
+int wd_grid(int64_t mb) {
+  const int64_t tiles = (mb + WD_RT - 1) / WD_RT;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, WD_GRID_MAX));
+}
+
+}  // namespace
+}  // namespace prl
+
+using namespace prl;
+
+extern "C" int prl_ppo_wide_info(int32_t D, int32_t A, int32_t discrete, int64_t mini_batch,
+                                 int64_t* n_params, int64_t* part_floats, int32_t* grid) {
+  WdNet n;
+  if (n_params) *n_params = 0;
+  if (part_floats) *part_floats = 0;
+  if (grid) *grid = 0;
+  PRL_REQUIRE(mini_batch > 0, "prl_ppo_wide_info: mini_batch must be > 0");
+  if (!wd_layout(D, A, discrete, n) || wd_ksm(D) == 0) return PRL_ERR_ARG;
+  if (wd_lds_bytes(n, wd_ksm(D)) > 160 * 1024) return PRL_ERR_ARG;
+  const int G = wd_grid(mini_batch);
+  if (n_params) *n_params = n.P;
+  if (part_floats) *part_floats = (int64_t)G * (n.Pq + 4);
+  if (grid) *grid = G;
+  return PRL_OK;
+}
+
+extern "C" int prl_ppo_wide_grad(const float* params, int32_t D, int32_t A, int32_t discrete,
+                                 const float* S, const float* actions, const float* old_logp,
+                                 const float* adv, const float* ret, int64_t N,
+                                 int64_t mini_batch, const int64_t* cursor, const float* scales,
+                                 float clip, float vf_coef, float ent_coef, float* grad,
+                                 float* loss_out, float* part, int64_t part_floats, void* stream) {
+  WdNet n;
+  PRL_REQUIRE(mini_batch > 0 && N >= 0, "prl_ppo_wide_grad: bad sizes");
+  PRL_REQUIRE(wd_layout(D, A, discrete, n) && wd_ksm(D) > 0,
+              "prl_ppo_wide_grad: shape D=%d A=%d outside the wide kernel", D, A);
+  PRL_REQUIRE(params && S && actions && old_logp && adv && ret && cursor && grad && part,
+              "prl_ppo_wide_grad: null pointer");
+  const int G = wd_grid(mini_batch);
+  PRL_REQUIRE(part_floats >= (int64_t)G * (n.Pq + 4), "prl_ppo_wide_grad: part buffer too small");
+  const int KSM = wd_ksm(D);
+  const size_t lds = wd_lds_bytes(n, KSM);
+  PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_wide_grad: LDS %zu bytes", lds);
+  WdArgs a{};
+  a.net = n;
+  a.params = params;
+  a.S = S;
+  a.act = actions;
+  a.old_logp = old_logp;
+  a.adv = adv;
+  a.ret = ret;
+  a.cursor = cursor;
+  a.scales = scales;
+  a.N = N;
+  a.mb = mini_batch;
+  a.clip = clip;
+  a.vf_coef = vf_coef;
+  a.part = part;
+  a.G = G;
+  hipStream_t st = as_stream(stream);
+  // the kernels' dynamic-LDS limit is raised once per process (not a stream operation, but kept
+  // out of the per-step path that graphs capture)
+  static bool lds_set[2] = {false, false};
+  if (KSM == 32) {
+    if (!lds_set[0]) {
+      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<32>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      lds_set[0] = true;
+    }
+    hipLaunchKernelGGL(ppo_wide_grad_kernel<32>, dim3(G), dim3(WD_THREADS), lds, st, a);
+  } else {
+    if (!lds_set[1]) {
+      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<88>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      lds_set[1] = true;
+    }
+    hipLaunchKernelGGL(ppo_wide_grad_kernel<88>, dim3(G), dim3(WD_THREADS), lds, st, a);
+  }
+  PRL_LAUNCH_CHECK("ppo_wide_grad");
+  const int nq = (n.Pq + 4) / 4;
+  hipLaunchKernelGGL(ppo_wide_reduce_kernel, dim3((unsigned)cdiv(nq, WR_QUADS)), dim3(256), 0, st,
+                     part, G, n.P, n.Pq, grad, loss_out, cursor, scales, N, mini_batch, vf_coef,
+                     ent_coef);
+  PRL_LAUNCH_CHECK("ppo_wide_reduce");
+  return PRL_OK;
+}

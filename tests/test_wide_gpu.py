@@ -1,0 +1,169 @@
+"""The wide-net optimizer step (csrc/prl_ppo_wide.hip, C-ABI prl_ppo_wide_grad) for shapes outside
+the persistent engine — C5's D = 348 / A = 17 continuous net — against
+float64 autograd of the reference loss (PPO/PPO.py:216-249: -min(surr1, surr2) + 0.5 SmoothL1 -
+0.01 H, mean, backward) on the same parameters and rows.  Gradients differ only by float32
+rounding / summation order: each tensor is checked at 1e-4 of its largest entry (the persistent
+engine's bar, tests/test_engine_gpu.py); the loss at 1e-5 relative."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+pytestmark = pytest.mark.gpu
+
+
+def _policy(cont, D, A, seed=0):
+    from PPO.ActorCritic import ActorCritic
+    torch.manual_seed(seed)
+    return ActorCritic(cont, D, A, device=torch.device("cuda"))
+
+
+def _sample(pol, S, seed=9):
+    """Actions sampled from the policy's own Gaussian.  Far off-distribution actions (narrow
+    std, |a - mu| ~ 1) give |log p| ~ 500 for A = 17, whose float32 rounding alone moves every
+    ratio by ~1e-4 (the same conditioning limit as the persistent engine's test)."""
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        return pol.get_dist(S).sample().float().contiguous()
+
+
+def _rows(pol, cont, N, D, A, spread, seed=3, clip=0.2):
+    """Random states / actions, advantages, returns; old log-probs = float64 log-probs + noise of
+    `spread` (0: on-policy), nudged 1e-2 away from the clip kinks (the gradient jumps there)."""
+    rng = np.random.default_rng(seed)
+    S = torch.from_numpy((rng.normal(size=(N, D)) * 0.7).astype(np.float32)).cuda()
+    if cont:   # actions drawn from the policy, as a rollout stores them: |log p| stays O(A)
+        act = _sample(pol, S)
+    else:
+        act = torch.from_numpy(rng.integers(0, A, size=(N, 1)).astype(np.float32)).cuda()
+    adv = torch.from_numpy(rng.normal(size=N).astype(np.float32)).cuda()
+    ret = torch.from_numpy(rng.normal(0.3, 1.5, size=N).astype(np.float32)).cuda()
+    p64 = copy.deepcopy(pol).cpu().double()
+    with torch.no_grad():
+        l64, _, _ = p64.get_evaluate(S.cpu().double(), act.cpu().double() if cont else
+                                     act.cpu().double().reshape(-1))
+    old = l64 + torch.from_numpy(rng.normal(size=N) * spread)
+    r = torch.exp(l64 - old)
+    near = ((r - (1 - clip)).abs() < 1e-3) | ((r - (1 + clip)).abs() < 1e-3)
+    old = torch.where(near, old + 1e-2, old)
+    return S, act, old.float().cuda(), adv, ret
+
+
+def _grad64(pol, cont, S, act, old, adv, ret, clip=0.2, vf=0.5, ent=0.01):
+    p64 = copy.deepcopy(pol).cpu().double()
+    a = act.cpu().double() if cont else act.cpu().double().reshape(-1)
+    logp, V, H = p64.get_evaluate(S.cpu().double(), a)
+    ratio = torch.exp(torch.clamp(logp - old.cpu().double(), -20, 20))
+    A_ = adv.cpu().double()
+    s1, s2 = ratio * A_, torch.clamp(ratio, 1 - clip, 1 + clip) * A_
+    loss = (-torch.min(s1, s2) + vf * nn.SmoothL1Loss()(V, ret.cpu().double()) - ent * H).mean()
+    loss.backward()
+    return [p.grad for p in p64.parameters()], float(loss.detach())
+
+
+def _wide(pol, cont, D, A, S, act, old, adv, ret, mb, j):
+    import prl_native
+    info = prl_native.ppo_wide_info(D, A, not cont, mb)
+    assert info is not None
+    n_params, part_floats, grid = info
+    params = list(pol.parameters())
+    assert n_params == sum(p.numel() for p in params)
+    flat = torch.cat([p.detach().reshape(-1) for p in params])
+    grad = torch.full((n_params,), float("nan"), device="cuda")
+    loss = torch.zeros(1, device="cuda")
+    part = torch.full((part_floats,), float("nan"), device="cuda")
+    cur = torch.tensor([j], dtype=torch.int64, device="cuda")
+    prl_native.ppo_wide_grad(flat, D, A, not cont, S, act, old, adv, ret, mb, cur, None, 0.2, 0.5,
+                             0.01, grad, loss, part)
+    torch.cuda.synchronize()
+    out, off = [], 0
+    for p in params:
+        out.append(grad[off:off + p.numel()].view_as(p).double().cpu())
+        off += p.numel()
+    return out, float(loss)
+
+
+CASES = [
+    # cont, D, A, N, mb, spread     (C5's net; a ragged minibatch; discrete; D % 4 != 0)
+    (True, 348, 17, 1000, 512, 0.3),
+    (True, 348, 17, 300, 4096, 0.0),
+    (False, 100, 5, 700, 256, 0.5),
+    (True, 201, 3, 530, 512, 1.0),
+    (False, 66, 30, 257, 128, 0.3),
+]
+
+
+@pytest.mark.parametrize("cont,D,A,N,mb,spread", CASES)
+def test_wide_gradient_matches_float64_autograd(cont, D, A, N, mb, spread):
+    pol = _policy(cont, D, A)
+    S, act, old, adv, ret = _rows(pol, cont, N, D, A, spread)
+    nb = -(-N // mb)
+    for j in range(nb):
+        lo, hi = j * mb, min(N, (j + 1) * mb)
+        g64, l64 = _grad64(pol, cont, S[lo:hi], act[lo:hi], old[lo:hi], adv[lo:hi], ret[lo:hi])
+        gw, lw = _wide(pol, cont, D, A, S, act, old, adv, ret, mb, j)
+        errs = {}
+        for (name, _), a, b in zip(pol.named_parameters(), gw, g64):
+            assert torch.isfinite(a).all(), name
+            errs[name] = float((a - b).abs().max()) / (float(b.abs().max()) + 1e-30)
+        worst = max(errs.values())
+        top = sorted(errs.items(), key=lambda kv: -kv[1])[:4]
+        print(j, {k: f"{v:.1e}" for k, v in top})
+        assert worst <= 1e-4, (j, [(k, f"{v:.1e}") for k, v in top])
+        assert abs(lw - l64) <= 1e-5 * max(1.0, abs(l64)), (lw, l64)
+
+
+def test_wide_deterministic_and_info_bounds():
+    import prl_native
+    assert prl_native.ppo_wide_info(348, 17, False, 65536) is not None
+    assert prl_native.ppo_wide_info(353, 4, False, 512) is None      # D > 352
+    assert prl_native.ppo_wide_info(64, 24, False, 512) is None      # 49 outputs > 48
+    pol = _policy(True, 348, 17)
+    S, act, old, adv, ret = _rows(pol, True, 4096 + 77, 348, 17, 0.3)
+    g1, l1 = _wide(pol, True, 348, 17, S, act, old, adv, ret, 4096, 0)
+    g2, l2 = _wide(pol, True, 348, 17, S, act, old, adv, ret, 4096, 0)
+    assert l1 == l2
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
+
+
+def test_wide_learn_matches_autograd_step_path():
+    """learn() on a C5-shaped net through the wide kernel (graphed + the ragged minibatch) against
+    the PyTorch autograd step path (PRL_WIDE=0) in function space: log-probs / values on probe
+    states after 2 epochs agree to 1e-3 (the persistent engine's function-space bar, in its
+    smooth regime: clip 1e3, on-policy actions)."""
+    import os
+    from PPO import PPO
+    D, A = 348, 17
+    rng = np.random.default_rng(11)
+    N, mb = 3 * 1024 + 200, 1024
+    S = torch.from_numpy((rng.normal(size=(N, D)) * 0.5).astype(np.float32)).cuda()
+    R = torch.from_numpy(rng.normal(1, 0.5, N).astype(np.float32)).cuda()
+    Dn = torch.from_numpy((rng.random(N) < 0.02).astype(np.float32)).cuda()
+    Dn[-1] = 1
+    Aa = _sample(_policy(True, D, A), S)   # PPO(...) below builds the same net from seed 0
+    out = {}
+    for wide in ("1", "0"):
+        os.environ["PRL_WIDE"] = wide
+        try:
+            torch.manual_seed(0)
+            p = PPO(True, D, A, action_scaling=1.0, lr=3e-4, k_epochs=2, batch_size=64,
+                    mini_batch_size=mb, policy_clip=1e3)   # smooth surrogate (no clip kinks)
+            p.show_progress = False
+            p.graph_min_steps = 1
+            p.memory.push_device(S, Aa, R, Dn)
+            p.learn()
+            assert p.last_update_path == "graph"
+            pol = copy.deepcopy(p.policy).cpu().double()
+            with torch.no_grad():
+                lp, V, _ = pol.get_evaluate(S[:512].cpu().double(), Aa[:512].cpu().double())
+            out[wide] = (lp, V, float(p.last_loss))
+        finally:
+            os.environ.pop("PRL_WIDE", None)
+    (l1, v1, L1), (l0, v0, L0) = out["1"], out["0"]
+    el = float((l1 - l0).abs().max()) / (float(l0.abs().max()) + 1.0)
+    ev = float((v1 - v0).abs().max()) / (float(v0.abs().max()) + 1.0)
+    assert el <= 1e-3 and ev <= 1e-3, (el, ev)
+    assert abs(L1 - L0) <= 1e-3 * max(1.0, abs(L0)), (L1, L0)
