@@ -287,6 +287,14 @@ int prl_ppo_wide_grad(const float* params, int32_t D, int32_t A, int32_t discret
                       const float* ret, int64_t N, int64_t mini_batch, const int64_t* cursor,
                       const float* scales, float clip, float vf_coef, float ent_coef, float* grad,
                       float* loss_out, float* part, int64_t part_floats, void* stream);
+/* prl_ppo_wide_grad with workgroup 0's s_memrealtime ticks (100 MHz) per tile stage added into
+ * prof[8] (stage, trunk, heads, outputs, loss, heads bwd, dW1 + dF, dW0); diagnostics. */
+int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A, int32_t discrete,
+                           const float* S, const float* actions, const float* old_logp,
+                           const float* adv, const float* ret, int64_t N, int64_t mini_batch,
+                           const int64_t* cursor, const float* scales, float clip, float vf_coef,
+                           float ent_coef, float* grad, float* loss_out, float* part,
+                           int64_t part_floats, unsigned long long* prof, void* stream);
 /* Column sums out[c] = sum_r x[r][c] of a row-major f32 matrix (cols >= 1): the bias
  * gradient of a Linear over a large batch (nn.Linear backward, reached from PPO.py:249 /
  * RND.py:112).  Two deterministic passes; `partial` holds prl_colsum_partial_floats(rows, cols)

@@ -109,7 +109,8 @@ __host__ __device__ inline int wd_scratch_floats(int KSM) {
          + WD_RT * WD_GS             // Gs  [16][196]     head outputs (3 x 64 channels)
          + 2 * WD_RT * WD_OS         // Os, dOs [16][52]  outputs, d loss / d outputs
          + WD_MAXH * WD_RT * WD_FS   // Zs  [3][16][80]   head dZ
-         + 4 * WD_RT * 16;           // Tw  [4][16][16]   per-wave dH0 transpose slot
+         + 4 * WD_RT * 16            // Tw  [4][16][16]   per-wave dH0 transpose slot
+         + 8 * WD_H;                 // Gn  [8][64]       GroupNorm gamma / beta gradients
 }
 inline size_t wd_lds_bytes(const WdNet& n, int KSM) {
   return sizeof(float) * (size_t)(n.Lp + wd_scratch_floats(KSM));
@@ -129,6 +130,7 @@ struct WdArgs {
   float clip, vf_coef;
   float* part;             // [G][Pq + 4]
   int G;
+  unsigned long long* prof;   // [8] workgroup 0's s_memrealtime ticks per tile stage (or null)
 };
 
 typedef float wd_v4 __attribute__((ext_vector_type(4)));
@@ -215,51 +217,84 @@ __device__ inline WdHead wd_head(const WdNet& n, int h) {
   return r;
 }
 
-// Row loss (the persistent engine's upd_row_loss arithmetic, for up to 32 actions, reading the
-// outputs from LDS): writes dO[0 .. 48) (zeros past nout) and returns {-min(s1,s2), SmoothL1, H}.
-__device__ inline void wd_row_loss(const WdNet& n, const float* O, const float* rin, float invB,
-                                   float clip, float vf_coef, float* dO, float (&lp)[3]) {
+// max over the 16 lanes of a DPP row
+__device__ inline float wd_rmax16(float v) {
+  v = fmaxf(v, wd_dpp<0xB1>(v));
+  v = fmaxf(v, wd_dpp<0x4E>(v));
+  v = fmaxf(v, wd_dpp<0x141>(v));
+  v = fmaxf(v, wd_dpp<0x140>(v));
+  return v;
+}
+
+// The tile's row losses on all 256 threads: row r = t >> 4 is one DPP row of 16 lanes, lane c
+// takes the actions / classes k = c and c + 16 (A <= 32); per-row sums are DPP row sums, so every
+// lane of a row holds the same bits.  Same arithmetic as upd_row_loss (prl_ppo_update.hip) up to
+// the order of the per-action sums.  Writes dO[r][0 .. 48) and returns {-min(s1, s2), SmoothL1,
+// H} of row r (every lane of the row).
+__device__ inline void wd_tile_loss(const WdNet& n, const float* Os, const float* Rin, float* dOs,
+                                    float invB, float clip, float vf_coef, float (&lp)[3]) {
+  const int t = threadIdx.x, r = t >> 4, c = t & 15;
   const int A = n.A;
   const bool discrete = n.discrete != 0;
   const int vcol = discrete ? A : 2 * A;
-  float logp = 0.f, H = 0.f;
-  // discrete: softmax then torch's Categorical(probs) renormalisation + clamped log
-  float mx = 0.f, rs = 1.f, rS2 = 1.f, qa = 1.f;
+  const float* O = Os + r * WD_OS;
+  const float* rin = Rin + r * WD_RS;
+  float* dO = dOs + r * WD_OS;
+  dO[c] = 0.f;
+  dO[c + 16] = 0.f;
+  dO[c + 32] = 0.f;
+  float logp, H;
+  // per-lane state of its (up to) two actions
+  float e0 = 0.f, e1 = 0.f, mx = 0.f, rs = 1.f, rS2 = 1.f, qa = 1.f;
+  float sd0 = 1.f, sd1 = 1.f, dd0 = 0.f, dd1 = 0.f, ls0 = 0.f, ls1 = 0.f, lc0 = 0.f, lc1 = 0.f;
+  const int k0 = c, k1 = c + 16;
+  const bool ok0 = k0 < A, ok1 = k1 < A;
   int ai = 0;
   if (discrete) {
-    mx = O[0];
-    for (int k = 1; k < A; ++k) mx = fmaxf(mx, O[k]);
-    float s = 0.f;
-    for (int k = 0; k < A; ++k) s += wd_exp(O[k] - mx);
-    rs = wd_rcp(s);
-    float S2 = 0.f;
-    for (int k = 0; k < A; ++k) S2 += wd_exp(O[k] - mx) * rs;
-    rS2 = wd_rcp(S2);
+    const float o0 = ok0 ? O[k0] : -FLT_MAX, o1 = ok1 ? O[k1] : -FLT_MAX;
+    mx = wd_rmax16(fmaxf(o0, o1));
+    e0 = ok0 ? wd_exp(o0 - mx) : 0.f;
+    e1 = ok1 ? wd_exp(o1 - mx) : 0.f;
+    rs = wd_rcp(wd_rsum16(e0 + e1));
+    const float p0 = e0 * rs, p1 = e1 * rs;
+    rS2 = wd_rcp(wd_rsum16(p0 + p1));
+    const float q0 = p0 * rS2, q1 = p1 * rS2;
     ai = (int)rin[0];
     const bool bad = ai < 0 || ai >= A;
-    float la = 0.f;
-    for (int k = 0; k < A; ++k) {
-      const float qk = (wd_exp(O[k] - mx) * rs) * rS2;
-      const float c = qk < FLT_EPSILON ? FLT_EPSILON : (qk > 1.0f - FLT_EPSILON ? 1.0f - FLT_EPSILON : qk);
-      const float l = wd_log(c);
-      H += l * qk;
-      if (k == ai) { la = l; qa = qk; }
-    }
-    H = -H;
+    const float c0 = q0 < FLT_EPSILON ? FLT_EPSILON : (q0 > 1.0f - FLT_EPSILON ? 1.0f - FLT_EPSILON : q0);
+    const float c1 = q1 < FLT_EPSILON ? FLT_EPSILON : (q1 > 1.0f - FLT_EPSILON ? 1.0f - FLT_EPSILON : q1);
+    const float l0 = wd_log(c0), l1 = wd_log(c1);
+    H = -wd_rsum16((ok0 ? l0 * q0 : 0.f) + (ok1 ? l1 * q1 : 0.f));
+    const float la = wd_rsum16((k0 == ai ? l0 : 0.f) + (k1 == ai ? l1 : 0.f));
+    qa = bad ? 1.f : wd_rsum16((k0 == ai ? q0 : 0.f) + (k1 == ai ? q1 : 0.f));
     logp = bad ? __builtin_nanf("") : la;
-    // S2 is needed below through rS2 only
   } else {
     const float half_log_2pi = 0.91893853320467274f;
-    for (int k = 0; k < A; ++k) {
-      const float mu = O[k];
-      const float lsr = O[A + k];
+    float lpart = 0.f, hpart = 0.f;
+    if (ok0) {
+      const float lsr = O[A + k0];
+      lc0 = lsr;
       const float lsc = lsr < -2.0f ? -2.0f : (lsr > 2.0f ? 2.0f : lsr);
-      const float sd = wd_log(1.0f + wd_exp(lsc));
-      const float dd = rin[k] - mu;
-      const float lsd = wd_log(sd);
-      logp += -(dd * dd) * wd_rcp(2.0f * (sd * sd)) - lsd - half_log_2pi;
-      H += 0.5f + half_log_2pi + lsd;
+      ls0 = lsc;
+      sd0 = wd_log(1.0f + wd_exp(lsc));
+      dd0 = rin[k0] - O[k0];
+      const float lsd = wd_log(sd0);
+      lpart += -(dd0 * dd0) * wd_rcp(2.0f * (sd0 * sd0)) - lsd - half_log_2pi;
+      hpart += 0.5f + half_log_2pi + lsd;
     }
+    if (ok1) {
+      const float lsr = O[A + k1];
+      lc1 = lsr;
+      const float lsc = lsr < -2.0f ? -2.0f : (lsr > 2.0f ? 2.0f : lsr);
+      ls1 = lsc;
+      sd1 = wd_log(1.0f + wd_exp(lsc));
+      dd1 = rin[k1] - O[k1];
+      const float lsd = wd_log(sd1);
+      lpart += -(dd1 * dd1) * wd_rcp(2.0f * (sd1 * sd1)) - lsd - half_log_2pi;
+      hpart += 0.5f + half_log_2pi + lsd;
+    }
+    logp = wd_rsum16(lpart);
+    H = wd_rsum16(hpart);
   }
   const float V = O[vcol];
   const float diff = logp - rin[32];
@@ -285,37 +320,69 @@ __device__ inline void wd_row_loss(const WdNet& n, const float* O, const float* 
   lp[0] = -m;
   lp[1] = sl;
   lp[2] = H;
-  for (int j = 0; j < WD_MAXO; ++j) dO[j] = 0.f;
-  dO[vcol] = vf_coef * invB * gx;
+  if (c == 0) dO[vcol] = vf_coef * invB * gx;
   if (discrete) {
     const float mk = (qa >= FLT_EPSILON && qa <= 1.0f - FLT_EPSILON) ? 1.0f : 0.0f;
     const float gq = (logp != logp) ? logp : dlogp * mk;
     const float rqa = wd_rcp(qa);
-    // dp_k = gq (1[k = a] / qa - 1) / S2;  dO_k = p_k (dp_k - sum_k' p_k' dp_k')
-    float dot = 0.f;
-    for (int k = 0; k < A; ++k) {
-      const float pk = wd_exp(O[k] - mx) * rs;
-      dot += pk * (gq * (((k == ai) ? rqa : 0.0f) - 1.0f) * rS2);
-    }
-    for (int k = 0; k < A; ++k) {
-      const float pk = wd_exp(O[k] - mx) * rs;
-      const float dpk = gq * (((k == ai) ? rqa : 0.0f) - 1.0f) * rS2;
-      dO[k] = pk * (dpk - dot);
-    }
+    const float p0 = e0 * rs, p1 = e1 * rs;
+    const float dp0 = ok0 ? gq * (((k0 == ai) ? rqa : 0.0f) - 1.0f) * rS2 : 0.f;
+    const float dp1 = ok1 ? gq * (((k1 == ai) ? rqa : 0.0f) - 1.0f) * rS2 : 0.f;
+    const float dot = wd_rsum16(p0 * dp0 + p1 * dp1);
+    if (ok0) dO[k0] = p0 * (dp0 - dot);
+    if (ok1) dO[k1] = p1 * (dp1 - dot);
   } else {
-    for (int k = 0; k < A; ++k) {
-      const float mu = O[k];
-      const float lsr = O[A + k];
-      const float lsc = lsr < -2.0f ? -2.0f : (lsr > 2.0f ? 2.0f : lsr);
-      const float sd = wd_log(1.0f + wd_exp(lsc));
-      const float d = rin[k] - mu;
-      const float var = sd * sd;
-      const float rvar = wd_rcp(var), rsd = wd_rcp(sd);
-      dO[k] = dlogp * (d * rvar);
-      const float dsd = dlogp * ((d * d) * (rvar * rsd) - rsd);
-      const float pass = (lsr >= -2.0f && lsr <= 2.0f) ? 1.0f : 0.0f;
-      dO[A + k] = dsd * wd_sigmoid(lsc) * pass;
+    if (ok0) {
+      const float var = sd0 * sd0, rvar = wd_rcp(var), rsd = wd_rcp(sd0);
+      dO[k0] = dlogp * (dd0 * rvar);
+      const float dsd = dlogp * ((dd0 * dd0) * (rvar * rsd) - rsd);
+      const float pass = (lc0 >= -2.0f && lc0 <= 2.0f) ? 1.0f : 0.0f;
+      dO[A + k0] = dsd * wd_sigmoid(ls0) * pass;
     }
+    if (ok1) {
+      const float var = sd1 * sd1, rvar = wd_rcp(var), rsd = wd_rcp(sd1);
+      dO[k1] = dlogp * (dd1 * rvar);
+      const float dsd = dlogp * ((dd1 * dd1) * (rvar * rsd) - rsd);
+      const float pass = (lc1 >= -2.0f && lc1 <= 2.0f) ? 1.0f : 0.0f;
+      dO[A + k1] = dsd * wd_sigmoid(ls1) * pass;
+    }
+  }
+}
+
+// Next-tile prefetch (D % 4 == 0, 16-B aligned S; the X buffers then have row stride D): the X
+// tile — 16 consecutive rows of S, one contiguous block — is copied global -> LDS by 16-B
+// global_load_lds (no VGPR destination; a wave-instruction writes 1 KiB contiguously), issued
+// before the loss and drained at the barrier after it; the row records go through 3 registers.
+__device__ inline void wd_glds_x(const WdNet& n, const WdArgs& a, int64_t row0, int rc, float* Xs) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int tot = WD_RT * n.D, have = rc * n.D;
+  const float* src = a.S + row0 * n.D;
+  const int nchunk = (tot + 255) >> 8;   // 256-float chunks, one wave-instruction each
+  for (int c = w; c < nchunk; c += 4) {
+    const int f = (c << 8) + 4 * l;
+    const int fs = f < have ? f : 0;     // past the minibatch's rows / the tile: any valid row
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + fs),
+                                     reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                         reinterpret_cast<uintptr_t>(Xs + (c << 8))),
+                                     16, 0, 0);
+  }
+}
+__device__ inline void wd_rin_load(const WdNet& n, const WdArgs& a, int64_t row0, int rc, float (&pr)[3]) {
+  const int t = threadIdx.x;
+  const int Aw = n.discrete ? 1 : n.A;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int e = t + WD_THREADS * i;
+    const int r = e / WD_RS, k = e - r * WD_RS;
+    float v = 0.f;
+    if (e < WD_RT * WD_RS && r < rc) {
+      const int64_t row = row0 + r;
+      if (k < WD_MAXA) v = k < Aw ? a.act[row * Aw + k] : 0.f;
+      else if (k == 32) v = a.old_logp[row];
+      else if (k == 33) v = a.adv[row];
+      else if (k == 34) v = a.ret[row];
+    }
+    pr[i] = v;
   }
 }
 
@@ -361,10 +428,14 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
   const WdNet& n = a.net;
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   const int D = n.D, nh = n.nh;
-  const int XS = wd_xs(KSM);
+  // X buffers: row stride D (unpadded, global_load_lds prefetch) when D % 4 == 0 and S is 16-B
+  // aligned, else wd_xs(KSM) (zero pad columns, register staging)
+  const bool pfv = (D & 3) == 0 && (reinterpret_cast<uintptr_t>(a.S) & 15u) == 0;
+  const int XS = pfv ? D : wd_xs(KSM);
+  constexpr int XBUF = WD_RT * (4 * KSM + 4);   // floats per X buffer (>= 16 D + 64 spill-over)
   float* W = lds;
   float* p = lds + n.Lp;
-  float* Xs0 = p; p += 2 * WD_RT * XS;
+  float* Xs0 = p; p += 2 * XBUF;
   float* Rin0 = p; p += 2 * WD_RT * WD_RS;
   float* Fs = p; p += WD_RT * WD_FS;
   float* Gs = p; p += WD_RT * WD_GS;
@@ -372,6 +443,10 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
   float* dOs = p; p += WD_RT * WD_OS;
   float* Zs = p; p += WD_MAXH * WD_RT * WD_FS;
   float* Tw = p + w * WD_RT * 16;
+  p += 4 * WD_RT * 16;
+  // GroupNorm gradient accumulators: [2h] gamma_h, [2h + 1] beta_h (heads), [6] gamma_0, [7] beta_0;
+  // entry 16w + 4q + i is owned by lane (x = 0, q) of wave w
+  float* Gn = p;
 
   // ---- minibatch of this step
   const int64_t j = *a.cursor;
@@ -382,7 +457,8 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
 
   // ---- head parameters -> LDS (padding entries 0); both X buffers' pad columns -> 0
   for (int k = t; k < n.Lp; k += WD_THREADS) W[k] = 0.f;
-  for (int k = t; k < 2 * WD_RT * XS; k += WD_THREADS) Xs0[k] = 0.f;
+  for (int k = t; k < 2 * XBUF; k += WD_THREADS) Xs0[k] = 0.f;
+  for (int k = t; k < 8 * WD_H; k += WD_THREADS) Gn[k] = 0.f;
   __syncthreads();
   for (int k = t; k < WD_H; k += WD_THREADS) {
     W[n.Lg0 + k] = a.params[n.g0 + k];
@@ -416,7 +492,6 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
   wd_v4 gW0[KE];
   wd_v4 gW1[WD_MAXH][4];
   wd_v4 gW2[WD_MAXH][2];
-  wd_v4 gg1[WD_MAXH], gb1[WD_MAXH], gg0, gb0;
   const wd_v4 z4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int e = 0; e < KE; ++e) gW0[e] = z4;
@@ -426,22 +501,28 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
     for (int bb = 0; bb < 4; ++bb) gW1[h][bb] = z4;
     gW2[h][0] = z4;
     gW2[h][1] = z4;
-    gg1[h] = z4;
-    gb1[h] = z4;
   }
-  gg0 = z4;
-  gb0 = z4;
   double gbias = 0.0;                 // wave 3, lane l < nout: output bias l
-  double lpacc[3] = {0.0, 0.0, 0.0};  // wave 0, lanes x < 16, q == 0: loss terms of row x
+  double lpacc[3] = {0.0, 0.0, 0.0};  // threads t % 16 == 0: loss terms of row t >> 4
 
+  const bool timer = a.prof != nullptr && blockIdx.x == 0 && t == 0;
+  unsigned long long tm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tl = timer ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#define WD_MARK(i)                                                     \
+  if (timer) {                                                         \
+    const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();  \
+    tm[i] += now_ - tl;                                                \
+    tl = now_;                                                         \
+  }
   int it = 0;
   for (int tile = blockIdx.x; tile < ntile; tile += a.G, ++it) {
     const int64_t row0 = row_lo + (int64_t)tile * WD_RT;
     const int rc = (int)(rows - (int64_t)tile * WD_RT < WD_RT ? rows - (int64_t)tile * WD_RT : WD_RT);
-    float* Xs = Xs0 + (it & 1) * WD_RT * XS;
+    float* Xs = Xs0 + (it & 1) * XBUF;
     float* Rin = Rin0 + (it & 1) * WD_RT * WD_RS;
-    wd_stage(n, a, row0, rc, XS, Xs, Rin);
+    if (it == 0 || !pfv) wd_stage(n, a, row0, rc, XS, Xs, Rin);   // else prefetched last tile
     __syncthreads();   // #1: Xs, Rin (and, on the first tile, the parameter image)
+    WD_MARK(0)
 
     // ---- trunk: H0^T block w = W0 block w X^T, GroupNorm + SiLU
     wd_v4 xh0, Fw;
@@ -475,6 +556,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
       wd_st4(Fs + x * WD_FS + 16 * w + 4 * q, Fw);
     }
     __syncthreads();   // #2: Fs
+    WD_MARK(1)
     // ---- heads: Z_h^T block w = W1_h block w F^T, GroupNorm + SiLU -> G_h
     wd_v4 F[4];
 #pragma unroll
@@ -503,6 +585,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
       }
     }
     __syncthreads();   // #3: Gs
+    WD_MARK(2)
     // ---- output layer: wave m < 3 forms outputs 16m .. 16m+15 of every row (K = each
     //      overlapping head's 64 channels): lane (x = row, q) reg i = O[row x][16m + 4q + i]
     if (w < 3 && 16 * w < n.nout) {
@@ -538,20 +621,43 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
       wd_st4(Os + x * WD_OS + 16 * w + 4 * q, o);
     }
     __syncthreads();   // #4: Os
-    // ---- per-row loss and dO (wave 0, lanes q == 0: row x)
-    if (w == 0 && q == 0) {
-      float* dOr = dOs + x * WD_OS;
-      if (x < rc) {
-        float lp[3];
-        wd_row_loss(n, Os + x * WD_OS, Rin + x * WD_RS, invB, a.clip, a.vf_coef, dOr, lp);
+    WD_MARK(3)
+    // ---- next tile's inputs in flight under the loss (written to the other buffers after it)
+    const int tile_n = tile + a.G;
+    const bool has_next = pfv && tile_n < ntile;
+    float pr[3];
+    if (has_next) {
+      const int64_t rn = rows - (int64_t)tile_n * WD_RT;
+      const int rcn = (int)(rn < WD_RT ? rn : WD_RT);
+      const int64_t r0n = row_lo + (int64_t)tile_n * WD_RT;
+      wd_glds_x(n, a, r0n, rcn, Xs0 + ((it + 1) & 1) * XBUF);
+      wd_rin_load(n, a, r0n, rcn, pr);
+    }
+    // ---- per-row loss and dO: row t >> 4, 16 lanes per row
+    {
+      float lp[3];
+      wd_tile_loss(n, Os, Rin, dOs, invB, a.clip, a.vf_coef, lp);
+      if ((t & 15) == 0 && (t >> 4) < rc) {
         lpacc[0] += (double)lp[0];
         lpacc[1] += (double)lp[1];
         lpacc[2] += (double)lp[2];
-      } else {
-        for (int jj = 0; jj < WD_MAXO; ++jj) dOr[jj] = 0.f;
+      }
+      if ((t >> 4) >= rc) {   // rows past the minibatch: no gradient
+        float* dOr = dOs + (t >> 4) * WD_OS;
+        dOr[t & 15] = 0.f;
+        dOr[(t & 15) + 16] = 0.f;
+        dOr[(t & 15) + 32] = 0.f;
       }
     }
+    if (has_next) {
+      float* Rn = Rin0 + ((it + 1) & 1) * WD_RT * WD_RS;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (t + WD_THREADS * i < WD_RT * WD_RS) Rn[t + WD_THREADS * i] = pr[i];
+      __builtin_amdgcn_s_waitcnt(0);   // the global_load_lds copies, before the barrier
+    }
     __syncthreads();   // #5: dOs
+    WD_MARK(4)
     // ---- heads backward (block w): dW2, dG -> GroupNorm bwd -> dZ (to Zs), dgamma / dbeta
 #pragma unroll
     for (int h = 0; h < WD_MAXH; ++h) {
@@ -586,10 +692,18 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
         const wd_v4 dz = wd_gn_bwd(dg, xhh[h], wd_ld4(W + hi.Lg1 + 16 * w + 4 * q),
                                    wd_ld4(W + hi.Lb1 + 16 * w + 4 * q), rh[h], dy);
         wd_st4(Zs + h * WD_RT * WD_FS + x * WD_FS + 16 * w + 4 * q, dz);
+        {
+          wd_v4 sg, sb;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          gg1[h][i] += wd_rsum16(dy[i] * xhh[h][i]);
-          gb1[h][i] += wd_rsum16(dy[i]);
+          for (int i = 0; i < 4; ++i) {
+            sg[i] = wd_rsum16(dy[i] * xhh[h][i]);
+            sb[i] = wd_rsum16(dy[i]);
+          }
+          if (x == 0) {
+            float* pg = Gn + 2 * h * WD_H + 16 * w + 4 * q;
+            wd_st4(pg, wd_ld4(pg) + sg);
+            wd_st4(pg + WD_H, wd_ld4(pg + WD_H) + sb);
+          }
         }
       }
     }
@@ -600,6 +714,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
       gbias += s;
     }
     __syncthreads();   // #6: Zs
+    WD_MARK(5)
     // ---- dW1_h[16w + 4q + i][16bb + x] += sum_rows dZ_h[row][16w + ..] F[row][16bb + x]
 #pragma unroll
     for (int h = 0; h < WD_MAXH; ++h) {
@@ -639,12 +754,21 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
     wd_v4 dy0;
     const wd_v4 dH0 = wd_gn_bwd(dF, xh0, wd_ld4(W + n.Lg0 + 16 * w + 4 * q),
                                 wd_ld4(W + n.Lb0 + 16 * w + 4 * q), r0, dy0);
+    {
+      wd_v4 sg, sb;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      gg0[i] += wd_rsum16(dy0[i] * xh0[i]);
-      gb0[i] += wd_rsum16(dy0[i]);
+      for (int i = 0; i < 4; ++i) {
+        sg[i] = wd_rsum16(dy0[i] * xh0[i]);
+        sb[i] = wd_rsum16(dy0[i]);
+      }
+      if (x == 0) {
+        float* pg = Gn + 6 * WD_H + 16 * w + 4 * q;
+        wd_st4(pg, wd_ld4(pg) + sg);
+        wd_st4(pg + WD_H, wd_ld4(pg + WD_H) + sb);
+      }
     }
     // ---- dW0[16w + 4q + i][16e + x] += sum_rows dH0[row][ch] X[row][16e + x]
+    WD_MARK(6)
     wd_st4(Tw + x * 16 + 4 * q, dH0);
     wd_wave_sync();
     {
@@ -660,6 +784,12 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
       }
     }
     wd_wave_sync();   // Tw is rewritten by the next tile only after its barriers; keep order
+    WD_MARK(7)
+  }
+#undef WD_MARK
+  if (timer) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a.prof[i] += tm[i];
   }
 
   // ---- this workgroup's partial gradient -> part[g] (flat order; every entry written once)
@@ -692,8 +822,8 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
       if (x == 0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          out[fg1 + 16 * w + 4 * q + i] = gg1[h][i];
-          out[fb1 + 16 * w + 4 * q + i] = gb1[h][i];
+          out[fg1 + 16 * w + 4 * q + i] = Gn[2 * h * WD_H + 16 * w + 4 * q + i];
+          out[fb1 + 16 * w + 4 * q + i] = Gn[(2 * h + 1) * WD_H + 16 * w + 4 * q + i];
         }
       }
     }
@@ -701,8 +831,8 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
   if (x == 0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      out[n.g0 + 16 * w + 4 * q + i] = gg0[i];
-      out[n.b0 + 16 * w + 4 * q + i] = gb0[i];
+      out[n.g0 + 16 * w + 4 * q + i] = Gn[6 * WD_H + 16 * w + 4 * q + i];
+      out[n.b0 + 16 * w + 4 * q + i] = Gn[7 * WD_H + 16 * w + 4 * q + i];
     }
   }
   if (w == 3 && l < n.nout) {
@@ -712,13 +842,26 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
       if (h < nh && l >= n.ocol[h]) fb = (h == 1 ? n.b2[1] : n.b2[2]) + (l - n.ocol[h]);
     out[fb] = (float)gbias;
   }
-  if (w == 0) {   // loss terms: lanes 0..15 (q == 0) hold rows' sums; lanes q > 0 hold 0
+  // loss terms: threads t % 16 == 0 hold their rows' sums (other lanes 0); 16-lane DPP row sums,
+  // then the 4 rows of each wave and the 4 waves in a fixed order through LDS
+  {
+    __syncthreads();   // the tile scratch is free
+    float* red = Zs;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const float s = wd_rsum16((float)lpacc[k]);
-      if (l == 0) out[n.Pq + k] = s;
+      if ((t & 15) == 0) red[(t >> 4) * 4 + k] = s;
     }
-    if (l == 0) out[n.Pq + 3] = 0.f;
+    __syncthreads();
+    if (t == 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        float s = 0.f;
+        for (int r = 0; r < WD_RT; ++r) s += red[r * 4 + k];
+        out[n.Pq + k] = s;
+      }
+      out[n.Pq + 3] = 0.f;
+    }
   }
 }
 
@@ -819,12 +962,33 @@ extern "C" int prl_ppo_wide_info(int32_t D, int32_t A, int32_t discrete, int64_t
   return PRL_OK;
 }
 
+extern "C" int prl_ppo_wide_grad_prof(const float*, int32_t, int32_t, int32_t, const float*,
+                                      const float*, const float*, const float*, const float*,
+                                      int64_t, int64_t, const int64_t*, const float*, float, float,
+                                      float, float*, float*, float*, int64_t, unsigned long long*,
+                                      void*);
+
 extern "C" int prl_ppo_wide_grad(const float* params, int32_t D, int32_t A, int32_t discrete,
                                  const float* S, const float* actions, const float* old_logp,
                                  const float* adv, const float* ret, int64_t N,
                                  int64_t mini_batch, const int64_t* cursor, const float* scales,
                                  float clip, float vf_coef, float ent_coef, float* grad,
                                  float* loss_out, float* part, int64_t part_floats, void* stream) {
+  return prl_ppo_wide_grad_prof(params, D, A, discrete, S, actions, old_logp, adv, ret, N,
+                                mini_batch, cursor, scales, clip, vf_coef, ent_coef, grad,
+                                loss_out, part, part_floats, nullptr, stream);
+}
+
+// prl_ppo_wide_grad + workgroup 0's per-stage tick counters added into prof[8] (diagnostics:
+// tools/wide_bench.py)
+extern "C" int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A, int32_t discrete,
+                                      const float* S, const float* actions, const float* old_logp,
+                                      const float* adv, const float* ret, int64_t N,
+                                      int64_t mini_batch, const int64_t* cursor,
+                                      const float* scales, float clip, float vf_coef,
+                                      float ent_coef, float* grad, float* loss_out, float* part,
+                                      int64_t part_floats, unsigned long long* prof,
+                                      void* stream) {
   WdNet n;
   PRL_REQUIRE(mini_batch > 0 && N >= 0, "prl_ppo_wide_grad: bad sizes");
   PRL_REQUIRE(wd_layout(D, A, discrete, n) && wd_ksm(D) > 0,
@@ -852,6 +1016,7 @@ extern "C" int prl_ppo_wide_grad(const float* params, int32_t D, int32_t A, int3
   a.vf_coef = vf_coef;
   a.part = part;
   a.G = G;
+  a.prof = prof;
   hipStream_t st = as_stream(stream);
   // the kernels' dynamic-LDS limit is raised once per process (not a stream operation, but kept
   // out of the per-step path that graphs capture)

@@ -51,6 +51,8 @@ SIGNATURES = {
     "prl_ppo_wide_info": [_I32, _I32, _I32, _I64, _P, _P, _P],
     "prl_ppo_wide_grad": [_P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I64, _P, _P, _F32,
                           _F32, _F32, _P, _P, _P, _I64, _P],
+    "prl_ppo_wide_grad_prof": [_P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I64, _P, _P,
+                               _F32, _F32, _F32, _P, _P, _P, _I64, _P, _P],
     "prl_categorical_fwd": [_P, _P, _I64, _I32, _P, _P, _P],
     "prl_categorical_bwd": [_P, _P, _P, _I64, _I32, _P, _P],
     "prl_ppo_update_info": [_I32, _I32, _I32, _I64, _P, _P, _P],
@@ -435,19 +437,21 @@ def ppo_wide_info(D: int, A: int, discrete: bool, mini_batch: int):
 
 
 def ppo_wide_grad(params, D, A, discrete, S, actions, old_logp, adv, ret, mini_batch, cursor,
-                  scales, clip, vf_coef, ent_coef, grad, loss_out, part):
+                  scales, clip, vf_coef, ent_coef, grad, loss_out, part, prof=None):
     """Gradient (flat, torch parameters() order) and loss of ONE optimizer step's minibatch
     (rows cursor*mb .. of S, ...) for the wide nets, in two HIP launches (prl_ppo_wide_grad).
     Graph-capturable: the minibatch index is read from the device `cursor` (int64)."""
     N = int(S.shape[0])
-    _check(lib().prl_ppo_wide_grad(
+    fn = lib().prl_ppo_wide_grad if prof is None else lib().prl_ppo_wide_grad_prof
+    extra = () if prof is None else (_dev(prof, torch.int64, "prof"),)
+    _check(fn(
         _dev(params, torch.float32, "params"), int(D), int(A), int(bool(discrete)),
         _dev(S, torch.float32, "S"), _dev(actions, torch.float32, "actions"),
         _dev(old_logp, torch.float32, "old_logp"), _dev(adv, torch.float32, "adv"),
         _dev(ret, torch.float32, "ret"), N, int(mini_batch), _dev(cursor, torch.int64, "cursor"),
         _dev(scales, torch.float32, "scales"), float(clip), float(vf_coef), float(ent_coef),
         _dev(grad, torch.float32, "grad"), _dev(loss_out, torch.float32, "loss_out"),
-        _dev(part, torch.float32, "part"), part.numel(), _stream()), "prl_ppo_wide_grad")
+        _dev(part, torch.float32, "part"), part.numel(), *extra, _stream()), "prl_ppo_wide_grad")
 
 
 def ppo_update(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp, adv,
