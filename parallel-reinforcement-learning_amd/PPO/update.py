@@ -57,10 +57,12 @@ class GraphedUpdate:
         prl_native.reserve_workspace(mb, dev)
         # wide nets (outside the persistent engine, e.g. C5's D = 348, A = 17): the step's
         # forward + loss + backward is prl_ppo_wide_grad (two HIP launches reading the minibatch
-        # in place) instead of ~60 PyTorch / hipBLASLt kernels; PRL_WIDE=0 keeps the autograd step
+        # in place) instead of ~60 PyTorch / hipBLASLt kernels.  Part of the native path
+        # (ppo.use_fused); PRL_WIDE=0 or use_fused = False keeps the autograd step
         self.wide = None
         info = (prl_native.ppo_wide_info(S.shape[1], ppo.action_dim, not ppo.is_continuous, mb)
-                if os.environ.get("PRL_WIDE", "1") == "1" else None)
+                if os.environ.get("PRL_WIDE", "1") == "1" and getattr(ppo, "use_fused", True)
+                else None)
         if info is not None and info[0] == sum(self.sizes) == sum(
                 p.numel() for p in ppo.policy.parameters()):
             self.wide = info
