@@ -324,6 +324,34 @@ def main():
                     "optimizer_steps_per_launch": steps_per_launch,
                     "us_per_optimizer_step": round(avg_ms * 1e3 / steps_per_launch, 2),
                     "dtype": "f32"}
+    gu = getattr(ppo, "_last_graphed", None)
+    if roofline is None and gu is not None and gu.wide is not None:
+        # shapes outside the persistent engine (C5): the per-step wide kernel, re-timed on the
+        # last learn()'s first minibatch (cursor 0, mb rows) — the dominant kernel of that update
+        cur0 = torch.zeros(1, dtype=torch.int64, device=gu.cursor.device)
+        wide_args = (gu.pflat, gu.sources[0].shape[1], ppo.action_dim, not ppo.is_continuous,
+                     *gu.sources, gu.mb, cur0, None, ppo.policy_clip, ppo.value_coef,
+                     ppo.entropy_coef, torch.empty_like(gu.pflat), torch.zeros(1, device=cur0.device),
+                     gu.part)
+        cold_med, _ = time_kernel(lambda: prl_native.ppo_wide_grad(*wide_args), cold=True)
+        warm_med, _ = time_kernel(lambda: prl_native.ppo_wide_grad(*wide_args), cold=False)
+        Dw, nout = int(gu.sources[0].shape[1]), (ppo.action_dim + 1 if not ppo.is_continuous
+                                                 else 2 * ppo.action_dim + 1)
+        nh = 2 if not ppo.is_continuous else 3
+        trunk, heads, outs = Dw * 64, nh * 64 * 64, nout * 64
+        fpr = 2 * (trunk + heads + outs) * 2 + 2 * (heads + outs)
+        rows = min(gu.mb, int(gu.sources[0].shape[0]))
+        ach = fpr * rows / (cold_med * 1e-3) / 1e12
+        roofline = {"kernel": "prl_ppo_wide_grad: ppo_wide_grad_kernel + ppo_wide_reduce_kernel "
+                              "(one optimizer step's forward + loss + backward, wide nets)",
+                    "bound": "mfma", "achieved": round(ach, 3), "peak": F32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / F32_PEAK_TFLOPS, 5), "traffic": None,
+                    "limiter": "one wave per SIMD (256 + 256 registers, no spills) and the LDS "
+                               "holding the heads: dependent MFMA chains per 16-row tile",
+                    "avg_launch_us": round(cold_med * 1e3, 2),
+                    "cache": "cold (512 MiB read-only flush)",
+                    "warm_launch_us": round(warm_med * 1e3, 2), "rows_per_launch": rows,
+                    "flops_per_row": fpr, "dtype": "f32"}
     roofline_gae = None
     if gae_call.args is not None:
         a, k = gae_call.args

@@ -329,6 +329,7 @@ class PPO:
                 scales = torch.tensor([mb / counts[j] for j in range(n_graph)],
                                       dtype=torch.float32, device=S.device)
             graphed = GraphedUpdate(self, S, A, old_logp, adv, returns, scales)
+        self._last_graphed = graphed        # (bench.py re-times its wide step)
         pbar = tqdm(total=sum(n_ranks) * self.k_epochs, leave=False,
                     disable=not self.show_progress or (world > 1 and tdist.get_rank() != 0))
         loss = None
