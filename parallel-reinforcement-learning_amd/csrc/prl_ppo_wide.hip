@@ -29,6 +29,8 @@
 
 #include <algorithm>
 
+#include <stdlib.h>
+
 namespace prl {
 namespace {
 
@@ -131,6 +133,7 @@ struct WdArgs {
   float* part;             // [G][Pq + 4]
   int G;
   unsigned long long* prof;   // [8] workgroup 0's s_memrealtime ticks per tile stage (or null)
+  float* dh0;              // split form: [mb][64] trunk pre-activation gradients (dW0 kernel input)
 };
 
 typedef float wd_v4 __attribute__((ext_vector_type(4)));
@@ -420,9 +423,31 @@ __device__ inline void wd_stage(const WdNet& n, const WdArgs& a, int64_t row0, i
   }
 }
 
-template <int KSM>
+// SPLIT: dW0 is left to ppo_wide_dw0_kernel (dH0 goes to HBM); the ~90 registers of its
+// accumulators hold the W0 fragments instead, loaded once per workgroup.
+// the X half of wd_stage (rows >= rc zero; columns >= D untouched)
+__device__ inline void wd_stage_x(const WdNet& n, const WdArgs& a, int64_t row0, int rc, int XS,
+                                  float* Xs) {
+  const int t = threadIdx.x, D = n.D;
+  const float* src = a.S + row0 * D;
+  const int tot = WD_RT * D, have = rc * D;
+  if ((D & 3) == 0 && ((reinterpret_cast<uintptr_t>(a.S) & 15u) == 0)) {
+    for (int f = 4 * t; f < tot; f += 4 * WD_THREADS) {
+      const int r = f / D, d = f - r * D;
+      const float4 v = f < have ? *reinterpret_cast<const float4*>(src + f) : float4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<float4*>(Xs + r * XS + d) = v;
+    }
+  } else {
+    for (int f = t; f < tot; f += WD_THREADS) {
+      const int r = f / D, d = f - r * D;
+      Xs[r * XS + d] = f < have ? src[f] : 0.f;
+    }
+  }
+}
+
+template <int KSM, bool SPLIT>
 __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) {
-  constexpr int KE = KSM / 4;          // 16-column blocks of dW0
+  constexpr int KE = SPLIT ? 1 : KSM / 4;   // 16-column blocks of dW0
   extern __shared__ float4 wd_lds4[];
   float* lds = reinterpret_cast<float*>(wd_lds4);
   const WdNet& n = a.net;
@@ -488,6 +513,23 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
   // dW0 accumulators instead
   const float* w0row = a.params + n.w0 + (int64_t)(16 * w + x) * D;
   const bool w0vec = (D & 3) == 0 && ((reinterpret_cast<uintptr_t>(a.params) & 15u) == 0);
+  float4 w0v[SPLIT ? KSM / 4 : 1];
+  if (SPLIT) {
+#pragma unroll
+    for (int sg = 0; sg < (SPLIT ? KSM / 4 : 1); ++sg) {
+      const int d0 = 16 * sg + 4 * q;
+      float4 wv;
+      if (w0vec) {
+        wv = d0 < D ? *reinterpret_cast<const float4*>(w0row + d0) : float4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        wv.x = d0 < D ? w0row[d0] : 0.f;
+        wv.y = d0 + 1 < D ? w0row[d0 + 1] : 0.f;
+        wv.z = d0 + 2 < D ? w0row[d0 + 2] : 0.f;
+        wv.w = d0 + 3 < D ? w0row[d0 + 3] : 0.f;
+      }
+      w0v[sg] = wv;
+    }
+  }
   // gradient accumulators
   wd_v4 gW0[KE];
   wd_v4 gW1[WD_MAXH][4];
@@ -534,7 +576,9 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
         const int d0 = 16 * sg + 4 * q;
         if (16 * sg < D) {
           float4 wv;
-          if (w0vec) {
+          if (SPLIT) {
+            wv = w0v[SPLIT ? sg : 0];
+          } else if (w0vec) {
             wv = d0 < D ? *reinterpret_cast<const float4*>(w0row + d0) : float4{0.f, 0.f, 0.f, 0.f};
           } else {
             wv.x = d0 < D ? w0row[d0] : 0.f;
@@ -769,6 +813,9 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
     }
     // ---- dW0[16w + 4q + i][16e + x] += sum_rows dH0[row][ch] X[row][16e + x]
     WD_MARK(6)
+    if (SPLIT) {
+      if (x < rc) wd_st4(a.dh0 + (row0 - row_lo + x) * WD_H + 16 * w + 4 * q, dH0);
+    } else {
     wd_st4(Tw + x * 16 + 4 * q, dH0);
     wd_wave_sync();
     {
@@ -782,6 +829,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
           for (int s = 0; s < 4; ++s) gW0[e] = wd_mma(ta[s], Xs[(4 * s + q) * XS + 16 * e + x], gW0[e]);
         }
       }
+    }
     }
     wd_wave_sync();   // Tw is rewritten by the next tile only after its barriers; keep order
     WD_MARK(7)
@@ -797,7 +845,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
     const int d = 16 * e + x;
-    if (d < D) {
+    if (!SPLIT && d < D) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) out[n.w0 + (16 * w + 4 * q + i) * D + d] = gW0[e][i];
     }
@@ -861,6 +909,115 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
         out[n.Pq + k] = s;
       }
       out[n.Pq + 3] = 0.f;
+    }
+  }
+}
+
+// Split form, second pass: dW0[c][d] = sum over the minibatch's rows of dH0[row][c] X[row][d]
+// (K = rows).  Workgroup g takes 32-row tiles g, g + G2, ...; wave w owns channels 16w .. 16w+15
+// (22 16 x 16 accumulators for D = 348).  The next tile's X and dH0 rows are loaded into
+// registers while the current tile's MFMAs run (D % 4 == 0, 16-B aligned S; else staged in
+// place), then written to LDS between two barriers.  Two workgroups per CU.  The partial goes to
+// part2[g] ([64 D] + 4 pad, flat W0 order) for the same fold as the other gradients.
+constexpr int WD2_GRID_MAX = 256;
+constexpr int WD2_RT = 32;
+template <int KSM>
+__global__ __launch_bounds__(WD_THREADS, 2) void ppo_wide_dw0_kernel(WdArgs a, float* part2, int G2) {
+  constexpr int KE = KSM / 4;
+  constexpr int XS2 = 4 * KSM + 4;
+  constexpr int HS = 68;
+  constexpr int NPF = (WD2_RT * 4 * KSM / 4 + WD_THREADS - 1) / WD_THREADS;   // float4 per thread
+  __shared__ float Xs[WD2_RT * XS2];
+  __shared__ float Hs[WD2_RT * HS];
+  const WdNet& n = a.net;
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  const int D = n.D;
+  const int64_t j = *a.cursor;
+  const int64_t row_lo = j * a.mb;
+  const int64_t rows = row_lo < a.N ? (a.N - row_lo < a.mb ? a.N - row_lo : a.mb) : 0;
+  const int ntile = (int)((rows + WD2_RT - 1) / WD2_RT);
+  const bool vec = (D & 3) == 0 && (reinterpret_cast<uintptr_t>(a.S) & 15u) == 0;
+  for (int k = t; k < WD2_RT * XS2; k += WD_THREADS) Xs[k] = 0.f;
+  const wd_v4 z4 = {0.f, 0.f, 0.f, 0.f};
+  wd_v4 acc[KE];
+#pragma unroll
+  for (int e = 0; e < KE; ++e) acc[e] = z4;
+  float4 px[NPF];
+  float4 ph[2];   // dH0: 32 rows x 64 = 512 float4, 2 per thread
+  auto load = [&](int tile) {
+    const int64_t r0 = (int64_t)tile * WD2_RT;   // relative to row_lo
+    const int rc = (int)(rows - r0 < WD2_RT ? rows - r0 : WD2_RT);
+    const float* src = a.S + (row_lo + r0) * D;
+    const int have = rc * D;
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int f = 4 * (t + WD_THREADS * i);
+      px[i] = f < have ? *reinterpret_cast<const float4*>(src + f) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int f = 4 * (t + WD_THREADS * i);
+      ph[i] = (f >> 6) < rc ? *reinterpret_cast<const float4*>(a.dh0 + r0 * WD_H + f)
+                            : float4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store = [&]() {
+    const int tot = WD2_RT * D;
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      const int f = 4 * (t + WD_THREADS * i);
+      if (f < tot) {
+        const int r = f / D, d = f - r * D;
+        *reinterpret_cast<float4*>(Xs + r * XS2 + d) = px[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int f = 4 * (t + WD_THREADS * i);
+      *reinterpret_cast<float4*>(Hs + (f >> 6) * HS + (f & 63)) = ph[i];
+    }
+  };
+  __syncthreads();
+  if (vec && (int)blockIdx.x < ntile) load(blockIdx.x);
+  for (int tile = blockIdx.x; tile < ntile; tile += G2) {
+    if (vec) {
+      store();
+    } else {   // scalar staging in place
+      const int64_t r0 = (int64_t)tile * WD2_RT;
+      const int rc = (int)(rows - r0 < WD2_RT ? rows - r0 : WD2_RT);
+      const float* src = a.S + (row_lo + r0) * D;
+      for (int f = t; f < WD2_RT * D; f += WD_THREADS) {
+        const int r = f / D, d = f - r * D;
+        Xs[r * XS2 + d] = r < rc ? src[f] : 0.f;
+      }
+      for (int e = t; e < WD2_RT * WD_H; e += WD_THREADS)
+        Hs[(e >> 6) * HS + (e & 63)] = (e >> 6) < rc ? a.dh0[r0 * WD_H + e] : 0.f;
+    }
+    __syncthreads();
+    if (vec && tile + G2 < ntile) load(tile + G2);   // in flight under the MFMAs
+#pragma unroll
+    for (int kk = 0; kk < WD2_RT / 16; ++kk) {
+      float ta[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) ta[s] = Hs[(16 * kk + 4 * s + q) * HS + 16 * w + x];
+#pragma unroll
+      for (int e = 0; e < KE; ++e) {
+        if (16 * e < D) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            acc[e] = wd_mma(ta[s], Xs[(16 * kk + 4 * s + q) * XS2 + 16 * e + x], acc[e]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* out = part2 + (int64_t)blockIdx.x * (WD_H * D + 4);
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    const int d = 16 * e + x;
+    if (d < D) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[(16 * w + 4 * q + i) * D + d] = acc[e][i];
     }
   }
 }
@@ -936,6 +1093,23 @@ __global__ __launch_bounds__(256) void ppo_wide_reduce_kernel(const float* __res
 // KSM instantiated for D <= 128 and D <= 352
 int wd_ksm(int D) { return D <= 128 ? 32 : (D <= 352 ? 88 : 0); }
 
+int wd_grid(int64_t mb);
+int wd_grid2(int64_t mb) {
+  const int64_t tiles = (mb + WD2_RT - 1) / WD2_RT;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, WD2_GRID_MAX));
+}
+bool wd_split() {
+  static const int v = [] {
+    const char* e = getenv("PRL_WIDE_SPLIT");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v != 0;
+}
+// part layout: [G][Pq + 4] kernel-1 partials | dH0 [mb][64] | [G2][64 D + 4] dW0 partials
+int64_t wd_part_floats(const WdNet& n, int64_t mb) {
+  return (int64_t)wd_grid(mb) * (n.Pq + 4) + mb * WD_H + (int64_t)wd_grid2(mb) * (WD_H * n.D + 4);
+}
+
 int wd_grid(int64_t mb) {
   const int64_t tiles = (mb + WD_RT - 1) / WD_RT;
   return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, WD_GRID_MAX));
@@ -957,7 +1131,7 @@ extern "C" int prl_ppo_wide_info(int32_t D, int32_t A, int32_t discrete, int64_t
   if (wd_lds_bytes(n, wd_ksm(D)) > 160 * 1024) return PRL_ERR_ARG;
   const int G = wd_grid(mini_batch);
   if (n_params) *n_params = n.P;
-  if (part_floats) *part_floats = (int64_t)G * (n.Pq + 4);
+  if (part_floats) *part_floats = wd_part_floats(n, mini_batch);
   if (grid) *grid = G;
   return PRL_OK;
 }
@@ -996,7 +1170,7 @@ extern "C" int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A,
   PRL_REQUIRE(params && S && actions && old_logp && adv && ret && cursor && grad && part,
               "prl_ppo_wide_grad: null pointer");
   const int G = wd_grid(mini_batch);
-  PRL_REQUIRE(part_floats >= (int64_t)G * (n.Pq + 4), "prl_ppo_wide_grad: part buffer too small");
+  PRL_REQUIRE(part_floats >= wd_part_floats(n, mini_batch), "prl_ppo_wide_grad: part buffer too small");
   const int KSM = wd_ksm(D);
   const size_t lds = wd_lds_bytes(n, KSM);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_wide_grad: LDS %zu bytes", lds);
@@ -1017,30 +1191,46 @@ extern "C" int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A,
   a.part = part;
   a.G = G;
   a.prof = prof;
+  const bool split = wd_split();
+  a.dh0 = part + (int64_t)G * (n.Pq + 4);
+  float* part2 = a.dh0 + mini_batch * WD_H;
+  const int G2 = wd_grid2(mini_batch);
   hipStream_t st = as_stream(stream);
   // the kernels' dynamic-LDS limit is raised once per process (not a stream operation, but kept
   // out of the per-step path that graphs capture)
-  static bool lds_set[2] = {false, false};
+  static bool lds_set[4] = {false, false, false, false};
+#define WD_LAUNCH(K, SP, slot)                                                                  \
+  do {                                                                                       \
+    if (!lds_set[slot]) {                                                                    \
+      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<K, SP>), \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); \
+      lds_set[slot] = true;                                                                  \
+    }                                                                                        \
+    hipLaunchKernelGGL((ppo_wide_grad_kernel<K, SP>), dim3(G), dim3(WD_THREADS), lds, st, a);  \
+  } while (0)
   if (KSM == 32) {
-    if (!lds_set[0]) {
-      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<32>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      lds_set[0] = true;
-    }
-    hipLaunchKernelGGL(ppo_wide_grad_kernel<32>, dim3(G), dim3(WD_THREADS), lds, st, a);
+    if (split) WD_LAUNCH(32, true, 0); else WD_LAUNCH(32, false, 1);
   } else {
-    if (!lds_set[1]) {
-      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<88>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      lds_set[1] = true;
-    }
-    hipLaunchKernelGGL(ppo_wide_grad_kernel<88>, dim3(G), dim3(WD_THREADS), lds, st, a);
+    if (split) WD_LAUNCH(88, true, 2); else WD_LAUNCH(88, false, 3);
   }
+#undef WD_LAUNCH
   PRL_LAUNCH_CHECK("ppo_wide_grad");
   const int nq = (n.Pq + 4) / 4;
   hipLaunchKernelGGL(ppo_wide_reduce_kernel, dim3((unsigned)cdiv(nq, WR_QUADS)), dim3(256), 0, st,
                      part, G, n.P, n.Pq, grad, loss_out, cursor, scales, N, mini_batch, vf_coef,
                      ent_coef);
   PRL_LAUNCH_CHECK("ppo_wide_reduce");
+  if (split) {   // dW0 = dH0^T X, then its fold over the G2 partials into grad's W0 block
+    if (KSM == 32)
+      hipLaunchKernelGGL(ppo_wide_dw0_kernel<32>, dim3(G2), dim3(WD_THREADS), 0, st, a, part2, G2);
+    else
+      hipLaunchKernelGGL(ppo_wide_dw0_kernel<88>, dim3(G2), dim3(WD_THREADS), 0, st, a, part2, G2);
+    PRL_LAUNCH_CHECK("ppo_wide_dw0");
+    const int P2 = WD_H * n.D;   // 64 D: a multiple of 4
+    hipLaunchKernelGGL(ppo_wide_reduce_kernel, dim3((unsigned)cdiv((P2 + 4) / 4, WR_QUADS)), dim3(256),
+                       0, st, part2, G2, P2, P2, grad + n.w0, nullptr, cursor, scales, N,
+                       mini_batch, vf_coef, ent_coef);
+    PRL_LAUNCH_CHECK("ppo_wide_reduce_dw0");
+  }
   return PRL_OK;
 }
