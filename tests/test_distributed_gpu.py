@@ -264,3 +264,75 @@ def test_two_ranks_at_config_per_rank_shape(tmp_path, name, cfg):
         if not key.startswith("_"):
             np.testing.assert_array_equal(outs[0][key], outs[1][key], err_msg=key)
     assert all(np.isfinite(o["_loss"]) for o in outs)   # each rank reports its own rows
+
+
+def _wide_shard(rank, mb, nb, D=348, A=17):
+    rng = np.random.default_rng(100 + rank)
+    n = mb * nb
+    S = (rng.normal(size=(n, D)) * 0.5).astype(np.float32)
+    Aa = (np.tanh(rng.normal(size=(n, A))) * 0.3).astype(np.float32)
+    R = rng.normal(1, 0.5, n).astype(np.float32)
+    Dn = (rng.random(n) < 0.02).astype(np.float32)
+    Dn[mb - 1::mb] = 1      # episodes end at every minibatch block: GAE equal on the union
+    return S, Aa, R, Dn
+
+
+def _make_wide_ppo(mb, k):
+    from PPO import PPO
+    torch.manual_seed(0)
+    p = PPO(True, 348, 17, action_scaling=1.0, lr=3e-4, k_epochs=k, batch_size=1,
+            mini_batch_size=mb, policy_clip=1e3)     # smooth surrogate: compare in function space
+    p.show_progress = False
+    p.graph_min_steps = 1
+    return p
+
+
+def _wide_worker(rank, world, port, mb, nb, k, out_dir):
+    sys.path[:0] = PATHS
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        p = _make_wide_ppo(mb, k)
+        p.memory.push_device(*(torch.from_numpy(x).cuda() for x in _wide_shard(rank, mb, nb)))
+        p.learn()
+        torch.cuda.synchronize()
+        sd = {kk: v.cpu().numpy() for kk, v in p.policy.state_dict().items()}
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **sd,
+                 _wide=np.int64(p._last_graphed is not None and p._last_graphed.wide is not None),
+                 _path=np.array(p.last_update_path))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_two_ranks_wide_step_equal_one_process_on_the_union(tmp_path):
+    """C5's net (D 348, A 17) on 2 ranks through the wide step (prl_ppo_wide_grad into the
+    all-reduce buffer, scaled by 1 / union rows) vs ONE process on the interleaved union with
+    minibatch 2 mb: both ranks bit-identical, and the learned function equal to 1e-3 (the sums
+    differ in order)."""
+    import copy
+    import random
+    import types
+    mb, nb, k = 256, 4, 2
+    port = 29960 + random.randint(0, 30)
+    mp.spawn(_wide_worker, args=(2, port, mb, nb, k, str(tmp_path)), nprocs=2, join=True)
+    outs = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(2)]
+    assert str(outs[0]["_path"]) == "graph" and int(outs[0]["_wide"]) == 1
+    shards = [_wide_shard(r, mb, nb) for r in range(2)]
+    cols = [np.concatenate([shards[r][c][j * mb:(j + 1) * mb] for j in range(nb) for r in range(2)])
+            for c in range(4)]
+    p = _make_wide_ppo(2 * mb, k)
+    p.memory.push_device(*(torch.from_numpy(x).cuda() for x in cols))
+    p.learn()
+    ref = {kk: v.cpu().numpy() for kk, v in p.policy.state_dict().items()}
+    for key in ref:
+        np.testing.assert_array_equal(outs[0][key], outs[1][key], err_msg=key)
+    q = types.SimpleNamespace(policy=copy.deepcopy(p.policy))
+    q.policy.load_state_dict({kk: torch.from_numpy(outs[0][kk]) for kk in ref})
+    S = torch.from_numpy(cols[0][:256]).cuda()
+    A = torch.from_numpy(cols[1][:256]).cuda()
+    from test_engine_gpu import _outputs
+    (l1, v1), (l2, v2) = _outputs(q, S, A), _outputs(p, S, A)
+    el = float((l1 - l2).abs().max()) / (float(l2.abs().max()) + 1.0)
+    ev = float((v1 - v2).abs().max()) / (float(v2.abs().max()) + 1.0)
+    assert el <= 1e-3 and ev <= 1e-3, (el, ev)
