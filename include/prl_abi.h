@@ -356,6 +356,12 @@ int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_sq, float* 
                        int32_t rank, void* const* xbufs, int64_t seq0, void* workspace,
                        int64_t workspace_bytes, void* stream);
 int64_t prl_dp_xbuf_bytes(int32_t D, int32_t A, int32_t discrete, int32_t mini_batch);
+/* polls of prl_ppo_update_dpx's cross-rank wait before it gives up (the launch then ends with a
+ * nonzero status word and the caller restores its snapshot, PPO/engine.py); 0 restores the
+ * default (2^24 polls, each a system-scope load: seconds, which also absorbs launch skew between
+ * the ranks).  Per process; returns the previous value.  Tests lower it to exercise the failure
+ * path.  No reference counterpart. */
+uint32_t prl_dp_set_spin_limit(uint32_t polls);
 int prl_dp_xbuf_alloc(int64_t bytes, void** out);
 int prl_dp_xbuf_free(void* p);
 int prl_dp_ipc_handle(void* p, uint8_t* out, int64_t out_bytes);   /* out: 64 bytes */

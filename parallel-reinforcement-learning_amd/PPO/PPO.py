@@ -286,6 +286,8 @@ class PPO:
         eng = getattr(self, "_engine", None)
         if eng is not None and eng.mini_batch == self.mini_batch_size:
             return eng
+        if eng is not None:   # mini_batch changed: release its RCCL comm / slice buffers first
+            eng.close()
         from .engine import FusedUpdate
         try:
             self._engine = FusedUpdate(self, self.mini_batch_size)
@@ -319,11 +321,14 @@ class PPO:
         nb = max(-(-n // mb) for n in n_ranks)
         counts = [sum(min(mb, max(0, n - j * mb)) for n in n_ranks) for j in range(nb)]
         n_graph = min(n // mb for n in n_ranks)
+        from .update import GraphedUpdate, wide_info
+        # nets the wide step covers (C5's D = 348 / A = 17) always go through it, however few
+        # steps there are (GraphedUpdate captures a graph only past its two eager warm-up steps)
         use_graph = (self.use_graphs and S.is_cuda
-                     and self.k_epochs * n_graph >= self.graph_min_steps)
+                     and (self.k_epochs * n_graph >= self.graph_min_steps
+                          or wide_info(self, S.shape[1]) is not None))
         graphed = None
         if use_graph:
-            from .update import GraphedUpdate
             scales = None
             if world > 1:
                 scales = torch.tensor([mb / counts[j] for j in range(n_graph)],

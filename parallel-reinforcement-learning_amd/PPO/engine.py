@@ -257,10 +257,12 @@ class FusedUpdate:
             prl_native.dp_xbuf_free(own)
             return None
         self._xbuf_own, self._xbufs, self._dp_rank, self._dp_seq = own, ptrs, rank, 0
-        ok = self._dp_selftest(world)
-        votes = [None] * world
-        tdist.all_gather_object(votes, ok)
-        if not all(votes):
+        # every rank runs the same collectives whatever its local outcome: ONE gather of
+        # (ok, checksum) per rank, then the same decision everywhere
+        res = [None] * world
+        tdist.all_gather_object(res, self._dp_selftest(world))
+        sums = [c for _, c in res]
+        if not (all(ok for ok, _ in res) and len(set(sums)) == 1 and sums[0] == sums[0]):
             warnings.warn("data-parallel persistent engine failed its self-test; using the "
                           "stepped loop")
             self.close()
@@ -271,10 +273,10 @@ class FusedUpdate:
     def _dp_checksum(self, flat) -> float:
         return float(flat.double().sum().item()) + float((flat.double() ** 2).sum().item())
 
-    def _dp_selftest(self, world) -> bool:
+    def _dp_selftest(self, world):
         """One small prl_ppo_update_dpx launch (2 minibatches per rank, k 1) on scratch copies
-        of the state: no in-kernel timeout and the same parameters on every rank."""
-        import torch.distributed as tdist
+        of the state.  Local only (no collective): returns (ok, parameter checksum); the caller
+        gathers every rank's pair at once."""
         try:
             mb = self.mini_batch
             n = 2 * mb
@@ -303,22 +305,29 @@ class FusedUpdate:
             if status != 0:
                 # the sticky word stays set: clear the workspace so the engine's own runs start clean
                 self.ws.zero_()
-                return False
-            sums = [None] * world
-            tdist.all_gather_object(sums, self._dp_checksum(flat))
-            return len(set(sums)) == 1 and all(x == x for x in sums)
+                return False, None
+            return True, self._dp_checksum(flat)
         except RuntimeError as e:
             warnings.warn(f"data-parallel persistent self-test failed ({e})")
-            return False
+            return False, None
 
-    def run_dp_persistent(self, S, A, old_logp, adv, ret, k_epochs: int, n_ranks):
+    def run_dp_persistent(self, S, A, old_logp, adv, ret, k_epochs: int, n_ranks, all_reduce):
         """run() as one data-parallel rank: ONE persistent launch for the whole loop; each step's
         gradient is summed over the ranks inside it (union minibatch j = every rank's rows
-        j*mb .. (j+1)*mb, weighted 1 / union rows, as run_stepped)."""
+        j*mb .. (j+1)*mb, weighted 1 / union rows, as run_stepped).
+
+        Failure handling: parameters, both moments and the step count (3 x 36 KB for CartPole)
+        are snapshotted before the launch.  After it every rank gathers (status, checksum) in ONE
+        collective.  If any rank's launch timed out in its cross-rank wait (a peer late or gone:
+        prl_dp_set_spin_limit) or the checksums differ, every rank restores its snapshot, drops
+        the slice buffers and re-runs this learn()'s update through the stepped loop
+        (run_stepped: one grad launch + all-reduce per step), which later learns keep using."""
         import torch.distributed as tdist
         xb = self.dp_slices()
         if not self.bound():
             self._bind()
+        world = tdist.get_world_size()
+        snap = (self.flat.clone(), self.m.clone(), self.v.clone(), self.step.clone())
         group = self.ppo.optimizer.param_groups[0]
         beta1, beta2 = group["betas"]
         mb = self.mini_batch
@@ -326,6 +335,13 @@ class FusedUpdate:
         counts = [sum(min(mb, max(0, n - j * mb)) for n in n_ranks) for j in range(nb)]
         inv = torch.tensor([1.0 / c for c in counts], dtype=torch.float32, device=S.device)
         A2 = A if A.dim() == 2 else A.reshape(-1, 1)
+        # the ranks' launches must overlap: line them up (the cross-rank wait also absorbs skew)
+        torch.cuda.synchronize()
+        tdist.barrier()
+        delay = os.environ.get("PRL_DP_TEST_DELAY", "")   # test-only: "rank:seconds"
+        if delay and int(delay.split(":")[0]) == self._dp_rank:
+            import time
+            time.sleep(float(delay.split(":")[1]))
         if self.events is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
@@ -334,24 +350,34 @@ class FusedUpdate:
             S.contiguous(), A2.contiguous(), old_logp.contiguous(), adv.contiguous(),
             ret.contiguous(), mb, k_epochs, nb, inv, self.ppo.policy_clip, self.ppo.value_coef,
             self.ppo.entropy_coef, group["lr"], beta1, beta2, group["eps"],
-            group["weight_decay"], 2.0, self.loss, tdist.get_world_size(), self._dp_rank, xb,
+            group["weight_decay"], 2.0, self.loss, world, self._dp_rank, xb,
             self._dp_seq, self.ws)
         self._dp_seq += int(k_epochs) * nb
         if self.events is not None:
             ev[1].record()
             self.events.append(("ppo_update_kernel_dp", ev[0], ev[1],
                                 int(S.shape[0]) * int(k_epochs), int(k_epochs) * nb))
-        self._sync_optimizer_state()
         status = max(prl_native.ppo_update_status(self.ws).tolist())
-        if status != 0:
-            raise RuntimeError(f"prl_ppo_update_dpx: in-kernel timeout (status {status}); the "
-                               "policy parameters are undefined")
-        # the ranks must still hold the same parameters (one scalar per rank per learn())
-        sums = [None] * tdist.get_world_size()
-        tdist.all_gather_object(sums, self._dp_checksum(self.flat))
-        if len(set(sums)) != 1:
-            raise RuntimeError(f"prl_ppo_update_dpx: ranks diverged (parameter checksums {sums})")
-        return self.loss.reshape(())
+        res = [None] * world
+        tdist.all_gather_object(res, (status, self._dp_checksum(self.flat) if status == 0 else None))
+        sums = [c for _, c in res]
+        if all(st == 0 for st, _ in res) and len(set(sums)) == 1:
+            self._sync_optimizer_state()
+            return self.loss.reshape(())
+        # a rank timed out or the ranks diverged: restore, and take the stepped loop from here
+        warnings.warn(f"data-parallel persistent launch failed (status / checksum per rank: "
+                      f"{res}); restoring the pre-launch state and re-running this update on "
+                      "the stepped loop")
+        self.flat.copy_(snap[0])
+        self.m.copy_(snap[1])
+        self.v.copy_(snap[2])
+        self.step.copy_(snap[3])
+        self.ws.zero_()
+        self.dp_fallbacks = getattr(self, "dp_fallbacks", 0) + 1
+        self.close()
+        self._xb_tried = True            # dp_slices() -> None from now on
+        self._sync_optimizer_state()
+        return self.run_stepped(S, A, old_logp, adv, ret, k_epochs, n_ranks, all_reduce)
 
     def run_stepped(self, S, A, old_logp, adv, ret, k_epochs: int, n_ranks, all_reduce,
                     comm=None):
@@ -367,7 +393,7 @@ class FusedUpdate:
         gradient image every step.  Both give the same bits."""
         import ctypes
         if k_epochs > 0 and comm is None and self.dp_slices() is not None:
-            return self.run_dp_persistent(S, A, old_logp, adv, ret, k_epochs, n_ranks)
+            return self.run_dp_persistent(S, A, old_logp, adv, ret, k_epochs, n_ranks, all_reduce)
         if not self.bound():
             self._bind()
         group = self.ppo.optimizer.param_groups[0]

@@ -23,6 +23,20 @@ from torch import nn
 import prl_native
 
 
+def wide_info(ppo, D: int):
+    """prl_ppo_wide_grad's (params, partial floats, grid) for this policy, or None when the wide
+    step does not apply (shape outside it, use_fused off, or PRL_WIDE=0)."""
+    if os.environ.get("PRL_WIDE", "1") != "1" or not getattr(ppo, "use_fused", True):
+        return None
+    info = prl_native.ppo_wide_info(D, ppo.action_dim, not ppo.is_continuous,
+                                    ppo.mini_batch_size)
+    n_params = sum(p.numel() for p in ppo.policy.parameters())
+    if info is None or info[0] != n_params or n_params != sum(
+            p.numel() for p in ppo.policy.parameters() if p.requires_grad):
+        return None
+    return info
+
+
 class GraphedUpdate:
     WARMUP = 2
 
@@ -60,11 +74,8 @@ class GraphedUpdate:
         # in place) instead of ~60 PyTorch / hipBLASLt kernels.  Part of the native path
         # (ppo.use_fused); PRL_WIDE=0 or use_fused = False keeps the autograd step
         self.wide = None
-        info = (prl_native.ppo_wide_info(S.shape[1], ppo.action_dim, not ppo.is_continuous, mb)
-                if os.environ.get("PRL_WIDE", "1") == "1" and getattr(ppo, "use_fused", True)
-                else None)
-        if info is not None and info[0] == sum(self.sizes) == sum(
-                p.numel() for p in ppo.policy.parameters()):
+        info = wide_info(ppo, S.shape[1])
+        if info is not None:
             self.wide = info
             self.pflat = torch.empty(info[0], dtype=torch.float32, device=dev)
             self.part = torch.empty(info[1], dtype=torch.float32, device=dev)

@@ -55,6 +55,11 @@ constexpr int UPD_MAXD = 64;      // max observation dim on the fused path
 constexpr int UPD_MAXA = 8;       // max action dim on the fused path
 constexpr int UPD_MAX_RANKS = 8;   // data-parallel ranks of one persistent launch (one node)
 constexpr unsigned UPD_SPIN_LIMIT = 1u << 22;  // ~0.1-0.3 s of s_sleep polls: never expected
+// the cross-RANK wait of the data-parallel launch (upd_dp_union_slice) also absorbs the skew
+// between the ranks' launches and each poll is a system-scope load (a peer GPU's memory over
+// xGMI): its own, much longer default limit, set per process by prl_dp_set_spin_limit (tests
+// lower it to provoke the timeout path)
+constexpr unsigned UPD_DP_SPIN_LIMIT = 1u << 24;
 
 struct UpdTensor {
   int flat, lds, rows, cols, stride;
@@ -145,6 +150,7 @@ struct UpdArgs {
   int world, rank;
   const float* inv_count;    // [nb] 1 / rows of union minibatch j over all ranks (null: 1 / B)
   unsigned long long dp_seq0;   // exchange sequence number of this launch's first step
+  unsigned dp_spin_limit;       // polls of the cross-rank wait before it gives up
   float* xbuf[UPD_MAX_RANKS];             // rank r's [2][Qtot * 4] slice buffers (peer mappings)
   unsigned long long* xflag[UPD_MAX_RANKS];   // rank r's [G] per-workgroup step flags
   float* xbuf_self;                       // == xbuf[rank] (no dynamic kernarg indexing)
@@ -1131,7 +1137,7 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
                          __hip_atomic_load(fl + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= want;
       if (__ballot(!ready) == 0ull) break;
       if (ld_sc1u(args.ctr + 2) != 0u) { ok = false; break; }
-      if (spins > UPD_SPIN_LIMIT) {
+      if (spins > args.dp_spin_limit) {
         if (t == 0) {
           __hip_atomic_store(args.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(args.ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1812,6 +1818,7 @@ struct UpdDp {
 };
 // the slice buffers [2][Qtot * 4] f32, then the per-workgroup step flags [G] u64
 size_t upd_xbuf_flags_off(const UpdNet& n) { return (((size_t)n.Lp / 4 + 1) * 32 + 255) & ~(size_t)255; }
+unsigned g_dp_spin_limit = UPD_DP_SPIN_LIMIT;
 
 int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, int32_t D,
             int32_t A, int32_t discrete, const float* S, const float* actions,
@@ -1879,6 +1886,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     args.rank = dp->rank;
     args.inv_count = dp->inv_count;
     args.dp_seq0 = (unsigned long long)dp->seq0;
+    args.dp_spin_limit = g_dp_spin_limit;
     const size_t fo = upd_xbuf_flags_off(args.net);
     for (int r = 0; r < dp->world; ++r) {
       PRL_REQUIRE(dp->xbufs[r], "prl_ppo_update_dpx: null slice buffer of rank %d", r);
@@ -1937,6 +1945,12 @@ extern "C" int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_
   return upd_run(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp,
                  adv, ret, N, mini_batch, k_epochs, clip, vf_coef, ent_coef, lr, beta1, beta2, eps,
                  weight_decay, max_norm, loss_out, workspace, workspace_bytes, stream, &dp);
+}
+
+extern "C" uint32_t prl_dp_set_spin_limit(uint32_t polls) {
+  const uint32_t prev = g_dp_spin_limit;
+  g_dp_spin_limit = polls ? polls : UPD_DP_SPIN_LIMIT;
+  return prev;
 }
 
 extern "C" int64_t prl_dp_xbuf_bytes(int32_t D, int32_t A, int32_t discrete, int32_t mini_batch) {

@@ -1196,15 +1196,18 @@ extern "C" int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A,
   float* part2 = a.dh0 + mini_batch * WD_H;
   const int G2 = wd_grid2(mini_batch);
   hipStream_t st = as_stream(stream);
-  // the kernels' dynamic-LDS limit is raised once per process (not a stream operation, but kept
-  // out of the per-step path that graphs capture)
-  static bool lds_set[4] = {false, false, false, false};
+  // the kernels' dynamic-LDS limit is raised once per process AND device (the attribute is
+  // per device; not a stream operation, but kept out of the per-step path that graphs capture)
+  static unsigned long long lds_set[4] = {0ull, 0ull, 0ull, 0ull};   // bit = device ordinal
+  int dev_ord = 0;
+  PRL_HIP_TRY(hipGetDevice(&dev_ord));
+  const unsigned long long dev_bit = 1ull << (dev_ord & 63);
 #define WD_LAUNCH(K, SP, slot)                                                                  \
   do {                                                                                       \
-    if (!lds_set[slot]) {                                                                    \
+    if (!(lds_set[slot] & dev_bit)) {                                                        \
       PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<K, SP>), \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); \
-      lds_set[slot] = true;                                                                  \
+      lds_set[slot] |= dev_bit;                                                              \
     }                                                                                        \
     hipLaunchKernelGGL((ppo_wide_grad_kernel<K, SP>), dim3(G), dim3(WD_THREADS), lds, st, a);  \
   } while (0)

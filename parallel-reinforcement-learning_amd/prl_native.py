@@ -69,6 +69,7 @@ SIGNATURES = {
     "prl_ppo_update_dpx": [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32,
                            _I32, _I32, _P] + [_F32] * 9 + [_P, _I32, _I32, _P, _I64, _P, _I64, _P],
     "prl_dp_xbuf_bytes": [_I32, _I32, _I32, _I32],
+    "prl_dp_set_spin_limit": [ctypes.c_uint32],
     "prl_dp_xbuf_alloc": [_I64, _P],
     "prl_dp_xbuf_free": [_P],
     "prl_dp_ipc_handle": [_P, _P, _I64],
@@ -86,6 +87,7 @@ SIGNATURES = {
                               + [_I64, _I32, _I64] + [_F32] * 10 + [_P, _P, _P, _I64, _P],
 }
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,
+             "prl_dp_set_spin_limit": ctypes.c_uint32,
              "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
 
 _lib = None
@@ -548,6 +550,12 @@ def dp_xbuf_bytes(D, A, discrete, mini_batch) -> int:
     if n <= 0:
         raise ValueError(f"prl_dp_xbuf_bytes: shape D={D} A={A} not on the fused engine")
     return n
+
+
+def dp_set_spin_limit(polls: int) -> int:
+    """Polls of the data-parallel launch's cross-rank wait before it times out (0: default);
+    returns the previous value."""
+    return int(lib().prl_dp_set_spin_limit(int(polls)))
 
 
 def dp_xbuf_alloc(nbytes: int) -> ctypes.c_void_p:

@@ -139,7 +139,7 @@ class _TorchProxy:
 
 
 def make_learn(torch, ppo_pkg, continuous=False, tag="learn", N=1500, mb=512, k_epochs=2,
-               use_rnd=False, D=None, A=None, ckpt=False, store_inputs=True):
+               use_rnd=False, D=None, A=None, ckpt=False, store_inputs=True, light=False):
     ppo_mod = sys.modules["PPO.PPO"]  # the package re-exports the class under the same name
     torch.manual_seed(0)
     if D is None:
@@ -228,14 +228,16 @@ def make_learn(torch, ppo_pkg, continuous=False, tag="learn", N=1500, mb=512, k_
         "old_logp": cat(rec["old_logp"]), "old_V": cat(rec["old_V"]),
         "returns": rec["gae_ret"][0], "adv_raw": rec["adv_raw"][0].numpy(),
         "adv": cat(rec["adv_mb"][: -(-N // mb)]),
-        # per optimizer step (k_epochs * ceil(N/mb) of them), concatenated
+    })
+    if not light:   # per optimizer step (k_epochs * ceil(N/mb) of them), concatenated
+        out.update({
         "step_logp": cat(rec["logp"]), "step_V": cat(rec["V"]),
         "step_H": torch.stack(rec["H"]).numpy(), "step_diff": cat(rec["diff"]),
         "step_ratio": cat(rec["ratio"]), "step_min": cat(rec["min"]),
         "step_sl1": torch.stack(rec["sl1"]).numpy(), "step_dlogp": cat(rec["dlogp"]),
         "step_dV": cat(rec["dV"]), "step_ret": cat(rec["sl1_in_R"]),
         "step_adv": cat(rec["adv_mb"]),
-    })
+        })
     for k, v in init_sd.items():
         out["init/" + k] = v
     for k, v in final_sd.items():
@@ -414,6 +416,13 @@ def main():
         "learn_rnd_big": lambda: make_learn(torch, ppo_pkg, continuous=True, tag="learn_rnd_big",
                                             N=20000, mb=16384, k_epochs=1, use_rnd=True, D=348,
                                             A=17, store_inputs=False),
+        # C5's own mini_batch (65,536 rows, the bench's) with a ragged second minibatch and two
+        # epochs: the wide step at full size against the reference's post-learn() weights
+        # (inputs regenerated by learn_inputs.py; per-step arrays not stored)
+        "learn_rnd_c5mb": lambda: make_learn(torch, ppo_pkg, continuous=True,
+                                             tag="learn_rnd_c5mb", N=65536 + 3000, mb=65536,
+                                             k_epochs=2, use_rnd=True, D=348, A=17,
+                                             store_inputs=False, light=True),
         "rnd": lambda: make_rnd(torch, ppo_pkg),
         "worker": lambda: make_worker(apo, utils, ppo_pkg),
         "envs": lambda: make_envs(apo),

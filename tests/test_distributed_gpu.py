@@ -336,3 +336,130 @@ def test_two_ranks_wide_step_equal_one_process_on_the_union(tmp_path):
     el = float((l1 - l2).abs().max()) / (float(l2.abs().max()) + 1.0)
     ev = float((v1 - v2).abs().max()) / (float(v2.abs().max()) + 1.0)
     assert el <= 1e-3 and ev <= 1e-3, (el, ev)
+
+
+def _rnd_gpu_worker(rank, world, port, mb, rows, D, out_dir):
+    sys.path[:0] = PATHS
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from PPO import PPO
+        from PPO.RND import RND
+        torch.manual_seed(7)                       # same initial predictor / target on every rank
+        r = RND(D, D, device="cuda")
+        x = torch.from_numpy(np.random.default_rng(100 + rank).normal(size=(rows[rank], D))
+                             .astype(np.float32)).cuda()
+        nb = max(-(-n // mb) for n in rows)
+        counts = [sum(min(mb, max(0, n - j * mb)) for n in rows) for j in range(nb)]
+        r.update_pred(list(x.split(mb)), PPO.all_reduce, counts)
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, f"rnd{rank}.npz"),
+                 **{k: v.cpu().numpy() for k, v in r.pred_net.state_dict().items()})
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_rnd_update_pred_two_ranks_on_gpu_equal_one_process_on_the_union(tmp_path):
+    """RND.update_pred (RND.py:96-115) on 2 data-parallel ranks sharing cuda:0, at
+    C5's width (D = 348) with a first minibatch of 16,384 rows per rank, so the predictor's
+    backward runs the HIP GroupNorm+SiLU kernels (layers.GroupNormSiLU) and, on rank 0, the
+    split-K / colsum weight and bias gradients (layers.SPLIT_MIN_ROWS); rank 1 has fewer rows
+    (unequal shards, lockstep).  Against ONE process on the CPU (the reference's own PyTorch-CPU
+    arithmetic) whose minibatch j is [rank0 slice j | rank1 slice j]: both ranks bit-identical,
+    weights within 5e-6 (3 AdamW steps of lr 1e-3 from different float32 summation orders:
+    < 0.2 % of the 3e-3 a weight can move)."""
+    import random
+    from PPO.RND import RND
+    D, mb, rows = 348, 16384, (16384 + 9000, 13000)
+    port = 29900 + random.randint(0, 50)
+    mp.spawn(_rnd_gpu_worker, args=(2, port, mb, rows, D, str(tmp_path)), nprocs=2, join=True)
+    outs = [np.load(os.path.join(tmp_path, f"rnd{r}.npz")) for r in range(2)]
+    xs = [np.random.default_rng(100 + r).normal(size=(rows[r], D)).astype(np.float32)
+          for r in range(2)]
+    nb = max(-(-n // mb) for n in rows)
+    union = [torch.from_numpy(np.concatenate([x[j * mb:(j + 1) * mb] for x in xs]))
+             for j in range(nb)]
+    torch.manual_seed(7)
+    r = RND(D, D, device="cpu")         # same (CPU-drawn) initial weights as the ranks
+    r.update_pred(union)
+    ref = r.pred_net.state_dict()
+    worst = 0.0
+    for key in ref:
+        np.testing.assert_array_equal(outs[0][key], outs[1][key], err_msg=key)
+        worst = max(worst, float(np.abs(outs[0][key] - ref[key].numpy()).max()))
+    print(f"max |2-rank GPU predictor - CPU union| {worst:.2e}")
+    assert worst <= 5e-6, worst
+
+
+def _dpx_fail_worker(rank, world, port, mb, nb, k, out_dir, persistent):
+    sys.path[:0] = PATHS
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      PRL_DP_PERSISTENT="1" if persistent else "0")
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import prl_native
+        torch.cuda.set_device(0)
+        p = _make_ppo(mb, k)
+        S, A, R, D = _shard(rank, mb, nb)
+        if rank == 1:
+            S, A, R, D = (x[:-mb] for x in (S, A, R, D))
+        data = [torch.from_numpy(x).cuda() for x in (S, A, R, D)]
+        p.memory.push_device(*data)
+        p.learn()                                   # healthy launch (default wait limit)
+        paths = [str(p.last_update_path)]
+        if persistent:   # second learn: rank 1 launches 2 s late, the wait limit is ~ms
+            prl_native.dp_set_spin_limit(1 << 12)
+            os.environ["PRL_DP_TEST_DELAY"] = "1:2.0"
+        p.memory.push_device(*data)
+        p.learn()
+        os.environ.pop("PRL_DP_TEST_DELAY", None)
+        prl_native.dp_set_spin_limit(0)
+        paths.append(str(p.last_update_path))
+        torch.cuda.synchronize()
+        sd = {kk: v.cpu().numpy() for kk, v in p.policy.state_dict().items()}
+        np.savez(os.path.join(out_dir, f"{'dpx' if persistent else 'st'}{rank}.npz"), **sd,
+                 _paths=np.array(paths), _fallbacks=np.int64(getattr(p._engine, "dp_fallbacks", 0)),
+                 _step=np.float32(p._engine.step.item()))
+        p._engine.close()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_dpx_timeout_restores_and_falls_back_to_stepped_loop(tmp_path):
+    """The data-parallel persistent launch when a peer is late:
+    the cross-rank wait limit lowered to ~ms (prl_dp_set_spin_limit) and rank 1 launching 2 s
+    after rank 0.  Rank 0's wait times out; rank 1 then waits on rank 0's next step and times
+    out too.  Every rank gathers (status, checksum) in one collective, restores the pre-launch
+    parameters / moments / step count and re-runs the update on the stepped loop.  Checked:
+    no hang, one fallback on each rank, the path recorded as the stepped one, both ranks
+    bit-identical, the AdamW step count continuous, and the result equal to two learns on the
+    stepped loop alone in function space (learn 1 ran persistent; the two forms sum the clip norm
+    in different orders)."""
+    import copy
+    import random
+    import types
+    mb, nb, k = 64, 5, 3
+    port = 29860 + random.randint(0, 30)
+    mp.spawn(_dpx_fail_worker, args=(2, port, mb, nb, k, str(tmp_path), True), nprocs=2, join=True)
+    mp.spawn(_dpx_fail_worker, args=(2, port + 40, mb, nb, k, str(tmp_path), False), nprocs=2,
+             join=True)
+    outs = [np.load(os.path.join(tmp_path, f"dpx{r}.npz")) for r in range(2)]
+    ref = np.load(os.path.join(tmp_path, "st0.npz"))
+    assert [str(x) for x in outs[0]["_paths"]] == ["fused-dp-persistent", "fused-dp"]
+    assert [str(x) for x in ref["_paths"]] == ["fused-dp", "fused-dp"]
+    assert int(outs[0]["_fallbacks"]) == 1 and int(outs[1]["_fallbacks"]) == 1
+    assert float(outs[0]["_step"]) == float(ref["_step"]) == 2 * k * nb
+    keys = [kk for kk in outs[0].files if not kk.startswith("_")]
+    for key in keys:
+        np.testing.assert_array_equal(outs[0][key], outs[1][key], err_msg=key)
+    p = _make_ppo(mb, k)
+    q1 = types.SimpleNamespace(policy=copy.deepcopy(p.policy))
+    q2 = types.SimpleNamespace(policy=copy.deepcopy(p.policy))
+    q1.policy.load_state_dict({kk: torch.from_numpy(outs[0][kk]) for kk in keys})
+    q2.policy.load_state_dict({kk: torch.from_numpy(ref[kk]) for kk in keys})
+    S, A, _, _ = _shard(0, mb, nb)
+    from test_engine_gpu import _outputs
+    (l1, v1), (l2, v2) = (_outputs(q, torch.from_numpy(S[:256]).cuda(),
+                                   torch.from_numpy(A[:256]).cuda()) for q in (q1, q2))
+    assert float((l1 - l2).abs().max()) <= 1e-4 and float((v1 - v2).abs().max()) <= 1e-4

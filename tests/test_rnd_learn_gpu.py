@@ -8,9 +8,14 @@ Checked, from the same initial policy / RND weights and the same memory:
   * the normalised advantages (HIP prl_adv_normalize)       1e-5 relative (+1e-6 absolute guard)
   * the predictor after update_pred (PyTorch + HIP GN/colsum backward) and the updated policy
     (fused engine or graphed per-step path): absolute tolerances per case below.
-The C5-shaped cases (D = 348, A = 17, continuous) run the graphed per-step path (the fused engine
-covers D <= 64); learn_rnd_big's mini_batch of 16,384 puts the policy's and the predictor's
-Linear backward on the split-K + colsum path (layers.SPLIT_MIN_ROWS).
+The C5-shaped cases (D = 348, A = 17, continuous) run outside the persistent engine (it covers
+D <= 64).  Path "wide" is the product default for them (use_fused = True): every optimizer step's
+forward + loss + backward is the wide HIP kernel (prl_ppo_wide_grad; csrc/prl_ppo_wide.hip),
+including the ragged last minibatch and learns too short to capture a graph.  Path "graph"
+(use_fused = False) is the PyTorch autograd step, kept as a second witness.  learn_rnd_big's
+mini_batch of 16,384 puts the autograd path's Linear backward on the split-K + colsum path
+(layers.SPLIT_MIN_ROWS); learn_rnd_c5mb is C5's own mini_batch (65,536 rows) with a ragged second
+minibatch and two epochs.
 """
 import os
 import sys
@@ -33,7 +38,8 @@ pytestmark = pytest.mark.gpu
 # (mini_batch 16,384: 17-dim Gaussian log-probs of random actions reach |logp| ~ 1e2, whose float32
 # rounding alone moves each ratio by ~1e-5) measured 2.5e-5 on the policy after its
 # 2 steps (1.2 % of the 2e-3 the steps move a weight) and 8.6e-7 on the predictor: 5e-5 / 5e-6.
-WEIGHT_ATOL = {"learn_rnd": (2e-6, 2e-6), "learn_rnd_c5": (1e-5, 5e-6), "learn_rnd_big": (5e-5, 5e-6)}
+WEIGHT_ATOL = {"learn_rnd": (2e-6, 2e-6), "learn_rnd_c5": (1e-5, 5e-6), "learn_rnd_big": (5e-5, 5e-6),
+               "learn_rnd_c5mb": (2e-4, 5e-6)}
 
 
 def _sub(g, prefix):
@@ -59,14 +65,18 @@ def _ppo_from_fixture(g, path):
             policy_clip=0.2, GAE_lambda=0.95, gamma=0.995, batch_size=min(1024, N),
             mini_batch_size=int(g["mb"]), use_RND=True, beta=0.001)
     p.show_progress = False
-    p.use_fused = path == "fused"
+    p.use_fused = path in ("fused", "wide")
     init = _sub(g, "init/")
     p.policy.load_state_dict(init)
     p.policy_old.load_state_dict(init)
     p.rnd.load_state_dict(_sub(g, "rnd_init/"))
     S, A = _inputs(g)
-    for i in range(N):
-        p.memory.push(S[i], A[i] if cont else np.asarray(A[i]), g["R"][i], g["Dn"][i])
+    if N <= 4096:   # the reference's per-transition push (Memory.py:14-24)
+        for i in range(N):
+            p.memory.push(S[i], A[i] if cont else np.asarray(A[i]), g["R"][i], g["Dn"][i])
+    else:
+        p.memory.push_device(*(torch.from_numpy(np.ascontiguousarray(x)).cuda()
+                               for x in (S, A, g["R"], g["Dn"])))
     return p
 
 
@@ -82,10 +92,22 @@ def _max_abs(a, b):
 
 
 @pytest.mark.parametrize("tag,path", [("learn_rnd", "fused"), ("learn_rnd", "graph"),
-                                      ("learn_rnd_c5", "graph"), ("learn_rnd_big", "graph")])
+                                      ("learn_rnd_c5", "wide"), ("learn_rnd_c5", "graph"),
+                                      ("learn_rnd_big", "wide"), ("learn_rnd_big", "graph"),
+                                      ("learn_rnd_c5mb", "wide")])
 def test_learn_with_rnd_matches_reference_learn(golden, tag, path):
     g = golden(tag)
     p = _ppo_from_fixture(g, path)
+    wide_steps = []
+    if path == "wide":   # count the optimizer steps the wide kernel took
+        import prl_native
+        orig_wide = prl_native.ppo_wide_grad
+
+        def counted(*a, **k):
+            wide_steps.append(1)
+            return orig_wide(*a, **k)
+
+        prl_native.ppo_wide_grad = counted
     rec = {}
     orig = p.rnd.compute_intrinsic_reward
 
@@ -95,9 +117,19 @@ def test_learn_with_rnd_matches_reference_learn(golden, tag, path):
         return out
 
     p.rnd.compute_intrinsic_reward = cir
-    p.learn()
-    torch.cuda.synchronize()
-    assert p.last_update_path == path and len(p.memory) == 0
+    try:
+        p.learn()
+        torch.cuda.synchronize()
+    finally:
+        if path == "wide":
+            prl_native.ppo_wide_grad = orig_wide
+    assert len(p.memory) == 0
+    if path == "wide":
+        N, mb = int(g["N"]), int(g["mb"])
+        assert p.last_update_path == "graph" and p._last_graphed.wide is not None
+        assert len(wide_steps) == int(g["k_epochs"]) * -(-N // mb)   # every step, ragged too
+    else:
+        assert p.last_update_path == path
     _close(rec["r_int"].cpu().numpy(), g["r_int"], 1e-5, 1e-9, "intrinsic reward")
     _, _, _, adv, returns = p._last_update_inputs
     _close(returns.cpu().numpy(), g["returns"], 1e-5, 1e-5, "GAE returns")
@@ -121,7 +153,7 @@ def test_load_reference_checkpoint_then_learn(golden, tag):
     the reference's post-learn weights, and a GPU learn() continues from them."""
     g = golden(tag)
     d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"ckpt_{tag}")
-    p = _ppo_from_fixture(g, "fused" if tag == "learn_rnd" else "graph")
+    p = _ppo_from_fixture(g, "fused" if tag == "learn_rnd" else "wide")
     p.load_weights(d)
     for k, v in _sub(g, "final/").items():
         assert torch.equal(p.policy.state_dict()[k].cpu(), v), k

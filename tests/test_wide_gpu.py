@@ -167,3 +167,57 @@ def test_wide_learn_matches_autograd_step_path():
     ev = float((v1 - v0).abs().max()) / (float(v0.abs().max()) + 1.0)
     assert el <= 1e-3 and ev <= 1e-3, (el, ev)
     assert abs(L1 - L0) <= 1e-3 * max(1.0, abs(L0)), (L1, L0)
+
+
+def test_wide_learn_clip02_relational_to_cpu():
+    """The reference's policy_clip = 0.2 on C5's net (D 348, A 17), end to end through learn():
+    ratios crossing 0.8 / 1.2 flip single rows' gradient terms, so two valid float32 paths drift
+    apart (the persistent engine's test (iii), tests/test_engine_gpu.py).  The check is
+    relational: the wide kernel must be (about) as close to the CPU path (PyTorch-CPU autograd +
+    AdamW with the oracle's GAE / surrogate, i.e. the reference's arithmetic) as the GPU
+    autograd step path (PRL_WIDE=0) is."""
+    import os
+    from fake_ops import FakeOps
+    from PPO import PPO
+    from test_engine_gpu import _fdist
+    D, A = 348, 17
+    rng = np.random.default_rng(12)
+    N, mb, k = 3 * 1024 + 200, 1024, 2
+    S = torch.from_numpy((rng.normal(size=(N, D)) * 0.5).astype(np.float32)).cuda()
+    R = torch.from_numpy(rng.normal(1, 0.5, N).astype(np.float32)).cuda()
+    Dn = torch.from_numpy((rng.random(N) < 0.02).astype(np.float32)).cuda()
+    Dn[-1] = 1
+    Aa = _sample(_policy(True, D, A), S)
+
+    def make():
+        torch.manual_seed(0)
+        p = PPO(True, D, A, action_scaling=1.0, lr=3e-4, k_epochs=k, batch_size=64,
+                mini_batch_size=mb, policy_clip=0.2)
+        p.show_progress = False
+        return p
+
+    runs = {}
+    for wide in ("1", "0"):
+        os.environ["PRL_WIDE"] = wide
+        try:
+            p = make()
+            p.memory.push_device(S, Aa, R, Dn)
+            p.learn()
+            torch.cuda.synchronize()
+            assert p.last_update_path == "graph"
+            assert (p._last_graphed.wide is not None) == (wide == "1")
+            runs[wide] = p
+        finally:
+            os.environ.pop("PRL_WIDE", None)
+    c = make()
+    c.policy.cpu()
+    c.policy_old.cpu()
+    c.device = torch.device("cpu")
+    c.optimizer = torch.optim.AdamW(c.policy.parameters(), lr=3e-4)
+    c._ops = FakeOps()
+    c.memory.push_device(S.cpu(), Aa.cpu(), R.cpu(), Dn.cpu())
+    c.learn()
+    data = (S, Aa)
+    d_wc, d_gc = _fdist(runs["1"], c, data), _fdist(runs["0"], c, data)
+    print(f"function distance to the CPU path: wide {d_wc:.2e}, autograd {d_gc:.2e}")
+    assert d_wc <= 2.0 * d_gc + 1e-4, (d_wc, d_gc)
