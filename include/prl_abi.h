@@ -287,6 +287,13 @@ int prl_ppo_wide_grad(const float* params, int32_t D, int32_t A, int32_t discret
                       const float* ret, int64_t N, int64_t mini_batch, const int64_t* cursor,
                       const float* scales, float clip, float vf_coef, float ent_coef, float* grad,
                       float* loss_out, float* part, int64_t part_floats, void* stream);
+/* policy_old.get_evaluate over all N rows for the wide nets (PPO/PPO.py:127-154,
+ * ActorCritic.py:118-146): log_prob into logp_out [N] and the state value into V_out [N], with
+ * exactly prl_ppo_wide_grad's forward and row arithmetic, so the first minibatch of learn() sees
+ * ratio == 1 exactly, as in the reference (one get_evaluate for both).  One launch. */
+int prl_ppo_wide_evaluate(const float* params, int32_t D, int32_t A, int32_t discrete,
+                          const float* S, const float* actions, int64_t N, float* logp_out,
+                          float* V_out, void* stream);
 /* prl_ppo_wide_grad with workgroup 0's s_memrealtime ticks (100 MHz) per tile stage added into
  * prof[8] (stage, trunk, heads, outputs, loss, heads bwd, dW1 + dF, dW0); diagnostics. */
 int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A, int32_t discrete,

@@ -231,6 +231,17 @@ class PPO:
             eng = self._fused_engine()
             if eng is not None:
                 return eng.evaluate(self.policy_old, S, A)
+        if S.is_cuda and self.use_graphs:
+            from .update import wide_info
+            if wide_info(self, S.shape[1]) is not None:
+                # the wide step updates on these rows: its own forward arithmetic here too
+                flat = torch.cat([p.detach().reshape(-1) for p in self.policy_old.parameters()])
+                A2 = (A if A.dim() == 2 else A.reshape(-1, 1)).float().contiguous()
+                logp = torch.empty(S.shape[0], dtype=torch.float32, device=S.device)
+                V = torch.empty_like(logp)
+                prl_native.ppo_wide_evaluate(flat, S.shape[1], self.action_dim,
+                                             not self.is_continuous, S.contiguous(), A2, logp, V)
+                return logp, V
         lps, vs = [], []
         for lo in range(0, S.shape[0], self.eval_chunk):
             lp, v, _ = self.policy_old.get_evaluate(S[lo:lo + self.eval_chunk],

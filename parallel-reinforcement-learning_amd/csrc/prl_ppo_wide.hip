@@ -134,6 +134,8 @@ struct WdArgs {
   int G;
   unsigned long long* prof;   // [8] workgroup 0's s_memrealtime ticks per tile stage (or null)
   float* dh0;              // split form: [mb][64] trunk pre-activation gradients (dW0 kernel input)
+  float* eval_logp;        // evaluate form: [N] log-prob and state value per row
+  float* eval_V;
 };
 
 typedef float wd_v4 __attribute__((ext_vector_type(4)));
@@ -235,7 +237,8 @@ __device__ inline float wd_rmax16(float v) {
 // the order of the per-action sums.  Writes dO[r][0 .. 48) and returns {-min(s1, s2), SmoothL1,
 // H} of row r (every lane of the row).
 __device__ inline void wd_tile_loss(const WdNet& n, const float* Os, const float* Rin, float* dOs,
-                                    float invB, float clip, float vf_coef, float (&lp)[3]) {
+                                    float invB, float clip, float vf_coef, float (&lp)[3],
+                                    float& logp_row, float& v_row) {
   const int t = threadIdx.x, r = t >> 4, c = t & 15;
   const int A = n.A;
   const bool discrete = n.discrete != 0;
@@ -300,6 +303,8 @@ __device__ inline void wd_tile_loss(const WdNet& n, const float* Os, const float
     H = wd_rsum16(hpart);
   }
   const float V = O[vcol];
+  logp_row = logp;
+  v_row = V;
   const float diff = logp - rin[32];
   const float cl = diff < -20.0f ? -20.0f : (diff > 20.0f ? 20.0f : diff);
   const float ratio = wd_exp(cl);
@@ -381,6 +386,7 @@ __device__ inline void wd_rin_load(const WdNet& n, const WdArgs& a, int64_t row0
     if (e < WD_RT * WD_RS && r < rc) {
       const int64_t row = row0 + r;
       if (k < WD_MAXA) v = k < Aw ? a.act[row * Aw + k] : 0.f;
+      else if (a.old_logp == nullptr) v = 0.f;   // evaluate form: actions only
       else if (k == 32) v = a.old_logp[row];
       else if (k == 33) v = a.adv[row];
       else if (k == 34) v = a.ret[row];
@@ -415,6 +421,7 @@ __device__ inline void wd_stage(const WdNet& n, const WdArgs& a, int64_t row0, i
     if (r < rc) {
       const int64_t row = row0 + r;
       if (k < WD_MAXA) v = k < Aw ? a.act[row * Aw + k] : 0.f;
+      else if (a.old_logp == nullptr) v = 0.f;   // evaluate form: actions only
       else if (k == 32) v = a.old_logp[row];
       else if (k == 33) v = a.adv[row];
       else if (k == 34) v = a.ret[row];
@@ -445,7 +452,11 @@ __device__ inline void wd_stage_x(const WdNet& n, const WdArgs& a, int64_t row0,
   }
 }
 
-template <int KSM, bool SPLIT>
+// EVAL: the evaluate form (prl_ppo_wide_evaluate): the same tile forward and row arithmetic over
+// all N rows, writing each row's log-prob and value instead of a gradient — PPO.learn's
+// policy_old pass for the rows the wide step then updates on, so the first minibatch's ratio is
+// exactly 1 (as in the reference, where both come from one get_evaluate).
+template <int KSM, bool SPLIT, bool EVAL = false>
 __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) {
   constexpr int KE = SPLIT ? 1 : KSM / 4;   // 16-column blocks of dW0
   extern __shared__ float4 wd_lds4[];
@@ -474,7 +485,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
   float* Gn = p;
 
   // ---- minibatch of this step
-  const int64_t j = *a.cursor;
+  const int64_t j = EVAL ? 0 : *a.cursor;
   const int64_t row_lo = j * a.mb;
   const int64_t rows = row_lo < a.N ? (a.N - row_lo < a.mb ? a.N - row_lo : a.mb) : 0;
   const float invB = rows > 0 ? (a.scales ? a.scales[j] : 1.0f) / (float)rows : 0.f;
@@ -679,9 +690,14 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
     }
     // ---- per-row loss and dO: row t >> 4, 16 lanes per row
     {
-      float lp[3];
-      wd_tile_loss(n, Os, Rin, dOs, invB, a.clip, a.vf_coef, lp);
-      if ((t & 15) == 0 && (t >> 4) < rc) {
+      float lp[3], logp_r, v_r;
+      wd_tile_loss(n, Os, Rin, dOs, invB, a.clip, a.vf_coef, lp, logp_r, v_r);
+      if (EVAL) {
+        if ((t & 15) == 0 && (t >> 4) < rc) {
+          a.eval_logp[row0 + (t >> 4)] = logp_r;
+          a.eval_V[row0 + (t >> 4)] = v_r;
+        }
+      } else if ((t & 15) == 0 && (t >> 4) < rc) {
         lpacc[0] += (double)lp[0];
         lpacc[1] += (double)lp[1];
         lpacc[2] += (double)lp[2];
@@ -702,6 +718,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
     }
     __syncthreads();   // #5: dOs
     WD_MARK(4)
+    if (EVAL) continue;
     // ---- heads backward (block w): dW2, dG -> GroupNorm bwd -> dZ (to Zs), dgamma / dbeta
 #pragma unroll
     for (int h = 0; h < WD_MAXH; ++h) {
@@ -835,6 +852,7 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
     WD_MARK(7)
   }
 #undef WD_MARK
+  if (EVAL) return;
   if (timer) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) a.prof[i] += tm[i];
@@ -1133,6 +1151,48 @@ extern "C" int prl_ppo_wide_info(int32_t D, int32_t A, int32_t discrete, int64_t
   if (n_params) *n_params = n.P;
   if (part_floats) *part_floats = wd_part_floats(n, mini_batch);
   if (grid) *grid = G;
+  return PRL_OK;
+}
+
+extern "C" int prl_ppo_wide_evaluate(const float* params, int32_t D, int32_t A, int32_t discrete,
+                                     const float* S, const float* actions, int64_t N,
+                                     float* logp_out, float* V_out, void* stream) {
+  WdNet n;
+  PRL_REQUIRE(N >= 0, "prl_ppo_wide_evaluate: N < 0");
+  PRL_REQUIRE(wd_layout(D, A, discrete, n) && wd_ksm(D) > 0,
+              "prl_ppo_wide_evaluate: shape D=%d A=%d outside the wide kernel", D, A);
+  PRL_REQUIRE(params && S && actions && logp_out && V_out, "prl_ppo_wide_evaluate: null pointer");
+  if (N == 0) return PRL_OK;
+  const int KSM = wd_ksm(D);
+  const size_t lds = wd_lds_bytes(n, KSM);
+  PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_wide_evaluate: LDS %zu bytes", lds);
+  WdArgs a{};
+  a.net = n;
+  a.params = params;
+  a.S = S;
+  a.act = actions;
+  a.N = N;
+  a.mb = N;
+  a.G = wd_grid(N);
+  a.eval_logp = logp_out;
+  a.eval_V = V_out;
+  hipStream_t st = as_stream(stream);
+  static unsigned long long lds_set[2] = {0ull, 0ull};   // bit = device ordinal
+  int dev_ord = 0;
+  PRL_HIP_TRY(hipGetDevice(&dev_ord));
+  const unsigned long long dev_bit = 1ull << (dev_ord & 63);
+#define WD_ELAUNCH(K, slot)                                                                       \
+  do {                                                                                         \
+    if (!(lds_set[slot] & dev_bit)) {                                                          \
+      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<K, true, true>), \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));   \
+      lds_set[slot] |= dev_bit;                                                                \
+    }                                                                                          \
+    hipLaunchKernelGGL((ppo_wide_grad_kernel<K, true, true>), dim3(a.G), dim3(WD_THREADS), lds, st, a); \
+  } while (0)
+  if (KSM == 32) WD_ELAUNCH(32, 0); else WD_ELAUNCH(88, 1);
+#undef WD_ELAUNCH
+  PRL_LAUNCH_CHECK("ppo_wide_evaluate");
   return PRL_OK;
 }
 

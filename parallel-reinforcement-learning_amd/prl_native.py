@@ -53,6 +53,7 @@ SIGNATURES = {
                           _F32, _F32, _P, _P, _P, _I64, _P],
     "prl_ppo_wide_grad_prof": [_P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I64, _P, _P,
                                _F32, _F32, _F32, _P, _P, _P, _I64, _P, _P],
+    "prl_ppo_wide_evaluate": [_P, _I32, _I32, _I32, _P, _P, _I64, _P, _P, _P],
     "prl_categorical_fwd": [_P, _P, _I64, _I32, _P, _P, _P],
     "prl_categorical_bwd": [_P, _P, _P, _I64, _I32, _P, _P],
     "prl_ppo_update_info": [_I32, _I32, _I32, _I64, _P, _P, _P],
@@ -454,6 +455,16 @@ def ppo_wide_grad(params, D, A, discrete, S, actions, old_logp, adv, ret, mini_b
         _dev(scales, torch.float32, "scales"), float(clip), float(vf_coef), float(ent_coef),
         _dev(grad, torch.float32, "grad"), _dev(loss_out, torch.float32, "loss_out"),
         _dev(part, torch.float32, "part"), part.numel(), *extra, _stream()), "prl_ppo_wide_grad")
+
+
+def ppo_wide_evaluate(params, D, A, discrete, S, actions, logp, V):
+    """ActorCritic.get_evaluate's log_prob and value over all rows with the wide step's forward
+    arithmetic (prl_ppo_wide_evaluate)."""
+    _check(lib().prl_ppo_wide_evaluate(
+        _dev(params, torch.float32, "params"), int(D), int(A), int(bool(discrete)),
+        _dev(S, torch.float32, "S"), _dev(actions, torch.float32, "actions"), int(S.shape[0]),
+        _dev(logp, torch.float32, "logp"), _dev(V, torch.float32, "V"), _stream()),
+        "prl_ppo_wide_evaluate")
 
 
 def ppo_update(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp, adv,

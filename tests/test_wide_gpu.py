@@ -221,3 +221,38 @@ def test_wide_learn_clip02_relational_to_cpu():
     d_wc, d_gc = _fdist(runs["1"], c, data), _fdist(runs["0"], c, data)
     print(f"function distance to the CPU path: wide {d_wc:.2e}, autograd {d_gc:.2e}")
     assert d_wc <= 2.0 * d_gc + 1e-4, (d_wc, d_gc)
+
+
+@pytest.mark.parametrize("cont,D,A", [(True, 348, 17), (False, 100, 5), (True, 201, 3)])
+def test_wide_evaluate_matches_get_evaluate_and_row_placement(cont, D, A):
+    """prl_ppo_wide_evaluate (learn()'s policy_old pass for the wide nets, PPO.py:127-154) against
+    float64 get_evaluate: log-probs within 2e-6 of max |logp| and values within 2e-6 of max |V|
+    (float32 rounding; the persistent engine's evaluate bar).  Every row's result depends only on
+    that row: the same rows evaluated at other tile positions (a 5-row shift, a ragged count)
+    give the same bits — the wide step's loss uses this same arithmetic on the same rows, so the
+    first minibatch of learn() sees ratio == 1 exactly, as in the reference."""
+    import prl_native
+    pol = _policy(cont, D, A, seed=4)
+    N = 1000
+    S, act, _, _, _ = _rows(pol, cont, N, D, A, 0.0)
+    flat = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
+
+    def ev(lo):
+        Ss, As = S[lo:].contiguous(), act[lo:].contiguous()
+        lp = torch.full((N - lo,), float("nan"), device="cuda")
+        V = torch.full((N - lo,), float("nan"), device="cuda")
+        prl_native.ppo_wide_evaluate(flat, D, A, not cont, Ss, As, lp, V)
+        return lp, V
+
+    lp, V = ev(0)
+    lp5, V5 = ev(5)
+    torch.cuda.synchronize()
+    assert torch.equal(lp[5:], lp5) and torch.equal(V[5:], V5)
+    p64 = copy.deepcopy(pol).cpu().double()
+    with torch.no_grad():
+        l64, v64, _ = p64.get_evaluate(S.cpu().double(), act.cpu().double() if cont else
+                                       act.cpu().double().reshape(-1))
+    el = float((lp.cpu().double() - l64).abs().max()) / (1.0 + float(l64.abs().max()))
+    ev_ = float((V.cpu().double() - v64).abs().max()) / (1.0 + float(v64.abs().max()))
+    print(f"logp {el:.1e}, V {ev_:.1e}")
+    assert el <= 2e-6 and ev_ <= 2e-6, (el, ev_)
