@@ -194,6 +194,7 @@ def test_wide_learn_clip02_relational_to_cpu():
         p = PPO(True, D, A, action_scaling=1.0, lr=3e-4, k_epochs=k, batch_size=64,
                 mini_batch_size=mb, policy_clip=0.2)
         p.show_progress = False
+        p.graph_min_steps = 1        # the autograd arm graph-replays its steps too
         return p
 
     runs = {}
