@@ -183,52 +183,15 @@ def pmc_traffic(n):
     return round(per * n), src
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--num-envs", type=int, default=None, help="per GPU")
-    ap.add_argument("--mb", type=int, default=None)
-    ap.add_argument("--k-epochs", type=int, default=None)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-learn-fixed", action="store_true",
-                    help="skip learn() on the fixed synthetic 2^20 memory (learn_fixed_2p20)")
-    ap.add_argument("--cpu-envs", type=int, default=8192,
-                    help="num_envs of the CPU baseline's sample iteration (~20 s of host work)")
-    ap.add_argument("--no-env-scale", action="store_true",
-                    help="skip the rollout-step kernel's 2^22-env re-timing (roofline_env.at_scale)")
-    ap.add_argument("--dist-backend", default="nccl",
-                    help="nccl (= RCCL on ROCm, the measured configuration) or gloo (rehearsal of "
-                         "the multi-rank path with several ranks on one GPU)")
-    ap.add_argument("--dump-gae", default=None,
-                    help="save the roofline GAE launch's inputs (torch.save) for PMC passes")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev_index = local % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(dev_index)
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
-        else:
-            dist.init_process_group(args.dist_backend)
-
+def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
+    """K timed AsyncPPO iterations of one configuration (after `warmup` untimed ones) and the
+    roofline re-timings of its kernels.  Returns the measured record (whole-job numbers are
+    max / sum over ranks)."""
     from AsyncTools.AsyncPPO import AsyncPPO
     from AsyncTools.envs import make
     import prl_native
     from PPO import PPO
 
-    cfg = dict(CONFIGS[args.config])
-    if args.num_envs:
-        cfg["num_envs"] = args.num_envs
-    if args.mb:
-        cfg["mb"] = args.mb
-    if args.k_epochs:
-        cfg["k_epochs"] = args.k_epochs
     spec = make(cfg["env"])
     torch.manual_seed(1234)
     ppo = PPO(is_continuous=cfg["cont"], observ_dim=spec.obs_dim, action_dim=spec.act_dim,
@@ -246,7 +209,8 @@ def main():
         setattr(ppo._ops, name, getattr(prl_native, name))
     ppo._ops.gae = gae_call
     # ... and the RND forward's (RND.compute_intrinsic_reward calls prl_native.rnd_forward)
-    rnd_call = LastCall(prl_native.rnd_forward)
+    rnd_plain = prl_native.rnd_forward
+    rnd_call = LastCall(rnd_plain)
     prl_native.rnd_forward = rnd_call
 
     def iteration():
@@ -259,7 +223,7 @@ def main():
         t2 = time.perf_counter()
         return n, t1 - t0, t2 - t1, runner.last_vector_steps
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         iteration()
     # the update engine's launches inside the timed region, timed with HIP events on its stream
     eng = ppo._fused_engine() if getattr(ppo, "use_fused", False) else None
@@ -270,11 +234,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    recs = [iteration() for _ in range(args.steps)]
+    recs = [iteration() for _ in range(steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    prl_native.rnd_forward = rnd_plain
 
     n_local = float(sum(r[0] for r in recs))
     roll_t = float(sum(r[1] for r in recs))
@@ -292,7 +257,6 @@ def main():
         roll_max, learn_per_tr = float(mx[2]), float(mx[4])
     else:
         total_n, roll_max, learn_per_tr = n_local, roll_t, learn_t / max(n_local, 1)
-
     roofline = None
     if eng is not None and eng.events:
         torch.cuda.synchronize()
@@ -359,10 +323,10 @@ def main():
         cold_med, cold_min = time_kernel(lambda: prl_native.gae(*a, **k), cold=True)
         warm_med, _ = time_kernel(lambda: prl_native.gae(*a, **k), cold=False)
         achieved = GAE_BYTES_PER_TRANSITION * n_gae / (cold_med * 1e-3) / 1e9
-        if args.dump_gae and rank == 0:
+        if dump_gae and rank == 0:
             torch.save({"r": a[0].cpu(), "d": a[1].cpu(), "V": a[2].cpu(),
                         "next_value": None if a[3] is None else a[3].cpu(),
-                        "gamma": a[4], "lam": a[5]}, args.dump_gae)
+                        "gamma": a[4], "lam": a[5]}, dump_gae)
         traffic, traffic_src = pmc_traffic(n_gae)
         roofline_gae = {"kernel": "prl_gae: gae_kernel<true> (single-pass segmented GAE scan)",
                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -418,13 +382,100 @@ def main():
                         "cache": "cold (512 MiB read-only flush)",
                         "warm_launch_us": round(env_warm * 1e3, 2),
                         "envs_per_launch": E, "bytes_per_env_step": bpe}
-        if not args.no_env_scale:
+        if env_scale:
             roofline_env["at_scale"] = env_at_scale(cfg["env"], spec_, scaling, bpe)
+
+    out = {"value": round(total_n / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 2),
+           "steps": steps, "warmup": warmup, "elapsed_s": elapsed, "total_n": total_n,
+           "rollout_env_steps_per_s": round(total_n / max(roll_max, 1e-9), 1),
+           "learn_ms_per_1M": round(learn_per_tr * (1 << 20) * 1e3, 1),
+           "transitions_per_step": round(total_n / steps, 1),
+           "vector_steps_per_rollout": vec_steps,
+           "roofline": roofline, "roofline_gae": roofline_gae, "roofline_env": roofline_env,
+           "roofline_rnd": roofline_rnd}
+    if eng is not None:
+        eng.events = None     # release the HIP events before interpreter teardown
+        eng.close()           # the engine's own RCCL communicator / slice buffers (world > 1)
+    return out, spec
+
+
+def workload(name, cfg):
+    return (f"{name}: {cfg['env']} num_envs={cfg['num_envs']}/GPU, one episode per env per "
+            f"iteration, learn() batch>={cfg['batch_size']} gamma=0.995 GAE_lambda=0.95 "
+            f"k_epochs={cfg['k_epochs']} mini_batch={cfg['mb']}" + (" use_RND" if cfg["rnd"] else ""))
+
+
+# the other per-GPU configurations, timed briefly after the headline (rank 0, one GPU):
+# SURVEY.md 8d's second C2 row (mini_batch 65,536) and BASELINE.json configs[2] / configs[4]
+SUBCONFIGS = (("c2_mb65536", "c2", {"mb": 65536}), ("c3", "c3", {}), ("c5", "c5", {}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--num-envs", type=int, default=None, help="per GPU")
+    ap.add_argument("--mb", type=int, default=None)
+    ap.add_argument("--k-epochs", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-learn-fixed", action="store_true",
+                    help="skip learn() on the fixed synthetic 2^20 memory (learn_fixed_2p20)")
+    ap.add_argument("--no-subconfigs", action="store_true",
+                    help="skip the short c2_mb65536 / c3 / c5 sub-records after the headline")
+    ap.add_argument("--sub-steps", type=int, default=2, help="timed steps of each sub-record")
+    ap.add_argument("--cpu-envs", type=int, default=8192,
+                    help="num_envs of the CPU baseline's sample iteration (~20 s of host work)")
+    ap.add_argument("--no-env-scale", action="store_true",
+                    help="skip the rollout-step kernel's 2^22-env re-timing (roofline_env.at_scale)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL on ROCm, the measured configuration) or gloo (rehearsal of "
+                         "the multi-rank path with several ranks on one GPU)")
+    ap.add_argument("--dump-gae", default=None,
+                    help="save the roofline GAE launch's inputs (torch.save) for PMC passes")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev_index = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(args.dist_backend)
+
+    cfg = dict(CONFIGS[args.config])
+    if args.num_envs:
+        cfg["num_envs"] = args.num_envs
+    if args.mb:
+        cfg["mb"] = args.mb
+    if args.k_epochs:
+        cfg["k_epochs"] = args.k_epochs
+    res, spec = run_config(args, cfg, args.steps, args.warmup, world, rank,
+                           env_scale=not args.no_env_scale, dump_gae=args.dump_gae)
+    total_n = res["total_n"]
 
     fixed = None
     if rank == 0 and world == 1 and args.config == "c2" and not args.no_learn_fixed:
         fixed = learn_fixed(spec, cfg)
 
+    subs = None
+    if rank == 0 and world == 1 and args.config == "c2" and not args.no_subconfigs:
+        import gc
+        subs = {}
+        for name, base, over in SUBCONFIGS:
+            gc.collect()
+            torch.cuda.empty_cache()
+            scfg = dict(CONFIGS[base])
+            scfg.update(over)
+            r, _ = run_config(args, scfg, args.sub_steps, 1, 1, 0, env_scale=False)
+            r.pop("elapsed_s")
+            r.pop("total_n")
+            r["workload"] = workload(base, scfg)
+            subs[name] = r
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["env"] == "CartPole-v1":
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -453,34 +504,24 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(total_n / elapsed, 1), "unit": "env-steps/s",
+            "metric": METRIC, "value": res["value"], "unit": "env-steps/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "ms_per_step": res["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"{args.config}: {cfg['env']} num_envs={cfg['num_envs']}/GPU, "
-                                   f"one episode per env per iteration, learn() batch>="
-                                   f"{cfg['batch_size']} gamma=0.995 GAE_lambda=0.95 "
-                                   f"k_epochs={cfg['k_epochs']} mini_batch={cfg['mb']}"
-                                   + (" use_RND" if cfg["rnd"] else ""),
+            "config": {"workload": workload(args.config, cfg),
                        "env": cfg["env"], "num_envs_per_gpu": cfg["num_envs"],
                        "global_num_envs": cfg["num_envs"] * world,
                        "mini_batch_size": cfg["mb"], "k_epochs": cfg["k_epochs"],
                        "parallelism": f"dp{world}"},
-            "rollout_env_steps_per_s": round(total_n / max(roll_max, 1e-9), 1),
-            "learn_ms_per_1M": round(learn_per_tr * (1 << 20) * 1e3, 1),
-            "transitions_per_step": round(total_n / args.steps, 1),
-            "vector_steps_per_rollout": vec_steps,
-            "roofline": roofline,
-            "roofline_gae": roofline_gae,
-            "roofline_env": roofline_env,
-            "roofline_rnd": roofline_rnd,
-            "learn_fixed_2p20": fixed,
-            "cpu_baseline": cpu,
         }
+        for k in ("rollout_env_steps_per_s", "learn_ms_per_1M", "transitions_per_step",
+                  "vector_steps_per_rollout", "roofline", "roofline_gae", "roofline_env",
+                  "roofline_rnd"):
+            out[k] = res[k]
+        out["learn_fixed_2p20"] = fixed
+        out["subconfigs"] = subs
+        out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
-    if eng is not None:
-        eng.events = None     # release the HIP events before interpreter teardown
-        eng.close()           # the engine's own RCCL communicator (world > 1)
     if world > 1:
         dist.destroy_process_group()
 
