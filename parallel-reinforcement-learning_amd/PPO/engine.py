@@ -122,6 +122,10 @@ class FusedUpdate:
         out = {name: round(p[i] * 0.01 / steps, 2) for i, name in enumerate(self.PHASES)}
         out["chunk"] = {name: round(p[8 + i] * 0.01 / steps, 2)
                         for i, name in enumerate(self.CHUNK_STAGES)}
+        # sub-phase marks (time since the phase began): phase B's partial loads landed, its
+        # slice stores issued; phase C's gradient loads landed
+        out["sub"] = {name: round(p[16 + i] * 0.01 / steps, 2) for i, name in
+                      enumerate(("B: partials landed", "B: slice stored", "C: gradient landed"))}
         if p[30] > 0:
             out["shader_clock_GHz"] = round(p[31] / (p[30] * 10.0), 3)
         return out

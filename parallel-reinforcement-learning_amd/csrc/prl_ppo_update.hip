@@ -189,16 +189,24 @@ __device__ inline float4 ld4_sc1(__amdgpu_buffer_rsrc_t rs, size_t float_off) {
 __device__ inline void st4_sc1(__amdgpu_buffer_rsrc_t rs, size_t float_off, float4 x) {
   st4_aux<UPD_AUX_SC1>(rs, float_off, x);
 }
+// Hand-off words (counters, status, flags) are addressed through the GLOBAL address space:
+// without it, kernels whose pointers pass through private memory (the runtime-layout kernel)
+// lowered them to flat_ atomics / loads, which the guide's hand-off table does not cover
+// (tests/test_host_cpu.py::test_handoff_isa checks the built code object).
+template <class T>
+__device__ inline __attribute__((address_space(1))) T* upd_g(T* p) {
+  return (__attribute__((address_space(1))) T*)(p);
+}
 __device__ inline float ld_sc1f(const float* p) {
-  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+  return __uint_as_float(__hip_atomic_load(upd_g(reinterpret_cast<const unsigned*>(p)), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT));
 }
 __device__ inline void st_sc1f(float* p, float x) {
-  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(x), __ATOMIC_RELAXED,
+  __hip_atomic_store(upd_g(reinterpret_cast<unsigned*>(p)), __float_as_uint(x), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ inline unsigned ld_sc1u(const unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(upd_g(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // 8-way sharded arrival counters (shard k at word 32 (1 + k) of its block, one 128-B line each):
@@ -209,7 +217,7 @@ constexpr int UPD_CTR_A = 32;                              // first shard word o
 constexpr int UPD_CTR_B = UPD_CTR_A + 32 * UPD_SHARDS;     // ... of counter B
 constexpr int UPD_CTR_WORDS = UPD_CTR_B + 32 * UPD_SHARDS;
 __device__ inline void upd_arrive(unsigned* ctr, int base, int g) {
-  __hip_atomic_fetch_add(ctr + base + 32 * (g & (UPD_SHARDS - 1)), 1u, __ATOMIC_RELAXED,
+  __hip_atomic_fetch_add(upd_g(ctr + base + 32 * (g & (UPD_SHARDS - 1))), 1u, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ inline unsigned upd_isum8(unsigned v) {
@@ -229,9 +237,9 @@ __device__ inline bool upd_wait_sharded(unsigned* ctr, int base, unsigned target
     if (ld_sc1u(ctr + 2) != 0u) return false;
     if (spins > UPD_SPIN_LIMIT) {
       if (l == 0) {
-        __hip_atomic_store(ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_or(ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky
+        __hip_atomic_store(upd_g(ctr + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(upd_g(ctr + 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_or(upd_g(ctr + 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky
       }
       return false;
     }
@@ -245,9 +253,9 @@ __device__ inline bool upd_wait(unsigned* ctr, int which, unsigned target) {
     if (ld_sc1u(ctr + which) >= target) return true;
     if (ld_sc1u(ctr + 2) != 0u) return false;
     if (spins > UPD_SPIN_LIMIT) {
-      __hip_atomic_store(ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_or(ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky
+      __hip_atomic_store(upd_g(ctr + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(upd_g(ctr + 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_or(upd_g(ctr + 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -1063,13 +1071,23 @@ __device__ __forceinline__ float adam_loss(const float* grad, int Lp, float inv_
   return lp.x * inv_count + vf_coef * (lp.y * inv_count) - ent_coef * (lp.z * inv_count);
 }
 
+// Diagnostic sub-phase marks (PRL_UPD_PROFILE=1, workgroup 0, thread 0): time since the
+// current phase began (pts[7]) added into acc[i]; off (null) in normal runs.
+struct UpdSub {
+  unsigned long long* acc;
+  const unsigned long long* ref;
+  __device__ inline void mark(int i) const {
+    if (acc && threadIdx.x == 0) acc[i] += __builtin_amdgcn_s_memrealtime() - *ref;
+  }
+};
+
 // Phase B: workgroup g sums its slice [qlo, qhi) of the gradient quads over the G partials in
 // workgroup order (deterministic) with float64 accumulators (the partials of the output biases
 // cancel across workgroups), publishes the slice (sc1) and returns this thread's share of the
 // slice's sum of squares (parameter quads only).  Uses scratch as [spl][nq] double4.
 __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_red,
                                          int Qtot, int Qp, int g, int G, float* scratch, int NT,
-                                         int aux = UPD_AUX_SC1) {
+                                         int aux = UPD_AUX_SC1, UpdSub sub = UpdSub{nullptr, nullptr}) {
   const int t = threadIdx.x;
   const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
   const int nq = qhi - qlo;
@@ -1093,17 +1111,18 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
     while (spl * 2 * nq <= NT && spl * 2 <= G) spl *= 2;
     double* red = reinterpret_cast<double*>(scratch);   // [spl][nq][4]
     if (t < spl * nq) {
-      const int qi = t % nq, sub = t / nq;
+      const int qi = t % nq, sub_ = t / nq;
       double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
-      upd_sum_partials(rs_part, Qtot, qlo + qi, sub, spl, G, ax, ay, az, aw);
-      double* o = red + 4 * (sub * nq + qi);
+      upd_sum_partials(rs_part, Qtot, qlo + qi, sub_, spl, G, ax, ay, az, aw);
+      double* o = red + 4 * (sub_ * nq + qi);
       o[0] = ax; o[1] = ay; o[2] = az; o[3] = aw;
     }
+    sub.mark(0);   // thread 0's partial loads landed and summed
     __syncthreads();
     if (t < nq) {
       double ax = red[4 * t], ay = red[4 * t + 1], az = red[4 * t + 2], aw = red[4 * t + 3];
-      for (int sub = 1; sub < spl; ++sub) {
-        const double* o = red + 4 * (sub * nq + t);
+      for (int k = 1; k < spl; ++k) {
+        const double* o = red + 4 * (k * nq + t);
         ax += o[0]; ay += o[1]; az += o[2]; aw += o[3];
       }
       fin(t, ax, ay, az, aw);
@@ -1125,7 +1144,7 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
                                    int g, int G, unsigned long long gstep, int par, int* s_abort) {
   const int t = threadIdx.x, NT = blockDim.x;
   const unsigned long long want = gstep + 1ull;
-  if (t == 0) __hip_atomic_store(args.xflag_self + g, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t == 0) __hip_atomic_store(upd_g(args.xflag_self + g), want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (t < 64) {
     unsigned long long* fl = args.xflag[0];   // lane r polls rank r (selected, not indexed)
 #pragma unroll
@@ -1134,14 +1153,14 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
     bool ok = true;
     for (unsigned spins = 0;; ++spins) {
       const bool ready = t >= args.world ||
-                         __hip_atomic_load(fl + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= want;
+                         __hip_atomic_load(upd_g(fl + g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= want;
       if (__ballot(!ready) == 0ull) break;
       if (ld_sc1u(args.ctr + 2) != 0u) { ok = false; break; }
       if (spins > args.dp_spin_limit) {
         if (t == 0) {
-          __hip_atomic_store(args.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(args.ctr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_or(args.ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(upd_g(args.ctr + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(upd_g(args.ctr + 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_or(upd_g(args.ctr + 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         ok = false;
         break;
@@ -1224,6 +1243,8 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     pts[8] = pts[7];
     pts[9] = __builtin_amdgcn_s_memtime();
   }
+  const UpdSub subm{(args.profile && g == 0) ? reinterpret_cast<unsigned long long*>(hdr + 16) + 8
+                                              : nullptr, pts + 7};
   auto mark = [&](int i) {
     if (args.profile && g == 0 && t == 0) {
       const unsigned long long now = __builtin_amdgcn_s_memrealtime();
@@ -1299,7 +1320,8 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       const unsigned long long gstep = args.dp_seq0 + (unsigned long long)s;
       const int par = (int)(gstep & 1ull);
       (void)upd_slice_reduce(rs_part, dp ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
-                             Qtot, Qp, g, G, scratch, NT, dp ? UPD_AUX_SYS : UPD_AUX_SC1);
+                             Qtot, Qp, g, G, scratch, NT, dp ? UPD_AUX_SYS : UPD_AUX_SC1, subm);
+      subm.mark(1);   // slice combined, its stores issued
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (dp && !upd_dp_union_slice(args, rs_red, Qtot, g, G, gstep, par, s_abort)) return;
@@ -1332,6 +1354,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
 #pragma unroll
       for (int i = 0; i < NQ; ++i)
         if (t + i * NT < Qp) acc += (gq[i].x * gq[i].x + gq[i].y * gq[i].y) + (gq[i].z * gq[i].z + gq[i].w * gq[i].w);
+      subm.mark(2);   // thread 0's gradient quads landed
       acc = wave_sum_f32_to63(acc);
       float* s_nrm = hdr + 4;   // [NW]
       if ((t & 63) == 63) s_nrm[t >> 6] = acc;
@@ -1601,7 +1624,7 @@ __device__ __forceinline__ void ppo_grad_body(const UpdNet& n, const UpdArgs& ar
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
-    __hip_atomic_fetch_add(args.ctr + 0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(upd_g(args.ctr + 0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *s_abort = upd_wait(args.ctr, 0, args.grad_target) ? 0 : 1;
   }
   __syncthreads();
