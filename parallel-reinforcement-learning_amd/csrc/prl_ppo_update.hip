@@ -597,12 +597,15 @@ struct UpdFwd {
 };
 template <int KA>
 constexpr int upd_ksm() { return KA > 0 ? 4 : 16; }
-// Waves per workgroup: the two-head discrete specialisation (CartPole) runs 8 waves, wave
-// w = (head group w >> 2, channel block w & 3): twice the waves per SIMD to hide latency and
-// half of every per-wave MFMA chain.  Three heads (Pendulum) and the generic kernel run 4 waves
-// (wave w = channel block w, all heads) to stay inside the LDS.
+// Waves per workgroup.  KD = 2 is the persistent engine's two-head discrete specialisation
+// (CartPole, used by prl_ppo_update / _dpx): 8 waves, wave w = (head group w >> 2, channel block
+// w & 3) — two waves per SIMD hide each other's MFMA / LDS latency and every per-wave chain is
+// half as long (round 3, tools/engine_profile.py: 15.65 -> 15.02 us per step at mb 512,
+// 140.1 -> 120.2 us at mb 65,536; the moments then take 5 quads per thread).  KD = 1 (the same
+// net; the stepped and evaluate kernels), the three-head nets (Pendulum) and the generic kernel
+// run 4 waves (wave w = channel block w, all heads) to stay inside the LDS.
 template <int KD, int KA>
-constexpr int upd_nw() { return (KD == 1 && KA == 2 && false) ? 8 : 4; }   // 8 waves measured slower: off
+constexpr int upd_nw() { return (KD == 2 && KA == 2) ? 8 : 4; }
 template <int NW>
 constexpr int upd_hpw() { return NW == 8 ? 1 : UPD_MAXH; }
 // global head of the wave's local head slot hs
@@ -1356,7 +1359,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
         if (t + i * NT < Qp) acc += (gq[i].x * gq[i].x + gq[i].y * gq[i].y) + (gq[i].z * gq[i].z + gq[i].w * gq[i].w);
       subm.mark(2);   // thread 0's gradient quads landed
       acc = wave_sum_f32_to63(acc);
-      float* s_nrm = hdr + 4;   // [NW]
+      float* s_nrm = hdr + 96;  // [NW <= 16] (hdr + 8 / + 10 hold s_abort / s_adam)
       if ((t & 63) == 63) s_nrm[t >> 6] = acc;
       __syncthreads();
       float tot = 0.f;
@@ -1718,9 +1721,23 @@ using namespace prl;
 namespace {
 
 // waves per workgroup of the kernels chosen for this shape (upd_nw<KD, KA>() on the device)
-int upd_nw_host(const UpdNet& n) { (void)n; return 4; }
-int upd_nt(const UpdNet& n) { return 64 * upd_nw_host(n); }
-int upd_nq(const UpdNet& n) { return (int)cdiv(n.Lp / 4, upd_nt(n)); }
+bool upd_force_generic();
+// PRL_UPD_WAVES=4 keeps the persistent CartPole engine at 4 waves (A/B, diagnostics)
+bool upd_waves8_enabled() {
+  static const int v = [] {
+    const char* e = getenv("PRL_UPD_WAVES");
+    return (e && e[0] == '4') ? 0 : 1;
+  }();
+  return v != 0;
+}
+bool upd_is_cartpole(const UpdNet& n) { return n.discrete && n.A == 2 && n.D == 4; }
+// waves of the kernel that runs this shape: the persistent kernels (update, data-parallel
+// update) or the others (evaluate, stepped gradient, AdamW)
+int upd_nw_host(const UpdNet& n, bool persistent) {
+  return (persistent && upd_is_cartpole(n) && !upd_force_generic() && upd_waves8_enabled()) ? 8 : 4;
+}
+int upd_nt(const UpdNet& n, bool persistent = false) { return 64 * upd_nw_host(n, persistent); }
+int upd_nq(const UpdNet& n) { return (int)cdiv(n.Lp / 4, upd_nt(n, true)); }
 // Specialisations for the configs' shapes (CartPole: discrete, A = 2; Pendulum: continuous,
 // A = 1); every other shape runs the generic (runtime head configuration) kernel.
 // PRL_UPD_PROFILE=1: the engine records workgroup 0's per-phase times (FusedUpdate.profile)
@@ -1737,14 +1754,16 @@ const void* upd_kernel_for(const UpdNet& n, bool dp = false) {
   if (dp) {
     const int nq = upd_nq(n);
     if (upd_force_generic()) return nq <= 20 ? reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0, true>) : nullptr;
-    if (n.discrete && n.A == 2 && n.D == 4 && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4, true>);
+    if (upd_is_cartpole(n) && nq <= 5) return reinterpret_cast<const void*>(ppo_update_kernel<5, 2, 2, 4, true>);
+    if (upd_is_cartpole(n) && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4, true>);
     if (!n.discrete && n.A == 1 && n.D == 3 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3, true>);
     if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0, true>);
     return nullptr;
   }
   const int nq = upd_nq(n);
   if (upd_force_generic()) return nq <= 20 ? reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0>) : nullptr;
-  if (n.discrete && n.A == 2 && n.D == 4 && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4>);
+  if (upd_is_cartpole(n) && nq <= 5) return reinterpret_cast<const void*>(ppo_update_kernel<5, 2, 2, 4>);
+  if (upd_is_cartpole(n) && nq <= 10) return reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4>);
   if (!n.discrete && n.A == 1 && n.D == 3 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3>);
   if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0>);
   return nullptr;
@@ -1781,8 +1800,8 @@ hipError_t upd_launch_resident(const void* kern, int G, int threads, size_t lds,
   return hipLaunchKernel(kern, dim3(G), dim3(threads), kargs, lds, st);
 }
 
-size_t upd_lds_bytes(const UpdNet& n) {
-  return sizeof(float) * (size_t)(UPD_HDR + 2 * n.Lp + 4 + ((upd_scratch_floats(n.D, upd_nw_host(n), upd_ts(n)) + 3) & ~3));
+size_t upd_lds_bytes(const UpdNet& n, bool persistent) {
+  return sizeof(float) * (size_t)(UPD_HDR + 2 * n.Lp + 4 + ((upd_scratch_floats(n.D, upd_nw_host(n, persistent), upd_ts(n)) + 3) & ~3));
 }
 
 struct UpdWs {
@@ -1828,7 +1847,7 @@ extern "C" int prl_ppo_update_info(int32_t D, int32_t A, int32_t discrete, int64
   if (n_params) *n_params = n.P;
   if (workspace_bytes) *workspace_bytes = (int64_t)upd_ws_carve(n, G, nullptr, nullptr);
   if (grid) *grid = G;
-  return (upd_lds_bytes(n) <= 160 * 1024 && upd_kernel_for(n)) ? PRL_OK : PRL_ERR_ARG;
+  return (upd_lds_bytes(n, true) <= 160 * 1024 && upd_kernel_for(n)) ? PRL_OK : PRL_ERR_ARG;
 }
 
 namespace {
@@ -1919,7 +1938,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     args.xbuf_self = args.xbuf[dp->rank];
     args.xflag_self = args.xflag[dp->rank];
   }
-  const size_t lds = upd_lds_bytes(args.net);
+  const size_t lds = upd_lds_bytes(args.net, true);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_update: %zu B of LDS needed", lds);
   hipStream_t st = as_stream(stream);
   const void* kern = upd_kernel_for(args.net, dp != nullptr);
@@ -1932,7 +1951,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   hipLaunchKernelGGL(ppo_image_kernel, dim3(img_grid), dim3(UPD_THREADS), 0, st, args.net, params,
                      exp_avg, exp_avg_sq, img_p, img_m, img_v, 1);
   PRL_LAUNCH_CHECK("ppo_image");
-  PRL_HIP_TRY(upd_launch_resident(kern, G, upd_nt(args.net), lds, kargs, st));
+  PRL_HIP_TRY(upd_launch_resident(kern, G, upd_nt(args.net, true), lds, kargs, st));
   hipLaunchKernelGGL(ppo_image_kernel, dim3(img_grid), dim3(UPD_THREADS), 0, st, args.net, params,
                      exp_avg, exp_avg_sq, img_p, img_m, img_v, 0);
   PRL_LAUNCH_CHECK("ppo_image");
@@ -2041,7 +2060,7 @@ extern "C" int prl_ppo_evaluate(const float* params, int32_t D, int32_t A, int32
   args.S = S;
   args.act = actions;
   args.N = N;
-  const size_t lds = sizeof(float) * (size_t)(UPD_HDR + args.net.Lp + ((upd_scratch_floats(D, upd_nw_host(args.net), upd_ts(args.net)) + 3) & ~3));
+  const size_t lds = sizeof(float) * (size_t)(UPD_HDR + args.net.Lp + ((upd_scratch_floats(D, upd_nw_host(args.net, false), upd_ts(args.net)) + 3) & ~3));
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_evaluate: %zu B of LDS needed", lds);
   const unsigned grid = (unsigned)std::min<int64_t>(cdiv(N, UPD_RT), 2 * 256);
   const void* kern = upd_eval_kernel_for(args.net);
@@ -2103,7 +2122,7 @@ extern "C" int prl_ppo_grad_step(const float* img_params, int32_t D, int32_t A, 
   args.ctr = ws.ctr;
   args.grad_target = (unsigned)G;
   args.profile = upd_profile_enabled();
-  const size_t lds = upd_lds_bytes(args.net);
+  const size_t lds = upd_lds_bytes(args.net, false);
   hipStream_t st = as_stream(stream);
   const void* kern = upd_grad_kernel_for(args.net);
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2184,7 +2203,7 @@ extern "C" int prl_ppo_grad_fold_step(const float* in_p, const float* in_m, cons
   UpdFold f{grad_prev, in_p, in_m, in_v, out_p, out_m, out_v, (double)step_prev,
             lr, beta1, beta2, eps, weight_decay, max_norm, inv_count_prev, vf_coef, ent_coef,
             loss_out};
-  const size_t lds = upd_lds_bytes(args.net);
+  const size_t lds = upd_lds_bytes(args.net, false);
   hipStream_t st = as_stream(stream);
   const void* kern = upd_grad_kernel_for(args.net);
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2317,7 +2336,7 @@ extern "C" int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, 
   args.vf_coef = vf_coef;
   args.part = ws.part;
   args.ctr = ws.ctr;
-  const size_t lds = upd_lds_bytes(args.net);
+  const size_t lds = upd_lds_bytes(args.net, false);
   hipStream_t st = as_stream(stream);
   const void* kern = upd_grad_kernel_for(args.net);
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
