@@ -186,6 +186,13 @@ __device__ inline void st4_aux(__amdgpu_buffer_rsrc_t rs, size_t float_off, floa
 __device__ inline float4 ld4_sc1(__amdgpu_buffer_rsrc_t rs, size_t float_off) {
   return ld4_aux<UPD_AUX_SC1>(rs, float_off);
 }
+// the same with the per-lane part in the VGPR offset and a wave-uniform part in the SGPR offset
+// (one address register for a whole strided sweep: nothing per load for the compiler to spill)
+__device__ inline float4 ld4_sc1_so(__amdgpu_buffer_rsrc_t rs, unsigned voff_bytes, unsigned soff_bytes) {
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_bytes, soff_bytes, UPD_AUX_SC1);
+  return float4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                __uint_as_float(v.w)};
+}
 __device__ inline void st4_sc1(__amdgpu_buffer_rsrc_t rs, size_t float_off, float4 x) {
   st4_aux<UPD_AUX_SC1>(rs, float_off, x);
 }
@@ -998,19 +1005,21 @@ __device__ inline void f4set(float4& v, int e, float x) {
 }
 
 // sum of quad q over partials gg = first, first + stride, ... < G (in that order), loads issued
-// in batches of 16 so their latencies overlap
+// in batches of NB so their latencies overlap (NB = 8 for the 8-wave kernel: its 256 registers
+// per lane cannot hold 16 quads in flight without spilling around the phase)
+template <int NB = 16>
 __device__ inline void upd_sum_partials(__amdgpu_buffer_rsrc_t rs_part, int Qtot, int q, int first,
                                         int stride, int G, double& ax, double& ay, double& az,
                                         double& aw) {
-  for (int g0 = first; g0 < G; g0 += 16 * stride) {
-    float4 v[16];
+  for (int g0 = first; g0 < G; g0 += NB * stride) {
+    float4 v[NB];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < NB; ++u) {
       const int gg = g0 + u * stride;
       if (gg < G) v[u] = ld4_sc1(rs_part, ((size_t)gg * Qtot + q) * 4);
     }
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < NB; ++u) {
       if (g0 + u * stride < G) {
         ax += v[u].x; ay += v[u].y; az += v[u].z; aw += v[u].w;
       }
@@ -1105,7 +1114,8 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
     // wide slices (few workgroups): each thread owns whole quads, partials summed in order
     for (int qi = t; qi < nq; qi += NT) {
       double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
-      upd_sum_partials(rs_part, Qtot, qlo + qi, 0, 1, G, ax, ay, az, aw);
+      if (NT > 256) upd_sum_partials<8>(rs_part, Qtot, qlo + qi, 0, 1, G, ax, ay, az, aw);
+      else upd_sum_partials<16>(rs_part, Qtot, qlo + qi, 0, 1, G, ax, ay, az, aw);
       fin(qi, ax, ay, az, aw);
     }
   } else if (nq > 0) {
@@ -1116,7 +1126,8 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
     if (t < spl * nq) {
       const int qi = t % nq, sub_ = t / nq;
       double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
-      upd_sum_partials(rs_part, Qtot, qlo + qi, sub_, spl, G, ax, ay, az, aw);
+      if (NT > 256) upd_sum_partials<8>(rs_part, Qtot, qlo + qi, sub_, spl, G, ax, ay, az, aw);
+      else upd_sum_partials<16>(rs_part, Qtot, qlo + qi, sub_, spl, G, ax, ay, az, aw);
       double* o = red + 4 * (sub_ * nq + qi);
       o[0] = ax; o[1] = ay; o[2] = az; o[3] = aw;
     }
@@ -1339,12 +1350,18 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       mark(4);   // wait B
     }
     // ---- phase C: clip_grad_norm_(2.0) + AdamW on every workgroup's own copy ------------------
-    float4 gq[NQ];   // this thread's gradient quads: loads issued first, in flight under the norm
+    // this thread's gradient quads: every load issued at once under a wave-uniform condition (a
+    // per-lane `q < Qp` guard put the last quads under divergent exec masks, and with 8 waves the
+    // compiler then drained each of them to a spill slot before issuing the next: three round
+    // trips instead of one).  Lanes past Qp read the workspace that follows `red` (its loss quad,
+    // then `part`): garbage, masked below.
+    float4 gq[NQ];
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      const int q = t + i * NT;
-      if (q < Qp) gq[i] = ld4_sc1(rs_red, (size_t)q * 4);
-    }
+    for (int i = 0; i < NQ; ++i)
+      if (i * NT < Qp) gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * NT));
+    // 8 waves (two per SIMD, 256 registers each): park the quads in the gradient image, free
+    // since the publish, so they do not stay live across the norm into AdamW
+    constexpr bool PARK = NW == 8;
     float clipc;
     {
       // clip_grad_norm_'s norm from the reduced gradient this workgroup just loaded: per thread
@@ -1355,8 +1372,12 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       // coefficient, run-to-run differences; tools/exp/engine_determinism4.py.)
       float acc = 0.f;
 #pragma unroll
-      for (int i = 0; i < NQ; ++i)
-        if (t + i * NT < Qp) acc += (gq[i].x * gq[i].x + gq[i].y * gq[i].y) + (gq[i].z * gq[i].z + gq[i].w * gq[i].w);
+      for (int i = 0; i < NQ; ++i) {
+        if (i * NT < Qp && t + i * NT < Qp) {
+          acc += (gq[i].x * gq[i].x + gq[i].y * gq[i].y) + (gq[i].z * gq[i].z + gq[i].w * gq[i].w);
+          if (PARK) *reinterpret_cast<float4*>(Ga + 4 * (t + i * NT)) = gq[i];
+        }
+      }
       subm.mark(2);   // thread 0's gradient quads landed
       acc = wave_sum_f32_to63(acc);
       float* s_nrm = hdr + 96;  // [NW <= 16] (hdr + 8 / + 10 hold s_abort / s_adam)
@@ -1389,9 +1410,10 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
           if (i < NQ && q < Qp) {
             float4 pw = *reinterpret_cast<float4*>(W + 4 * q);
             float4 m4 = mreg[i], v4 = vreg[i];
+            const float4 g4 = PARK ? *reinterpret_cast<const float4*>(Ga + 4 * q) : gq[i];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float gr = f4get(gq[i], e) * clipc;
+              const float gr = f4get(g4, e) * clipc;
               float m = f4get(m4, e), v = f4get(v4, e), p = f4get(pw, e);
               // torch AdamW (decoupled decay; lerp for m; addcmul for v) with fused multiply-adds
               p = p * decay;
