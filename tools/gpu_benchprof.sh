@@ -11,7 +11,7 @@ BENCH="bench.py ${BENCH_ARGS:-}"
 step bench 600 python $BENCH --dump-gae /tmp/gae_inputs.pt
 tail -1 $O/bench.log
 N=$(python -c "import torch; print(torch.load('/tmp/gae_inputs.pt', weights_only=True)['V'].numel())")
-step prof_bench 900 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o bench --output-format csv -- python $BENCH --no-cpu-baseline --no-learn-fixed
+step prof_bench 900 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o bench --output-format csv -- python $BENCH --no-cpu-baseline --no-learn-fixed --no-subconfigs
 grep '"metric"' $O/prof_bench.log | tail -1 > $O/bench_under_rocprof.json
 step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o fetch --output-format csv -- python tools/kernel_bench.py --gae-file /tmp/gae_inputs.pt --reps 3
 step pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o write --output-format csv -- python tools/kernel_bench.py --gae-file /tmp/gae_inputs.pt --reps 3
