@@ -369,6 +369,13 @@ int64_t prl_dp_xbuf_bytes(int32_t D, int32_t A, int32_t discrete, int32_t mini_b
  * the ranks).  Per process; returns the previous value.  Tests lower it to exercise the failure
  * path.  No reference counterpart. */
 uint32_t prl_dp_set_spin_limit(uint32_t polls);
+/* Form of prl_ppo_update's persistent kernel: 0 = the latency form (gradient image in LDS,
+ * AdamW moments in registers), 1 = the throughput form whenever a launch has >= 2 steps
+ * (gradient in registers, moments streamed from the workspace), 2 = auto (default: the
+ * throughput form when a workgroup takes >= 2 16-row tiles per step).  Both give the same bits.
+ * Per process (initial value from PRL_UPD_TP); returns the previous mode.  No reference
+ * counterpart (performance knob / tests). */
+int32_t prl_ppo_update_set_tp(int32_t mode);
 int prl_dp_xbuf_alloc(int64_t bytes, void** out);
 int prl_dp_xbuf_free(void* p);
 int prl_dp_ipc_handle(void* p, uint8_t* out, int64_t out_bytes);   /* out: 64 bytes */

@@ -155,6 +155,7 @@ struct UpdArgs {
   unsigned long long* xflag[UPD_MAX_RANKS];   // rank r's [G] per-workgroup step flags
   float* xbuf_self;                       // == xbuf[rank] (no dynamic kernarg indexing)
   unsigned long long* xflag_self;         // == xflag[rank]
+  float *tp_m0, *tp_v0, *tp_m1, *tp_v1;   // the throughput form's moment buffers (image layout)
 };
 
 // ---- sc1 (write-through / L1-bypassing) accessors -------------------------------------------
@@ -358,12 +359,14 @@ struct UpdDist {
   float S2, qa, logp, H;
   int ai;
 };
-// KD: 1 discrete / 0 continuous / -1 runtime;  KA: action dim (0 = runtime).  Specialised
-// kernels keep the per-row code (executed by 16 lanes, but fetched every step) small.
+// KD: 1 discrete / 0 continuous / -1 runtime, 2 / 3 the 8-wave discrete / continuous forms of
+// the persistent kernel (upd_nw);  KA: action dim (0 = runtime).  Specialised kernels keep the
+// per-row code (executed by 16 lanes, but fetched every step) small.
+constexpr bool upd_kd_discrete(int KD) { return KD == 1 || KD == 2; }
 template <int KD, int KA>
 __device__ inline void upd_row_dist(const UpdNet& n, const float* O, const float* act, UpdDist& d) {
   const int A = KA > 0 ? KA : n.A;
-  const bool discrete = KD >= 0 ? (KD != 0) : (n.discrete != 0);
+  const bool discrete = KD >= 0 ? upd_kd_discrete(KD) : (n.discrete != 0);
   d.logp = 0.f;
   d.H = 0.f;
   d.S2 = 0.f;
@@ -427,7 +430,7 @@ template <int KD, int KA>
 __device__ inline void upd_row_loss(const UpdNet& n, const float* O, const float* rin, float invB,
                                     float clip, float vf_coef, float* dO, float (&lp)[3]) {
   const int A = KA > 0 ? KA : n.A;
-  const bool discrete = KD >= 0 ? (KD != 0) : (n.discrete != 0);
+  const bool discrete = KD >= 0 ? upd_kd_discrete(KD) : (n.discrete != 0);
   const int vcol = discrete ? A : 2 * A;      // critic output column
 #pragma unroll
   for (int j = 0; j < UPD_MAXO; ++j) dO[j] = 0.f;
@@ -589,7 +592,7 @@ __device__ inline int upd_bias_of(const UpdNet& n, int j) {
 }
 
 template <int KD>
-__device__ inline int upd_nh(const UpdNet& n) { return KD > 0 ? 2 : (KD == 0 ? 3 : n.nh); }
+__device__ inline int upd_nh(const UpdNet& n) { return KD < 0 ? n.nh : (upd_kd_discrete(KD) ? 2 : 3); }
 
 // Forward state of one tile kept for the backward (wave w's channel block, lane's row x).
 // KSM = compile-time bound on the input k-steps ceil(D / 4) (4 for the specialised kernels);
@@ -612,9 +615,10 @@ constexpr int upd_ksm() { return KA > 0 ? 4 : 16; }
 // net; the stepped and evaluate kernels), the three-head nets (Pendulum) and the generic kernel
 // run 4 waves (wave w = channel block w, all heads) to stay inside the LDS.
 template <int KD, int KA>
-constexpr int upd_nw() { return (KD == 2 && KA == 2) ? 8 : 4; }
-template <int NW>
-constexpr int upd_hpw() { return NW == 8 ? 1 : UPD_MAXH; }
+constexpr int upd_nw() { return ((KD == 2 && KA == 2) || KD == 3) ? 8 : 4; }
+// heads per wave: with 8 waves group 0 takes heads 0 (and 2), group 1 head 1
+template <int KD, int KA>
+constexpr int upd_hpw() { return upd_nw<KD, KA>() == 8 ? (upd_kd_discrete(KD) ? 1 : 2) : UPD_MAXH; }
 // global head of the wave's local head slot hs
 template <int NW>
 __device__ inline int upd_head(int hs, int hg) { return NW == 8 ? hg + 2 * hs : hs; }
@@ -624,12 +628,20 @@ __device__ inline int upd_head(int hs, int hg) { return NW == 8 ? hg + 2 * hs : 
 struct UpdHead {
   int w1, g1, b1, w2, oc, no;
 };
+// Branch-free: head 0's value plus the steps to heads 1 and 2 times (h >= 1), (h >= 2).  (A
+// select chain let the compiler turn a runtime h — the 8-wave kernels' head group — into a
+// lookup table in private memory, i.e. scratch loads on every use.)
 __device__ inline UpdHead upd_head_info(const UpdNet& n, int h) {
-  UpdHead r{n.w1[0].lds, n.g1[0].lds, n.b1[0].lds, n.w2[0].lds, n.ocol[0], n.out[0]};
-#pragma unroll
-  for (int k = 1; k < UPD_MAXH; ++k)
-    if (h == k) r = UpdHead{n.w1[k].lds, n.g1[k].lds, n.b1[k].lds, n.w2[k].lds, n.ocol[k], n.out[k]};
-  return r;
+  if (n.nh == 2) {   // (the two-head nets: one select, as the register budget of their 8-wave kernel has it)
+    return h == 1 ? UpdHead{n.w1[1].lds, n.g1[1].lds, n.b1[1].lds, n.w2[1].lds, n.ocol[1], n.out[1]}
+                  : UpdHead{n.w1[0].lds, n.g1[0].lds, n.b1[0].lds, n.w2[0].lds, n.ocol[0], n.out[0]};
+  }
+  const int s1 = h >= 1 ? 1 : 0, s2 = h >= 2 ? 1 : 0;
+  auto pick = [&](int v0, int v1, int v2) { return v0 + s1 * (v1 - v0) + s2 * (v2 - v1); };
+  static_assert(UPD_MAXH == 3, "upd_head_info picks among three heads");
+  return UpdHead{pick(n.w1[0].lds, n.w1[1].lds, n.w1[2].lds), pick(n.g1[0].lds, n.g1[1].lds, n.g1[2].lds),
+                 pick(n.b1[0].lds, n.b1[1].lds, n.b1[2].lds), pick(n.w2[0].lds, n.w2[1].lds, n.w2[2].lds),
+                 pick(n.ocol[0], n.ocol[1], n.ocol[2]), pick(n.out[0], n.out[1], n.out[2])};
 }
 
 // A tile's global inputs, loaded into registers ahead of the tile (prefetch): the B fragments
@@ -674,8 +686,8 @@ __device__ inline void upd_tile_load(const UpdNet& n, const float* Sg, const flo
 template <int KD, int KA>
 __device__ inline void upd_tile_fwd(const UpdNet& n, const float* W, const UpdScr& sc,
                                     const UpdIn<upd_ksm<KA>()>& in,
-                                    UpdFwd<upd_ksm<KA>(), upd_hpw<upd_nw<KD, KA>()>()>& f) {
-  constexpr int KSM = upd_ksm<KA>(), NW = upd_nw<KD, KA>(), HPW = upd_hpw<NW>();
+                                    UpdFwd<upd_ksm<KA>(), upd_hpw<KD, KA>()>& f) {
+  constexpr int KSM = upd_ksm<KA>(), NW = upd_nw<KD, KA>(), HPW = upd_hpw<KD, KA>();
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   const int b = w & 3, hg = w >> 2;
   const int D = n.D, KS = (D + 3) >> 2;
@@ -792,14 +804,69 @@ __device__ inline void upd_colsum_add(upd_v4 v, float* g, bool owner, bool first
   }
 }
 
+// The throughput form (TP, many tiles per workgroup and step): the step's gradient accumulates in
+// REGISTERS of its owning lane — the same entries, tile order and per-tile sums as the LDS image
+// above (so the same bits), without the image's load + store per entry and tile — and is stored
+// straight from the registers into the workgroup's partial at the end of phase A.  With 8 waves
+// the two head groups own disjoint parts (group 1: dW1 of both heads; group 0: the trunk), so
+// they share the registers u[].
+template <int NW, int HPW, int KSM, int NH>
+struct UpdGrad {
+  static constexpr int NE = (KSM + 3) / 4;                   // dW0 column blocks
+  static constexpr int NU = NW == 8 ? (4 * NH > NE ? 4 * NH : NE) : 4 * UPD_MAXH + NE;
+  // GroupNorm column sums, packed: after the DPP row sum all 16 lanes of a row hold the same
+  // value, so lane x keeps value v = 16 r + x of cs[r] — v = 8 hs + i: the weight (i < 4) /
+  // bias (i >= 4) sums of head slot hs, v = 8 HPW + i: the trunk's — one or two registers
+  // instead of 4 per sum quad
+  static constexpr int NV = 8 * HPW + 8, NCS = (NV + 15) / 16;
+  upd_v4 w2[HPW];                     // dW2 of head slot hs: [out 4q+i][16b+x]
+  float cs[NCS];
+  upd_v4 u[NU];
+  float bias;                         // wave NW-1, lane l < nout: output bias l
+  float loss[3];                      // wave NW-1 (every lane the same sum; lane 0 publishes)
+  __device__ upd_v4& w1(int h, int bb) { return u[4 * h + bb]; }   // dW1_h [16b+4q+i][16bb+x]
+  __device__ upd_v4& w0(int e) { return u[(NW == 8 ? 0 : 4 * UPD_MAXH) + e]; }
+  // add a row sum s (the same in every lane of the row) into packed value v (compile-time)
+  __device__ void csadd(int v, float s, int x) { cs[v >> 4] += ((v & 15) == x) ? s : 0.f; }
+  __device__ void zero() {
+#pragma unroll
+    for (int k = 0; k < HPW; ++k) w2[k] = upd_v4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < NCS; ++k) cs[k] = 0.f;
+#pragma unroll
+    for (int k = 0; k < NU; ++k) u[k] = upd_v4{0.f, 0.f, 0.f, 0.f};
+    bias = 0.f;
+    loss[0] = loss[1] = loss[2] = 0.f;
+  }
+};
+template <int KD, int KA>
+using UpdGradOf = UpdGrad<upd_nw<KD, KA>(), upd_hpw<KD, KA>(), upd_ksm<KA>(),
+                          KD < 0 ? UPD_MAXH : (upd_kd_discrete(KD) ? 2 : 3)>;
+// sums over the tile's rows of a channel quad, added into packed values v0 .. v0 + 3
+template <class GR>
+__device__ inline void upd_colsum_acc(upd_v4 v, GR& gr, int v0) {
+  const int x = threadIdx.x & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) gr.csadd(v0 + i, upd_rsum16(v[i]), x);
+}
+// largest head output count (the dW2 rows any lane can hold)
+__device__ inline int upd_nomax(const UpdNet& n) {
+  const int a = n.out[0] > n.out[1] ? n.out[0] : n.out[1];
+  return (n.nh > 2 && n.out[2] > a) ? n.out[2] : a;
+}
+// 4-B write-through store of image entry k of a partial (buffer resource at the partial's base)
+__device__ inline void st1_sc1(__amdgpu_buffer_rsrc_t rs, int k, float x) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), rs, (unsigned)k * 4u, 0, UPD_AUX_SC1);
+}
+
 // One tile of the update: forward, loss, backward; the tile's gradient is added into the LDS
 // gradient image Ga (every image entry has exactly one owning lane, so no atomics).  Two
-// workgroup barriers per tile.
-template <int KD, int KA, bool FIRST>
+// workgroup barriers per tile.  RG: into the register gradient gr instead (Ga unused).
+template <int KD, int KA, bool FIRST, bool RG = false>
 __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, float* Ga,
                          const UpdScr& sc, const UpdIn<upd_ksm<KA>()>& in, int rc, float invB,
-                         unsigned long long* tm) {
-  constexpr int KSM = upd_ksm<KA>(), NW = upd_nw<KD, KA>(), HPW = upd_hpw<NW>();
+                         unsigned long long* tm, UpdGradOf<KD, KA>& gr) {
+  constexpr int KSM = upd_ksm<KA>(), NW = upd_nw<KD, KA>(), HPW = upd_hpw<KD, KA>();
   constexpr bool first = FIRST;
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   const int b = w & 3, hg = w >> 2;
@@ -865,8 +932,11 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
         acc = upd_mma(a, Th[(4 * s + q) * 16 + x], acc);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (4 * q + i < no) upd_gadd(Ga + hi.w2 + (4 * q + i) * UPD_HS + 16 * b + x, acc[i], first);
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (RG) {
+          if (i < upd_nomax(n)) gr.w2[hs][i] += acc[i];
+        } else if (4 * q + i < no) upd_gadd(Ga + hi.w2 + (4 * q + i) * UPD_HS + 16 * b + x, acc[i], first);
+      }
       // dG_h^T block b = W2_h^T dO_h^T (K = the head's outputs), GroupNorm + SiLU backward
       upd_v4 dg = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -886,8 +956,13 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
       upd_v4 dyx;
 #pragma unroll
       for (int i = 0; i < 4; ++i) dyx[i] = dy[i] * f.xh[hs][i];
-      upd_colsum_add(dyx, Ga + hi.g1 + 16 * b + 4 * q, x == 0, first);
-      upd_colsum_add(dy, Ga + hi.b1 + 16 * b + 4 * q, x == 0, first);
+      if constexpr (RG) {
+        upd_colsum_acc(dyx, gr, 8 * hs);
+        upd_colsum_acc(dy, gr, 8 * hs + 4);
+      } else {
+        upd_colsum_add(dyx, Ga + hi.g1 + 16 * b + 4 * q, x == 0, first);
+        upd_colsum_add(dy, Ga + hi.b1 + 16 * b + 4 * q, x == 0, first);
+      }
     }
   }
   // inputs, rows x channels, for the weight gradients (the trunk output is in Fs already)
@@ -905,9 +980,12 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
     for (int h = 0; h < UPD_MAXH; ++h) {
       if (h < nh) {
         const float* Zh = sc.Zs + h * UPD_RT * UPD_ZS;
+        // KD = 3 (8-wave three-head net; no LDS form to match bits with): the MFMAs accumulate
+        // straight into the register gradient — 16 registers fewer at the kernel's peak
+        constexpr bool CHAIN = RG && KD == 3;
         upd_v4 acc[4];
 #pragma unroll
-        for (int bb = 0; bb < 4; ++bb) acc[bb] = upd_v4{0.f, 0.f, 0.f, 0.f};
+        for (int bb = 0; bb < 4; ++bb) acc[bb] = CHAIN ? gr.w1(h, bb) : upd_v4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const float a = Zh[(4 * s + q) * UPD_ZS + 16 * b + x];
@@ -915,11 +993,21 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
           for (int bb = 0; bb < 4; ++bb)
             acc[bb] = upd_mma(a, sc.Fs[(4 * s + q) * UPD_ZS + 16 * bb + x], acc[bb]);
         }
-        float* gw1 = Ga + n.w1[h].lds + (16 * b + 4 * q) * UPD_HS + x;
+        if constexpr (CHAIN) {
 #pragma unroll
-        for (int bb = 0; bb < 4; ++bb)
+          for (int bb = 0; bb < 4; ++bb) gr.w1(h, bb) = acc[bb];
+        } else if constexpr (RG) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) upd_gadd(gw1 + i * UPD_HS + 16 * bb, acc[bb][i], first);
+          for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) gr.w1(h, bb)[i] += acc[bb][i];
+        } else {
+          float* gw1 = Ga + n.w1[h].lds + (16 * b + 4 * q) * UPD_HS + x;
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) upd_gadd(gw1 + i * UPD_HS + 16 * bb, acc[bb][i], first);
+        }
       }
     }
   }
@@ -954,8 +1042,13 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
       upd_v4 dyx;
 #pragma unroll
       for (int i = 0; i < 4; ++i) dyx[i] = dy0[i] * f.xh0[i];
-      upd_colsum_add(dyx, Ga + n.g0.lds + 16 * b + 4 * q, x == 0, first);
-      upd_colsum_add(dy0, Ga + n.b0.lds + 16 * b + 4 * q, x == 0, first);
+      if constexpr (RG) {
+        upd_colsum_acc(dyx, gr, 8 * HPW);
+        upd_colsum_acc(dy0, gr, 8 * HPW + 4);
+      } else {
+        upd_colsum_add(dyx, Ga + n.g0.lds + 16 * b + 4 * q, x == 0, first);
+        upd_colsum_add(dy0, Ga + n.b0.lds + 16 * b + 4 * q, x == 0, first);
+      }
     }
     UPD_CMARK(6)
     // ---- dW0[16b + 4q + i][16e + x] += sum_rows dH0[row][ch] X[row][d]  (dH0 transposed via Tw)
@@ -969,7 +1062,10 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
 #pragma unroll
         for (int s = 0; s < 4; ++s)
           acc = upd_mma(Tw[(4 * s + q) * 16 + x], d < D ? sc.Xs[(4 * s + q) * sc.XS + d] : 0.0f, acc);
-        if (d < D) {
+        if constexpr (RG) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) gr.w0(e)[i] += acc[i];
+        } else if (d < D) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             upd_gadd(Ga + n.w0.lds + (16 * b + 4 * q + i) * n.w0.stride + d, acc[i], first);
@@ -984,17 +1080,377 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
       double acc = 0.0;
 #pragma unroll
       for (int r = 0; r < UPD_RT; ++r) acc += (double)dOw[r * 16 + tl_];
-      upd_gadd(Ga + upd_bias_of(n, tl_), (float)acc, first);
+      if constexpr (RG) gr.bias += (float)acc;
+      else upd_gadd(Ga + upd_bias_of(n, tl_), (float)acc, first);
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const float s = upd_rsum16(lp[k]);
-      if (tl_ == 0) upd_gadd(Ga + n.Lp + k, s, first);
+      if constexpr (RG) gr.loss[k] += s;
+      else if (tl_ == 0) upd_gadd(Ga + n.Lp + k, s, first);
     }
   }
   // (the next tile rewrites Tw only after its barrier #0)
   UPD_CMARK(7)
 #undef UPD_CMARK
+}
+
+// T tiles in flight (the throughput form of the 4-wave kernels): upd_tile's stages, each run for
+// tiles u = 0 .. T-1 back to back (innermost where chains are independent), so one tile's
+// latency-bound stretches (the per-row loss, GroupNorm, LDS transposes) issue between the other's
+// MFMAs, and the three workgroup barriers are paid once per T tiles.  Every gradient entry still
+// adds its per-tile sums in tile order, so the bits equal T sequential upd_tile<.., RG> calls.
+// A tile with rc = 0 (odd tile count) runs on zero inputs and adds exact zeros.  Scratch sc[u]
+// per tile (the caller alternates the trunk-output buffers between groups).
+template <int KD, int KA, int T>
+__device__ void upd_tileT(const UpdNet& n, const UpdArgs& args, const float* W, const UpdScr* sc,
+                          const UpdIn<upd_ksm<KA>()>* in, const int* rc, float invB,
+                          unsigned long long* tm, UpdGradOf<KD, KA>& gr) {
+  constexpr int KSM = upd_ksm<KA>(), NW = 4, HPW = UPD_MAXH;
+  static_assert(upd_nw<KD, KA>() == 4, "the T-tile form runs the 4-wave kernels");
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  const int b = w;
+  const int D = n.D, KS = (D + 3) >> 2;
+  const int nh = upd_nh<KD>(n);
+  const bool timer = args.profile && blockIdx.x == 0 && t == 0;
+  unsigned long long tl = timer ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#define UPD_CMARK(i)                                                   \
+  if (timer) {                                                         \
+    const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();  \
+    tm[i] += now_ - tl;                                                \
+    tl = now_;                                                         \
+  }
+  UpdFwd<KSM, HPW> f[T];
+  // ---- trunk block b of every tile -> Fs
+#pragma unroll
+  for (int u = 0; u < T; ++u) {
+    upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* wr = W + n.w0.lds + (16 * b + x) * n.w0.stride;
+#pragma unroll
+    for (int s = 0; s < KSM; ++s) {
+      if (s < KS) {
+        const int d = 4 * s + q;
+        acc = upd_mma(d < D ? wr[d] : 0.0f, in[u].xin[s], acc);
+      }
+    }
+    upd_gn_fwd_frag(acc, upd_ld4(W + n.g0.lds + 16 * b + 4 * q), upd_ld4(W + n.b0.lds + 16 * b + 4 * q),
+                    f[u].xh0, f[u].r0, f[u].Fw);
+    upd_st4(sc[u].Fs + x * UPD_ZS + 16 * b + 4 * q, f[u].Fw);
+  }
+  __syncthreads();   // #0: Fs
+  // ---- heads and the output layer's partial over block b
+  {
+    upd_v4 F[T][4], z[T][HPW];
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) F[u][bb] = upd_ld4(sc[u].Fs + x * UPD_ZS + 16 * bb + 4 * q);
+#pragma unroll
+      for (int hs = 0; hs < HPW; ++hs) z[u][hs] = upd_v4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+#pragma unroll
+      for (int hs = 0; hs < HPW; ++hs) {
+        if (hs < nh) {
+          const UpdHead hi = upd_head_info(n, hs);
+          const upd_v4 wa = upd_ld4(W + hi.w1 + (16 * b + x) * UPD_HS + 16 * bb + 4 * q);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int u = 0; u < T; ++u) z[u][hs] = upd_mma(wa[e], F[u][bb][e], z[u][hs]);
+        }
+      }
+    }
+    upd_v4 o[T];
+#pragma unroll
+    for (int u = 0; u < T; ++u) o[u] = upd_v4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int hs = 0; hs < HPW; ++hs) {
+      if (hs < nh) {
+        const UpdHead hi = upd_head_info(n, hs);
+        const upd_v4 gw = upd_ld4(W + hi.g1 + 16 * b + 4 * q), gb = upd_ld4(W + hi.b1 + 16 * b + 4 * q);
+        const int oc = hi.oc, no = hi.no;
+        const bool mine = x >= oc && x < oc + no;
+        const upd_v4 wv = mine ? upd_ld4(W + hi.w2 + (x - oc) * UPD_HS + 16 * b + 4 * q)
+                               : upd_v4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < T; ++u)
+          upd_gn_fwd_frag(z[u][hs], gw, gb, f[u].xh[hs], f[u].rh[hs], f[u].G[hs]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int u = 0; u < T; ++u) o[u] = upd_mma(wv[e], f[u].G[hs][e], o[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+      upd_st4(sc[u].Op + (w * 16 + x) * 16 + 4 * q, o[u]);
+      if (t < UPD_RT * UPD_RIN) sc[u].Rin[t] = in[u].rin;
+    }
+  }
+  UPD_CMARK(0)
+  __syncthreads();   // #1: Op, Rin
+  UPD_CMARK(1)
+  // ---- loss of row x of every tile (lanes q == 0 of every wave)
+  float lp[T][3];
+#pragma unroll
+  for (int u = 0; u < T; ++u) {
+    lp[u][0] = lp[u][1] = lp[u][2] = 0.f;
+    const float* Orow = upd_tile_outputs<NW>(n, W, sc[u]);
+    if (q == 0) {
+      float* dOrow = sc[u].dOs + (w * 16 + x) * 16;
+      if (x < rc[u]) {
+        upd_row_loss<KD, KA>(n, Orow, sc[u].Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dOrow, lp[u]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < UPD_MAXO; ++j) dOrow[j] = 0.f;
+      }
+    }
+  }
+  upd_wave_sync();
+  UPD_CMARK(2)
+  const int TS = upd_ts(n);
+  float* Tw[T];
+#pragma unroll
+  for (int u = 0; u < T; ++u) {
+    Tw[u] = sc[u].Ts + w * TS * UPD_RT * 16;
+#pragma unroll
+    for (int hs = 0; hs < HPW; ++hs)
+      if (hs < TS && hs < nh) upd_st4(Tw[u] + hs * UPD_RT * 16 + x * 16 + 4 * q, f[u].G[hs]);
+  }
+  upd_wave_sync();
+  // ---- heads backward: dW2, dG -> GroupNorm + SiLU backward -> dZ (Zs), GN column sums
+#pragma unroll
+  for (int hs = 0; hs < HPW; ++hs) {
+    if (hs < nh) {
+      const UpdHead hi = upd_head_info(n, hs);
+      const int oc = hi.oc, no = hi.no;
+      const int slot = TS == 1 ? 0 : hs;
+      if (hs >= TS) {   // the shared slot is free once the previous head has read it
+        upd_wave_sync();
+#pragma unroll
+        for (int u = 0; u < T; ++u) upd_st4(Tw[u] + x * 16 + 4 * q, f[u].G[hs]);
+        upd_wave_sync();
+      }
+      const upd_v4 gw = upd_ld4(W + hi.g1 + 16 * b + 4 * q), gb = upd_ld4(W + hi.b1 + 16 * b + 4 * q);
+      upd_v4 acc[T], dg[T];
+#pragma unroll
+      for (int u = 0; u < T; ++u) acc[u] = dg[u] = upd_v4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int u = 0; u < T; ++u) {
+          const float* dOw = sc[u].dOs + w * 16 * 16;
+          const float a = x < no ? dOw[(4 * s + q) * 16 + oc + x] : 0.0f;
+          acc[u] = upd_mma(a, Tw[u][slot * UPD_RT * 16 + (4 * s + q) * 16 + x], acc[u]);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < UPD_MAXA / 4; ++s) {
+        if (4 * s < no) {
+          const int j = 4 * s + q;
+          const float a = j < no ? W[hi.w2 + j * UPD_HS + 16 * b + x] : 0.0f;
+#pragma unroll
+          for (int u = 0; u < T; ++u) {
+            const float* dOw = sc[u].dOs + w * 16 * 16;
+            dg[u] = upd_mma(a, j < no ? dOw[x * 16 + oc + j] : 0.0f, dg[u]);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < T; ++u) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i < upd_nomax(n)) gr.w2[hs][i] += acc[u][i];
+        upd_v4 dy;
+        const upd_v4 dz = upd_gn_bwd_frag(dg[u], f[u].xh[hs], gw, gb, f[u].rh[hs], dy);
+        upd_st4(sc[u].Zs + hs * UPD_RT * UPD_ZS + x * UPD_ZS + 16 * b + 4 * q, dz);
+        upd_v4 dyx;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dyx[i] = dy[i] * f[u].xh[hs][i];
+        upd_colsum_acc(dyx, gr, 8 * hs);
+        upd_colsum_acc(dy, gr, 8 * hs + 4);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < T; ++u)
+#pragma unroll
+    for (int s = 0; s < KSM; ++s)
+      if (s < KS && (s % NW) == w) sc[u].Xs[x * sc[u].XS + 4 * s + q] = in[u].xin[s];
+  UPD_CMARK(3)
+  __syncthreads();   // #2: Zs, Fs, Xs
+  UPD_CMARK(4)
+  // ---- dW1_h[16b + 4q + i][16bb + x] += sum_rows dZ_h[row][out] F[row][in]
+#pragma unroll
+  for (int h = 0; h < UPD_MAXH; ++h) {
+    if (h < nh) {
+      upd_v4 acc[T][4];
+#pragma unroll
+      for (int u = 0; u < T; ++u)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) acc[u][bb] = upd_v4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int u = 0; u < T; ++u) {
+          const float a = sc[u].Zs[h * UPD_RT * UPD_ZS + (4 * s + q) * UPD_ZS + 16 * b + x];
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb)
+            acc[u][bb] = upd_mma(a, sc[u].Fs[(4 * s + q) * UPD_ZS + 16 * bb + x], acc[u][bb]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < T; ++u)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) gr.w1(h, bb) += acc[u][bb];
+    }
+  }
+  UPD_CMARK(5)
+  // ---- dF^T block b = sum_h W1_h^T dZ_h^T, trunk GroupNorm + SiLU backward, its column sums
+  upd_v4 dH0[T];
+  {
+    upd_v4 d0[T], d1[T];
+#pragma unroll
+    for (int u = 0; u < T; ++u) d0[u] = d1[u] = upd_v4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < UPD_MAXH; ++h) {
+      if (h < nh) {
+        const float* Wh = W + n.w1[h].lds + 16 * b + x;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const int o = 16 * (s & 3) + 4 * q + (s >> 2);
+          const float a = Wh[o * UPD_HS];
+#pragma unroll
+          for (int u = 0; u < T; ++u) {
+            const float zb = sc[u].Zs[h * UPD_RT * UPD_ZS + x * UPD_ZS + o];
+            if (s & 1) d1[u] = upd_mma(a, zb, d1[u]);
+            else d0[u] = upd_mma(a, zb, d0[u]);
+          }
+        }
+      }
+    }
+    const upd_v4 g0w = upd_ld4(W + n.g0.lds + 16 * b + 4 * q), g0b = upd_ld4(W + n.b0.lds + 16 * b + 4 * q);
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+      upd_v4 dF, dy0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dF[i] = d0[u][i] + d1[u][i];
+      dH0[u] = upd_gn_bwd_frag(dF, f[u].xh0, g0w, g0b, f[u].r0, dy0);
+      upd_v4 dyx;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dyx[i] = dy0[i] * f[u].xh0[i];
+      upd_colsum_acc(dyx, gr, 8 * HPW);
+      upd_colsum_acc(dy0, gr, 8 * HPW + 4);
+    }
+  }
+  UPD_CMARK(6)
+  // ---- dW0[16b + 4q + i][16e + x] += sum_rows dH0[row][ch] X[row][d]  (dH0 transposed via Tw)
+#pragma unroll
+  for (int u = 0; u < T; ++u) upd_st4(Tw[u] + x * 16 + 4 * q, dH0[u]);
+  upd_wave_sync();
+#pragma unroll
+  for (int e = 0; e < (KSM + 3) / 4; ++e) {
+    if (16 * e < D) {
+      const int d = 16 * e + x;
+      upd_v4 acc[T];
+#pragma unroll
+      for (int u = 0; u < T; ++u) acc[u] = upd_v4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int u = 0; u < T; ++u)
+          acc[u] = upd_mma(Tw[u][(4 * s + q) * 16 + x], d < D ? sc[u].Xs[(4 * s + q) * sc[u].XS + d] : 0.0f, acc[u]);
+#pragma unroll
+      for (int u = 0; u < T; ++u) gr.w0(e) += acc[u];
+    }
+  }
+  // ---- output biases and loss partials (the last wave)
+  if (w == NW - 1) {
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+      if (l < n.nout) {   // f64 sum: the softmax outputs' dO cancel across rows
+        const float* dOw = sc[u].dOs + w * 16 * 16;
+        double acc = 0.0;
+#pragma unroll
+        for (int r = 0; r < UPD_RT; ++r) acc += (double)dOw[r * 16 + l];
+        gr.bias += (float)acc;
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) gr.loss[k] += upd_rsum16(lp[u][k]);
+    }
+  }
+  UPD_CMARK(7)
+#undef UPD_CMARK
+}
+
+// TP: store this lane's register gradient into the workgroup's partial (rs = its base), at the
+// image entries the LDS form would have written (the others were zeroed at launch start).
+// Lanes x of one register i store 16 consecutive words.
+template <int KD, int KA>
+__device__ inline void upd_grad_publish(const UpdNet& n, UpdGradOf<KD, KA>& gr,
+                                        __amdgpu_buffer_rsrc_t rs) {
+  constexpr int KSM = upd_ksm<KA>(), NW = upd_nw<KD, KA>(), HPW = upd_hpw<KD, KA>();
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  const int b = w & 3, hg = w >> 2;
+  const int D = n.D;
+  const int nh = upd_nh<KD>(n);
+#pragma unroll
+  for (int hs = 0; hs < HPW; ++hs) {
+    const int h = upd_head<NW>(hs, hg);
+    if (h < nh) {
+      const UpdHead hi = upd_head_info(n, h);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (i < upd_nomax(n) && 4 * q + i < hi.no) st1_sc1(rs, hi.w2 + (4 * q + i) * UPD_HS + 16 * b + x, gr.w2[hs][i]);
+    }
+  }
+  // packed column sums: lane x of register r holds value v = 16 r + x
+  using GR = UpdGradOf<KD, KA>;
+#pragma unroll
+  for (int r = 0; r < GR::NCS; ++r) {
+    const int v = 16 * r + x;
+    if (v < 8 * HPW) {
+      const int h = upd_head<NW>(v >> 3, hg), j = v & 7;
+      if (h < nh) {
+        const UpdHead hi = upd_head_info(n, h);
+        st1_sc1(rs, (j < 4 ? hi.g1 : hi.b1) + 16 * b + 4 * q + (j & 3), gr.cs[r]);
+      }
+    } else if (v < GR::NV && (NW == 4 || hg == 0)) {
+      const int j = v - 8 * HPW;
+      st1_sc1(rs, (j < 4 ? n.g0.lds : n.b0.lds) + 16 * b + 4 * q + (j & 3), gr.cs[r]);
+    }
+  }
+  if (NW == 4 || hg == 1) {
+#pragma unroll
+    for (int h = 0; h < UPD_MAXH; ++h) {
+      if (h < nh) {
+        const int base = n.w1[h].lds + (16 * b + 4 * q) * UPD_HS + x;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) st1_sc1(rs, base + i * UPD_HS + 16 * bb, gr.w1(h, bb)[i]);
+      }
+    }
+  }
+  if (NW == 4 || hg == 0) {
+#pragma unroll
+    for (int e = 0; e < (KSM + 3) / 4; ++e) {
+      const int d = 16 * e + x;
+      if (16 * e < D && d < D) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st1_sc1(rs, n.w0.lds + (16 * b + 4 * q + i) * n.w0.stride + d, gr.w0(e)[i]);
+      }
+    }
+  }
+  if (w == NW - 1) {
+    if (l < n.nout) st1_sc1(rs, upd_bias_of(n, l), gr.bias);
+    if (l == 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) st1_sc1(rs, n.Lp + k, gr.loss[k]);
+    }
+  }
 }
 
 __device__ inline float f4get(const float4& v, int e) {
@@ -1209,42 +1665,65 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
 // NQ = parameter quads per thread (ceil(Lp / 4 / 256)): AdamW's moments live in registers.
 // DP: the data-parallel form (prl_ppo_update_dpx): union-minibatch row weights and the
 // cross-rank slice sum; a separate instantiation, so the single-GPU kernel carries none of it.
-template <int NQ, int KD, int KA, bool DP>
+// TP: the throughput form for many tiles per workgroup and step (upd_tp_host): the gradient in
+// registers (UpdGrad, no LDS image) and the moments streamed from device memory in phase C
+// instead of held in registers — the owner of each slice writes its new moments to the other of
+// two buffers (the step's source for the next step) — so the tiles run with ~110 more registers
+// and without the image's LDS traffic.  Needs >= 2 steps (upd_run).  TPM = T >= 2: T tiles in
+// flight per wave (upd_tileT; 4-wave kernels), T scratch regions.
+template <int NQ, int KD, int KA, bool DP, int TPM = 0>
 __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& args) {
   constexpr int NW = upd_nw<KD, KA>(), NT = 64 * NW;
+  constexpr bool TP = TPM > 0;
+  constexpr int TT = TPM > 1 ? TPM : 1;   // tiles in flight
   extern __shared__ __align__(16) float upd_lds[];
   const int t = threadIdx.x, g = blockIdx.x, G = args.G;
   const int Lp = n.Lp;
   const int Qp = Lp / 4;            // parameter quads
   const int Qtot = Qp + 1;          // + one quad of loss partials
   float* hdr = upd_lds;             // [64] broadcast words + chunk stage timers
-  // LDS: header | tile scratch | parameter image W | gradient image Ga.  The scratch sits below
-  // 64 KB so every scratch address folds into the ds instructions' 16-bit offset field (no base
-  // registers kept live across the step loop)
+  // LDS: header | tile scratch | parameter image W | gradient image Ga (not TP).  The scratch
+  // sits below 64 KB so every scratch address folds into the ds instructions' 16-bit offset field
+  // (no base registers kept live across the step loop)
   float* scratch = upd_lds + UPD_HDR;                                   // tile activations
-  float* W = scratch + ((upd_scratch_floats(n.D, NW, upd_ts(n)) + 3) & ~3);         // [Lp]
+  const int scr_floats = (upd_scratch_floats(n.D, NW, upd_ts(n)) + 3) & ~3;
+  float* W = scratch + TT * scr_floats;                                  // [Lp]
   float* Ga = W + Lp;                                                    // [Lp + 4]
   const UpdScr sc = upd_scr(scratch, n.D, NW);
+  UpdScr scT[TT];
+#pragma unroll
+  for (int u = 0; u < TT; ++u) scT[u] = upd_scr(scratch + u * scr_floats, n.D, NW);
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
   float* s_adam = hdr + 10;         // [2] this step's AdamW step size, 1 / sqrt(bc2)
 
   // ---- load the parameter image into LDS and this thread's moment quads (q = t + NT i) into
   //      registers: args.params / exp_avg / exp_avg_sq are IMAGES here (prl_ppo_update converts
   //      the flat torch vectors around the launch), so no layout arithmetic stays live in SGPRs
-  float4 mreg[NQ], vreg[NQ];
+  constexpr int NQR = TP ? 1 : NQ;
+  float4 mreg[NQR], vreg[NQR];
   for (int q = t; q < Qp; q += NT)
     *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(args.params + 4 * q);
+  if constexpr (!TP) {
 #pragma unroll
-  for (int i = 0; i < NQ; ++i) {
-    const int q = t + i * NT;
-    mreg[i] = q < Qp ? *reinterpret_cast<const float4*>(args.exp_avg + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
-    vreg[i] = q < Qp ? *reinterpret_cast<const float4*>(args.exp_avg_sq + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NQ; ++i) {
+      const int q = t + i * NT;
+      mreg[i] = q < Qp ? *reinterpret_cast<const float4*>(args.exp_avg + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+      vreg[i] = q < Qp ? *reinterpret_cast<const float4*>(args.exp_avg_sq + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+  } else {
+    // the register gradient covers only real entries: the rest of this workgroup's partial
+    // (padding) is zeroed here once, drained before the first publish
+    const __amdgpu_buffer_rsrc_t rs_mypart = upd_rsrc(args.part + (size_t)g * Qtot * 4);
+    for (int q = t; q < Qtot; q += NT) st4_sc1(rs_mypart, (size_t)q * 4, float4{0.f, 0.f, 0.f, 0.f});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   const float step0 = args.adam_step[0];
   if (t < 24) reinterpret_cast<unsigned long long*>(hdr + 16)[t] = 0ull;
   __syncthreads();
-  for (int k = t; k < Lp + 4; k += NT) Ga[k] = 0.0f;   // padding stays 0 for good
-  __syncthreads();
+  if constexpr (!TP) {
+    for (int k = t; k < Lp + 4; k += NT) Ga[k] = 0.0f;   // padding stays 0 for good
+    __syncthreads();
+  }
 
   const int R = args.R;
   float loss_last = 0.f;
@@ -1266,7 +1745,21 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       pts[7] = now;
     }
   };
-  UpdIn<upd_ksm<KA>()> nin;   // inputs of the next tile to run (prefetched)
+  UpdIn<upd_ksm<KA>()> nin[TT];   // inputs of the next tile(s) to run (prefetched)
+  // load the TT tiles from row0 (rows_left rows of this workgroup's share from there on; with
+  // TT > 1 a tile past them loads zeros and runs as a zero tile)
+  auto load_next = [&](int64_t row0, int rows_left) {
+    if constexpr (TT == 1) {
+      upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret, row0,
+                            std::min(UPD_RT, rows_left), nin[0]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < TT; ++u)
+        upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret, row0 + u * UPD_RT,
+                              std::max(0, std::min(UPD_RT, rows_left - u * UPD_RT)), nin[u]);
+    }
+  };
+  unsigned long long* const tm = reinterpret_cast<unsigned long long*>(hdr + 16);
   for (int s = 0; s < args.total_steps; ++s) {
     const int j = s % args.nb;
     const int64_t mb0 = (int64_t)j * args.mb;
@@ -1276,40 +1769,60 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     const int myrows = args.profile == 2 ? 0 : std::max(0, std::min(R, B - g * R));
     const int64_t myrow0 = mb0 + (int64_t)g * R;
     // ---- phase A: partial gradient of this workgroup's rows ------------------------------------
-    if (s == 0 && myrows > 0)
-      upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret, myrow0,
-                            std::min(UPD_RT, myrows), nin);
-    if (myrows == 0) {   // no rows this step: publish zeros
+    if (s == 0 && myrows > 0) load_next(myrow0, myrows);
+    UpdGradOf<KD, KA> gr;
+    if constexpr (TP) gr.zero();
+    if (!TP && myrows == 0) {   // no rows this step: publish zeros
       for (int k = t; k < Lp + 4; k += NT) Ga[k] = 0.0f;
     }
-    for (int c0 = 0; c0 < myrows; c0 += UPD_RT) {
-      const UpdIn<upd_ksm<KA>()> cur = nin;
-      if (c0 + UPD_RT < myrows)   // prefetch the next tile of this step
-        upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
-                              myrow0 + c0 + UPD_RT, std::min(UPD_RT, myrows - c0 - UPD_RT), nin);
-      if (c0 == 0)
-        upd_tile<KD, KA, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0), invB,
-                               reinterpret_cast<unsigned long long*>(hdr + 16));
-      else
-        upd_tile<KD, KA, false>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0), invB,
-                                reinterpret_cast<unsigned long long*>(hdr + 16));
+    if constexpr (TT > 1) {
+      for (int c0 = 0; c0 < myrows; c0 += TT * UPD_RT) {
+        UpdIn<upd_ksm<KA>()> cur[TT];
+        int rcs[TT];
+        UpdScr scg[TT];
+#pragma unroll
+        for (int u = 0; u < TT; ++u) {
+          cur[u] = nin[u];
+          rcs[u] = std::max(0, std::min(UPD_RT, myrows - c0 - u * UPD_RT));
+          scg[u] = upd_scr_tile(scT[u], c0 / (TT * UPD_RT));   // trunk buffers alternate by group
+        }
+        if (c0 + TT * UPD_RT < myrows)   // prefetch the next group of this step
+          load_next(myrow0 + c0 + TT * UPD_RT, myrows - c0 - TT * UPD_RT);
+        upd_tileT<KD, KA, TT>(n, args, W, scg, cur, rcs, invB, tm, gr);
+      }
+    } else {
+      for (int c0 = 0; c0 < myrows; c0 += UPD_RT) {
+        const UpdIn<upd_ksm<KA>()> cur = nin[0];
+        if (c0 + UPD_RT < myrows)   // prefetch the next tile of this step
+          load_next(myrow0 + c0 + UPD_RT, myrows - c0 - UPD_RT);
+        if constexpr (TP)
+          upd_tile<KD, KA, false, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0),
+                                        invB, tm, gr);
+        else if (c0 == 0)
+          upd_tile<KD, KA, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0), invB,
+                                 tm, gr);
+        else
+          upd_tile<KD, KA, false>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0), invB,
+                                  tm, gr);
+      }
     }
-    __syncthreads();
+    if constexpr (!TP) __syncthreads();
     mark(0);   // phase A compute
-    const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part),
-                                 rs_red = upd_rsrc(args.red);
-    for (int q = t; q < Qtot; q += NT)
-      st4_sc1(rs_part, ((size_t)g * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
+    const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(args.red);
+    if constexpr (TP) {
+      upd_grad_publish<KD, KA>(n, gr, upd_rsrc(args.part + (size_t)g * Qtot * 4));
+    } else {
+      for (int q = t; q < Qtot; q += NT)
+        st4_sc1(rs_part, ((size_t)g * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     mark(1);   // publish partials
-    if (s + 1 < args.total_steps) {   // prefetch the next step's first tile (runs under the waits)
+    if (s + 1 < args.total_steps) {   // prefetch the next step's first tile(s) (runs under the waits)
       const int64_t nmb0 = (int64_t)((s + 1) % args.nb) * args.mb;
       const int nB = (int)std::min<int64_t>(args.mb, args.N - nmb0);
       const int nrows = std::max(0, std::min(R, nB - g * R));
-      if (nrows > 0)
-        upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
-                              nmb0 + (int64_t)g * R, std::min(UPD_RT, nrows), nin);
+      if (nrows > 0) load_next(nmb0 + (int64_t)g * R, nrows);
     }
     if (t < 64) {
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_A, g);
@@ -1359,9 +1872,30 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
 #pragma unroll
     for (int i = 0; i < NQ; ++i)
       if (i * NT < Qp) gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * NT));
+    // TP: this step's moments (written by the slice owners last step; the launch's images at
+    // step 0), loaded with the gradient; the new ones go to the other buffer (the images at the
+    // last step: every workgroup read them at step 0 only, before the barriers since)
+    constexpr int NQM = TP ? NQ : 1;
+    float4 mq[NQM], vq[NQM];
+    const bool lastst = s + 1 == args.total_steps;
+    const float* msrc = s == 0 ? args.exp_avg : ((s & 1) ? args.tp_m1 : args.tp_m0);
+    const float* vsrc = s == 0 ? args.exp_avg_sq : ((s & 1) ? args.tp_v1 : args.tp_v0);
+    float* mdst = lastst ? args.exp_avg : ((s & 1) ? args.tp_m0 : args.tp_m1);
+    float* vdst = lastst ? args.exp_avg_sq : ((s & 1) ? args.tp_v0 : args.tp_v1);
+    if constexpr (TP) {
+      const __amdgpu_buffer_rsrc_t rm = upd_rsrc(msrc), rv = upd_rsrc(vsrc);
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        if (i * NT < Qp) {
+          mq[i] = ld4_sc1_so(rm, 16u * (unsigned)t, 16u * (unsigned)(i * NT));
+          vq[i] = ld4_sc1_so(rv, 16u * (unsigned)t, 16u * (unsigned)(i * NT));
+        }
+      }
+    }
     // 8 waves (two per SIMD, 256 registers each): park the quads in the gradient image, free
     // since the publish, so they do not stay live across the norm into AdamW
-    constexpr bool PARK = NW == 8;
+    constexpr bool PARK = NW == 8 && !TP;
+    float* const park = Ga;
     float clipc;
     {
       // clip_grad_norm_'s norm from the reduced gradient this workgroup just loaded: per thread
@@ -1375,7 +1909,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       for (int i = 0; i < NQ; ++i) {
         if (i * NT < Qp && t + i * NT < Qp) {
           acc += (gq[i].x * gq[i].x + gq[i].y * gq[i].y) + (gq[i].z * gq[i].z + gq[i].w * gq[i].w);
-          if (PARK) *reinterpret_cast<float4*>(Ga + 4 * (t + i * NT)) = gq[i];
+          if (PARK) *reinterpret_cast<float4*>(park + 4 * (t + i * NT)) = gq[i];
         }
       }
       subm.mark(2);   // thread 0's gradient quads landed
@@ -1409,8 +1943,15 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
           const int q = t + i * NT;
           if (i < NQ && q < Qp) {
             float4 pw = *reinterpret_cast<float4*>(W + 4 * q);
-            float4 m4 = mreg[i], v4 = vreg[i];
-            const float4 g4 = PARK ? *reinterpret_cast<const float4*>(Ga + 4 * q) : gq[i];
+            float4 m4, v4;
+            if constexpr (TP) {
+              m4 = mq[i];
+              v4 = vq[i];
+            } else {
+              m4 = mreg[i];
+              v4 = vreg[i];
+            }
+            const float4 g4 = PARK ? *reinterpret_cast<const float4*>(park + 4 * q) : gq[i];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const float gr = f4get(g4, e) * clipc;
@@ -1427,8 +1968,15 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
               f4set(v4, e, v);
               f4set(pw, e, p);
             }
-            mreg[i] = m4;
-            vreg[i] = v4;
+            if constexpr (TP) {
+              if (q >= (int)((int64_t)Qtot * g / G) && q < (int)((int64_t)Qtot * (g + 1) / G)) {   // my slice
+                st4_sc1(upd_rsrc(mdst), (size_t)q * 4, m4);
+                st4_sc1(upd_rsrc(vdst), (size_t)q * 4, v4);
+              }
+            } else {
+              mreg[i] = m4;
+              vreg[i] = v4;
+            }
             *reinterpret_cast<float4*>(W + 4 * q) = pw;
           }
         }
@@ -1441,12 +1989,14 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
   if (g == 0) {
     for (int q = t; q < Qp; q += NT)
       *reinterpret_cast<float4*>(args.params + 4 * q) = *reinterpret_cast<const float4*>(W + 4 * q);
+    if constexpr (!TP) {   // (TP: the slice owners stored them at the last step)
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      const int q = t + i * NT;
-      if (q < Qp) {
-        *reinterpret_cast<float4*>(args.exp_avg + 4 * q) = mreg[i];
-        *reinterpret_cast<float4*>(args.exp_avg_sq + 4 * q) = vreg[i];
+      for (int i = 0; i < NQ; ++i) {
+        const int q = t + i * NT;
+        if (q < Qp) {
+          *reinterpret_cast<float4*>(args.exp_avg + 4 * q) = mreg[i];
+          *reinterpret_cast<float4*>(args.exp_avg_sq + 4 * q) = vreg[i];
+        }
       }
     }
     if (t == 0) {
@@ -1463,13 +2013,13 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
 
 // KDIM > 0: the observation dim is a compile-time constant and the whole parameter layout folds
 // into immediates (the specialised shapes); KDIM = 0: runtime layout from the kernel argument.
-template <int NQ, int KD, int KA, int KDIM, bool DP = false>
+template <int NQ, int KD, int KA, int KDIM, bool DP = false, int TPM = 0>
 __global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_update_kernel(UpdArgs args) {
   if constexpr (KDIM > 0) {
-    constexpr UpdNet N = upd_make(KDIM, KA, KD);
-    ppo_update_body<NQ, KD, KA, DP>(N, args);
+    constexpr UpdNet N = upd_make(KDIM, KA, upd_kd_discrete(KD) ? 1 : 0);
+    ppo_update_body<NQ, KD, KA, DP, TPM>(N, args);
   } else {
-    ppo_update_body<NQ, KD, KA, DP>(args.net, args);
+    ppo_update_body<NQ, KD, KA, DP, TPM>(args.net, args);
   }
 }
 
@@ -1497,7 +2047,7 @@ __device__ __forceinline__ void ppo_evaluate_body(const UpdNet& n, const UpdArgs
     const int rc = (int)std::min<int64_t>(UPD_RT, args.N - row0);
     UpdIn<upd_ksm<KA>()> in;
     upd_tile_load<KD, KA>(n, args.S, args.act, nullptr, nullptr, nullptr, row0, rc, in);
-    UpdFwd<upd_ksm<KA>(), upd_hpw<NW>()> f;
+    UpdFwd<upd_ksm<KA>(), upd_hpw<KD, KA>()> f;
     upd_tile_fwd<KD, KA>(n, W, sc, in, f);
     __syncthreads();
     if (w == 0) {
@@ -1518,7 +2068,7 @@ template <int KD, int KA, int KDIM>
 __global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_evaluate_kernel(UpdArgs args, float* logp_out,
                                                                               float* V_out, float* H_out) {
   if constexpr (KDIM > 0) {
-    constexpr UpdNet N = upd_make(KDIM, KA, KD);
+    constexpr UpdNet N = upd_make(KDIM, KA, upd_kd_discrete(KD) ? 1 : 0);
     ppo_evaluate_body<KD, KA>(N, args, logp_out, V_out, H_out);
   } else {
     ppo_evaluate_body<KD, KA>(args.net, args, logp_out, V_out, H_out);
@@ -1639,8 +2189,9 @@ __device__ __forceinline__ void ppo_grad_body(const UpdNet& n, const UpdArgs& ar
     UpdIn<upd_ksm<KA>()> in;
     upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
                           row0 + (int64_t)g * R + c0, rc, in);
-    if (c0 == 0) upd_tile<KD, KA, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), in, rc, inv_count, tm);
-    else upd_tile<KD, KA, false>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), in, rc, inv_count, tm);
+    UpdGradOf<KD, KA> unused;   // (the LDS form: never touched)
+    if (c0 == 0) upd_tile<KD, KA, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), in, rc, inv_count, tm, unused);
+    else upd_tile<KD, KA, false>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), in, rc, inv_count, tm, unused);
   }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(grad_out);
@@ -1664,7 +2215,7 @@ __global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_grad_kernel(Up
                                                                 int B_local, float inv_count,
                                                                 UpdFold fold) {
   if constexpr (KDIM > 0) {
-    constexpr UpdNet N = upd_make(KDIM, KA, KD);
+    constexpr UpdNet N = upd_make(KDIM, KA, upd_kd_discrete(KD) ? 1 : 0);
     constexpr int NI = (N.Lp / 4 + UPD_THREADS - 1) / UPD_THREADS;
     ppo_grad_body<KD, KA, NI>(N, args, img, grad_out, row0, B_local, inv_count, fold);
   } else {
@@ -1772,6 +2323,20 @@ bool upd_force_generic() {
   const char* e = getenv("PRL_UPD_GENERIC");
   return e && e[0] == '1';
 }
+// PRL_UPD_TP / prl_ppo_update_set_tp: 0 never, 1 whenever allowed, 2 (default) auto (>= 2
+// tiles per workgroup and step)
+int g_tp_mode = [] {
+  const char* e = getenv("PRL_UPD_TP");
+  return (e && e[0] == '0') ? 0 : ((e && e[0] == '1') ? 1 : 2);
+}();
+int upd_tp_mode() { return g_tp_mode; }
+// the throughput form (ppo_update_body<.., TP>) for this launch: rows per workgroup and step R,
+// total steps (the streamed moments need >= 2), single-GPU only
+bool upd_tp_host(int R, int total_steps, bool dp) {
+  const int m = upd_tp_mode();
+  if (dp || total_steps < 2 || m == 0) return false;
+  return m == 1 || R >= 2 * UPD_RT;
+}
 const void* upd_kernel_for(const UpdNet& n, bool dp = false) {
   if (dp) {
     const int nq = upd_nq(n);
@@ -1789,6 +2354,41 @@ const void* upd_kernel_for(const UpdNet& n, bool dp = false) {
   if (!n.discrete && n.A == 1 && n.D == 3 && nq <= 14) return reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3>);
   if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0>);
   return nullptr;
+}
+// The throughput form's kernel for this shape: T = 2 tiles in flight on the 4-wave kernels
+// (PRL_UPD_T=1: one tile, and CartPole's 8-wave head-split kernel); the runtime-layout kernel
+// runs one tile (it spills registers already).
+struct UpdPlan {
+  const void* kern;
+  int nw, tiles;
+};
+int g_tp_tiles = [] {
+  const char* e = getenv("PRL_UPD_T");
+  return (e && e[0] == '2') ? 2 : 1;
+}();
+UpdPlan upd_tp_plan(const UpdNet& n) {
+  const int qp = n.Lp / 4;
+  const bool two = g_tp_tiles == 2;
+  if (!upd_force_generic()) {
+    if (upd_is_cartpole(n) && two && cdiv(qp, 256) <= 10)
+      return {reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4, false, 2>), 4, 2};
+    if (upd_is_cartpole(n) && upd_waves8_enabled() && cdiv(qp, 512) <= 5)
+      return {reinterpret_cast<const void*>(ppo_update_kernel<5, 2, 2, 4, false, 1>), 8, 1};
+    if (upd_is_cartpole(n) && cdiv(qp, 256) <= 10)
+      return {reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4, false, 1>), 4, 1};
+    const bool pend = !n.discrete && n.A == 1 && n.D == 3;
+    if (pend && !two && upd_waves8_enabled() && cdiv(qp, 512) <= 7)
+      return {reinterpret_cast<const void*>(ppo_update_kernel<7, 3, 1, 3, false, 1>), 8, 1};
+    if (pend && cdiv(qp, 256) <= 14)
+      return two ? UpdPlan{reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3, false, 2>), 4, 2}
+                 : UpdPlan{reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3, false, 1>), 4, 1};
+  }
+  if (cdiv(qp, 256) <= 20) return {reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0, false, 1>), 4, 1};
+  return {nullptr, 4, 1};
+}
+size_t upd_lds_bytes_plan(const UpdNet& n, int nw, bool tp, int tiles) {
+  return sizeof(float) * (size_t)(UPD_HDR + (tp ? n.Lp : 2 * n.Lp + 4) +
+                                  tiles * ((upd_scratch_floats(n.D, nw, upd_ts(n)) + 3) & ~3));
 }
 const void* upd_grad_kernel_for(const UpdNet& n) {
   if (upd_force_generic()) return reinterpret_cast<const void*>(ppo_grad_kernel<-1, 0, 0>);
@@ -1822,8 +2422,9 @@ hipError_t upd_launch_resident(const void* kern, int G, int threads, size_t lds,
   return hipLaunchKernel(kern, dim3(G), dim3(threads), kargs, lds, st);
 }
 
-size_t upd_lds_bytes(const UpdNet& n, bool persistent) {
-  return sizeof(float) * (size_t)(UPD_HDR + 2 * n.Lp + 4 + ((upd_scratch_floats(n.D, upd_nw_host(n, persistent), upd_ts(n)) + 3) & ~3));
+size_t upd_lds_bytes(const UpdNet& n, bool persistent, bool tp = false) {
+  return sizeof(float) * (size_t)(UPD_HDR + (tp ? n.Lp : 2 * n.Lp + 4) +
+                                  ((upd_scratch_floats(n.D, upd_nw_host(n, persistent), upd_ts(n)) + 3) & ~3));
 }
 
 struct UpdWs {
@@ -1833,15 +2434,21 @@ struct UpdWs {
   float* red;
   float* part;
   float* img;   // [3][Lp + 4]: parameter, exp_avg, exp_avg_sq images of the persistent launch
+  float* mv;    // [4][Lp + 4]: the throughput form's moment buffers m0, v0, m1, v1
 };
 
-// workspace: ctr[UPD_CTR_WORDS] (words 0-3 and the shards zeroed per launch, word 4 sticky) | prof[32] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4]
+// workspace: ctr[UPD_CTR_WORDS] (words 0-3 and the shards zeroed per launch, word 4 sticky) |
+// prof[32] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4] | img[3][Qtot*4] | mv[4][Qtot*4] | slack
+// (phase C's sweeps read up to one thread block of quads past an image: the slack keeps the
+// last one inside the allocation)
 size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
   const size_t Qtot = (size_t)n.Lp / 4 + 1;
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
   const size_t o_ctr = take(4 * UPD_CTR_WORDS), o_prof = take(256), o_sq = take(2048 * 4), o_red = take(Qtot * 16),
-               o_part = take((size_t)G * Qtot * 16), o_img = take((size_t)3 * Qtot * 16);
+               o_part = take((size_t)G * Qtot * 16), o_img = take((size_t)3 * Qtot * 16),
+               o_mv = take((size_t)4 * Qtot * 16);
+  (void)take(512 * 16);
   if (ws) {
     ws->ctr = reinterpret_cast<unsigned*>(base + o_ctr);
     ws->prof = reinterpret_cast<unsigned long long*>(base + o_prof);
@@ -1849,6 +2456,7 @@ size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
     ws->red = reinterpret_cast<float*>(base + o_red);
     ws->part = reinterpret_cast<float*>(base + o_part);
     ws->img = reinterpret_cast<float*>(base + o_img);
+    ws->mv = reinterpret_cast<float*>(base + o_mv);
   }
   return off;
 }
@@ -1960,10 +2568,17 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     args.xbuf_self = args.xbuf[dp->rank];
     args.xflag_self = args.xflag[dp->rank];
   }
-  const size_t lds = upd_lds_bytes(args.net, true);
+  args.tp_m0 = ws.mv;
+  args.tp_v0 = ws.mv + L4;
+  args.tp_m1 = ws.mv + 2 * L4;
+  args.tp_v1 = ws.mv + 3 * L4;
+  const bool tp = upd_tp_host(args.R, args.total_steps, dp != nullptr);
+  UpdPlan plan{upd_kernel_for(args.net, dp != nullptr), upd_nw_host(args.net, true), 1};
+  if (tp) plan = upd_tp_plan(args.net);
+  const size_t lds = upd_lds_bytes_plan(args.net, plan.nw, tp, plan.tiles);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_update: %zu B of LDS needed", lds);
   hipStream_t st = as_stream(stream);
-  const void* kern = upd_kernel_for(args.net, dp != nullptr);
+  const void* kern = plan.kern;
   PRL_REQUIRE(kern, "prl_ppo_update: %d parameter quads per thread not built", upd_nq(args.net));
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
@@ -1973,7 +2588,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   hipLaunchKernelGGL(ppo_image_kernel, dim3(img_grid), dim3(UPD_THREADS), 0, st, args.net, params,
                      exp_avg, exp_avg_sq, img_p, img_m, img_v, 1);
   PRL_LAUNCH_CHECK("ppo_image");
-  PRL_HIP_TRY(upd_launch_resident(kern, G, upd_nt(args.net, true), lds, kargs, st));
+  PRL_HIP_TRY(upd_launch_resident(kern, G, 64 * plan.nw, lds, kargs, st));
   hipLaunchKernelGGL(ppo_image_kernel, dim3(img_grid), dim3(UPD_THREADS), 0, st, args.net, params,
                      exp_avg, exp_avg_sq, img_p, img_m, img_v, 0);
   PRL_LAUNCH_CHECK("ppo_image");
@@ -2009,6 +2624,12 @@ extern "C" int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_
   return upd_run(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp,
                  adv, ret, N, mini_batch, k_epochs, clip, vf_coef, ent_coef, lr, beta1, beta2, eps,
                  weight_decay, max_norm, loss_out, workspace, workspace_bytes, stream, &dp);
+}
+
+extern "C" int32_t prl_ppo_update_set_tp(int32_t mode) {
+  const int prev = g_tp_mode;
+  g_tp_mode = (mode >= 0 && mode <= 2) ? mode : 2;
+  return prev;
 }
 
 extern "C" uint32_t prl_dp_set_spin_limit(uint32_t polls) {

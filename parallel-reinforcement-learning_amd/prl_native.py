@@ -71,6 +71,7 @@ SIGNATURES = {
                            _I32, _I32, _P] + [_F32] * 9 + [_P, _I32, _I32, _P, _I64, _P, _I64, _P],
     "prl_dp_xbuf_bytes": [_I32, _I32, _I32, _I32],
     "prl_dp_set_spin_limit": [ctypes.c_uint32],
+    "prl_ppo_update_set_tp": [_I32],
     "prl_dp_xbuf_alloc": [_I64, _P],
     "prl_dp_xbuf_free": [_P],
     "prl_dp_ipc_handle": [_P, _P, _I64],
@@ -88,7 +89,7 @@ SIGNATURES = {
                               + [_I64, _I32, _I64] + [_F32] * 10 + [_P, _P, _P, _I64, _P],
 }
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,
-             "prl_dp_set_spin_limit": ctypes.c_uint32,
+             "prl_dp_set_spin_limit": ctypes.c_uint32, "prl_ppo_update_set_tp": _I32,
              "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
 
 _lib = None
@@ -567,6 +568,12 @@ def dp_set_spin_limit(polls: int) -> int:
     """Polls of the data-parallel launch's cross-rank wait before it times out (0: default);
     returns the previous value."""
     return int(lib().prl_dp_set_spin_limit(int(polls)))
+
+
+def ppo_update_set_tp(mode: int) -> int:
+    """Form of the fused update engine: 0 latency form, 1 throughput form (launches of >= 2
+    steps), 2 auto (default); returns the previous mode.  Both forms give the same bits."""
+    return int(lib().prl_ppo_update_set_tp(int(mode)))
 
 
 def dp_xbuf_alloc(nbytes: int) -> ctypes.c_void_p:

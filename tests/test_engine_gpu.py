@@ -586,3 +586,61 @@ def test_engine_bit_reproducible(cont):
         eng.run(*ins, 3)
         torch.cuda.synchronize()
         assert torch.equal(eng.flat.cpu(), flats[0])
+
+
+@pytest.mark.parametrize("cont", [False, True])
+@pytest.mark.parametrize("mb,N", [(512, 512 * 6 + 7), (8192, 8192 * 3 + 300), (65536, 65536 + 5000)])
+def test_throughput_form_equals_latency_form(cont, mb, N):
+    """The persistent kernel's two forms (prl_ppo_update_set_tp): the latency form (gradient
+    image in LDS, AdamW moments in registers) and the throughput form (gradient in registers,
+    moments streamed through the workspace by the slice owners), at one tile per workgroup
+    (mb 512, the form forced), two (mb 8192) and sixteen (mb 65536, ragged last minibatch).
+    CartPole: both run the 8-wave kernel with the same tiles, order and per-tile sums, so
+    parameters, moments, step count and loss are the same BITS.  Pendulum: the throughput form
+    runs 8 waves (the latency form's LDS image does not fit with 8), so the clip norm is summed
+    in another order (and dW1 accumulates across tiles in the MFMA): float32 rounding apart,
+    checked on the learned function (log-probs / values on probe states, rtol 1e-4) and the
+    moments."""
+    import copy
+    import types
+
+    import prl_native
+    from PPO import PPO
+    D, A = (3, 1) if cont else (4, 2)
+    data = _data(N, D, cont, seed=43)
+    torch.manual_seed(0)
+    p = PPO(cont, D, A, action_scaling=2.0 if cont else None, k_epochs=2, batch_size=64,
+            mini_batch_size=mb)
+    p.show_progress = False
+    eng = p._fused_engine()
+    init = [eng.flat.clone(), eng.m.clone(), eng.v.clone(), eng.step.clone()]
+    p.memory.push_device(*data)
+    p.learn()
+    torch.cuda.synchronize()
+    ins = [x.clone() for x in p._last_update_inputs]
+    outs, pols = {}, {}
+    for mode in (0, 1):
+        prev = prl_native.ppo_update_set_tp(mode)
+        try:
+            for dst, src in zip((eng.flat, eng.m, eng.v, eng.step), init):
+                dst.copy_(src)
+            eng.ws.fill_(0)
+            loss = eng.run(*ins, 2)
+            torch.cuda.synchronize()
+            outs[mode] = [t.cpu().clone() for t in (eng.flat, eng.m, eng.v, eng.step, loss)]
+            # (the policy's parameters alias eng.flat: snapshot them)
+            pols[mode] = types.SimpleNamespace(policy=copy.deepcopy(p.policy))
+        finally:
+            prl_native.ppo_update_set_tp(prev)
+    assert not torch.equal(outs[0][0], init[0].cpu())
+    names = ("params", "exp_avg", "exp_avg_sq", "step", "loss")
+    if not cont:
+        for a, b, name in zip(outs[0], outs[1], names):
+            assert torch.equal(a, b), (name, float((a.double() - b.double()).abs().max()))
+        return
+    _compare_function(pols[0], pols[1], data, rtol=1e-4)
+    assert torch.equal(outs[0][3], outs[1][3])
+    for k in (1, 2):   # moments: float32 rounding of the same steps
+        a, b = outs[0][k].double(), outs[1][k].double()
+        assert float((a - b).abs().max()) <= 1e-3 * float(a.abs().max()) + 1e-12, names[k]
+    assert abs(float(outs[0][4]) - float(outs[1][4])) <= 1e-4 * max(1.0, abs(float(outs[0][4])))
