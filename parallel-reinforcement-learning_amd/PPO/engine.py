@@ -154,6 +154,8 @@ class FusedUpdate:
         self._sync_optimizer_state()
         status = max(prl_native.ppo_update_status(self.ws).tolist())
         if status != 0:
+            # a launch that stopped part-way: start the next one from a clean workspace
+            self.ws.zero_()
             raise RuntimeError(f"prl_ppo_update: in-kernel timeout (status {status}); the policy "
                                "parameters are undefined")
         return self.loss.reshape(())
