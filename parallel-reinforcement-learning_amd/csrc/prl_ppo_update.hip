@@ -363,8 +363,8 @@ struct UpdDist {
 // the persistent kernel (upd_nw);  KA: action dim (0 = runtime).  Specialised kernels keep the
 // per-row code (executed by 16 lanes, but fetched every step) small.
 constexpr bool upd_kd_discrete(int KD) { return KD == 1 || KD == 2; }
-template <int KD, int KA>
-__device__ inline void upd_row_dist(const UpdNet& n, const float* O, const float* act, UpdDist& d) {
+template <int KD, int KA, class OT>
+__device__ inline void upd_row_dist(const UpdNet& n, const OT& O, const float* act, UpdDist& d) {
   const int A = KA > 0 ? KA : n.A;
   const bool discrete = KD >= 0 ? upd_kd_discrete(KD) : (n.discrete != 0);
   d.logp = 0.f;
@@ -425,17 +425,18 @@ __device__ inline void upd_row_dist(const UpdNet& n, const float* O, const float
 }
 
 // Per-row loss (surrogate, prl_loss.hip semantics) and the gradient w.r.t. the head outputs
-// dO[0 .. nout) (dO[nout .. 16) = 0).  lp = {-min(s1, s2), SmoothL1, H}.
-template <int KD, int KA>
-__device__ inline void upd_row_loss(const UpdNet& n, const float* O, const float* rin, float invB,
-                                    float clip, float vf_coef, float* dO, float (&lp)[3]) {
+// dO[0 .. nout) (dO[nout .. 16) = 0).  lp = {-min(s1, s2), SmoothL1, H}.  O / dO: LDS rows (the
+// runtime-layout kernel) or register arrays (the specialised kernels: indices fold to constants).
+template <int KD, int KA, class OT, class DT>
+__device__ inline void upd_row_loss(const UpdNet& n, const OT& O, const float* rin, float invB,
+                                    float clip, float vf_coef, DT& dO, float (&lp)[3]) {
   const int A = KA > 0 ? KA : n.A;
   const bool discrete = KD >= 0 ? upd_kd_discrete(KD) : (n.discrete != 0);
   const int vcol = discrete ? A : 2 * A;      // critic output column
 #pragma unroll
   for (int j = 0; j < UPD_MAXO; ++j) dO[j] = 0.f;
   UpdDist dist;
-  upd_row_dist<KD, KA>(n, O, rin, dist);
+  upd_row_dist<KD, KA, OT>(n, O, rin, dist);
   const float logp = dist.logp, H = dist.H, S2 = dist.S2, qa = dist.qa;
   const int ai = dist.ai;
   const float* p = dist.p;
@@ -526,6 +527,8 @@ __device__ inline float upd_pair_sum(float v) {
 }
 
 typedef float upd_v4 __attribute__((ext_vector_type(4)));
+typedef float upd_f2 __attribute__((ext_vector_type(2)));
+__device__ inline upd_f2 upd_pkfma(upd_f2 a, upd_f2 b, upd_f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ inline upd_v4 upd_mma(float a, float b, upd_v4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -786,6 +789,65 @@ __device__ inline const float* upd_tile_outputs(const UpdNet& n, const float* W,
   }
   return Orow;
 }
+// The same into registers (lanes q == 0; entries past nout undefined): the specialised kernels'
+// loss then reads its outputs without an LDS round trip.
+template <int NW>
+__device__ inline void upd_tile_outputs_reg(const UpdNet& n, const float* W, const UpdScr& sc,
+                                            float (&O)[UPD_MAXO]) {
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4;
+  if (q == 0) {
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      if (4 * j4 < n.nout) {
+        upd_v4 v = upd_ld4(sc.Op + (0 * 16 + x) * 16 + 4 * j4);
+#pragma unroll
+        for (int ww = 1; ww < NW; ++ww) {
+          const upd_v4 p = upd_ld4(sc.Op + (ww * 16 + x) * 16 + 4 * j4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += p[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = 4 * j4 + e;
+          O[j] = j < n.nout ? v[e] + W[upd_bias_of(n, j)] : 0.f;
+        }
+      }
+    }
+  }
+}
+// The row's loss into its dO row of LDS (only the first nout entries are ever read: dW2, dG and
+// the output biases index outputs < nout), 16-B stores; rows past rc get zeros.
+template <int NW, int KD, int KA>
+__device__ inline void upd_tile_loss(const UpdNet& n, const float* W, const UpdScr& sc, int rc,
+                                     float invB, const UpdArgs& args, float (&lp)[3]) {
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  float* dOrow = sc.dOs + (w * 16 + x) * 16;
+  if constexpr (KA > 0) {
+    float O[UPD_MAXO], dO[UPD_MAXO];
+    upd_tile_outputs_reg<NW>(n, W, sc, O);
+    if (q == 0) {
+      if (x < rc) {
+        upd_row_loss<KD, KA>(n, O, sc.Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dO, lp);
+      } else {
+#pragma unroll
+        for (int j = 0; j < UPD_MAXO; ++j) dO[j] = 0.f;
+      }
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4)
+        if (4 * j4 < n.nout) upd_st4(dOrow + 4 * j4, upd_v4{dO[4 * j4], dO[4 * j4 + 1], dO[4 * j4 + 2], dO[4 * j4 + 3]});
+    }
+  } else {
+    const float* Orow = upd_tile_outputs<NW>(n, W, sc);
+    if (q == 0) {
+      if (x < rc) {
+        upd_row_loss<KD, KA>(n, Orow, sc.Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dOrow, lp);
+      } else {
+#pragma unroll
+        for (int j = 0; j < UPD_MAXO; ++j) dOrow[j] = 0.f;
+      }
+    }
+  }
+}
 
 // gradient-image update: the step's first tile stores, later tiles accumulate (first is
 // wave-uniform; every image entry has one owning lane, so the step needs no zeroing pass)
@@ -888,18 +950,9 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
   __syncthreads();   // #1: Op, Rin
   UPD_CMARK(1)
   // ---- loss of row x (lanes q == 0 of every wave, redundantly: each wave needs dO)
-  const float* Orow = upd_tile_outputs<NW>(n, W, sc);
   const float* dOw = sc.dOs + w * 16 * 16;   // [row][j] of this wave
   float lp[3] = {0.f, 0.f, 0.f};
-  if (q == 0) {
-    float* dOrow = sc.dOs + (w * 16 + x) * 16;
-    if (x < rc) {
-      upd_row_loss<KD, KA>(n, Orow, sc.Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dOrow, lp);
-    } else {
-#pragma unroll
-      for (int j = 0; j < UPD_MAXO; ++j) dOrow[j] = 0.f;
-    }
-  }
+  upd_tile_loss<NW, KD, KA>(n, W, sc, rc, invB, args, lp);
   upd_wave_sync();
   UPD_CMARK(2)
   // this wave's [16 rows][16 ch] transpose slots (upd_ts): with one per head, every head stores
@@ -1197,16 +1250,7 @@ __device__ void upd_tileT(const UpdNet& n, const UpdArgs& args, const float* W, 
 #pragma unroll
   for (int u = 0; u < T; ++u) {
     lp[u][0] = lp[u][1] = lp[u][2] = 0.f;
-    const float* Orow = upd_tile_outputs<NW>(n, W, sc[u]);
-    if (q == 0) {
-      float* dOrow = sc[u].dOs + (w * 16 + x) * 16;
-      if (x < rc[u]) {
-        upd_row_loss<KD, KA>(n, Orow, sc[u].Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dOrow, lp[u]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < UPD_MAXO; ++j) dOrow[j] = 0.f;
-      }
-    }
+    upd_tile_loss<NW, KD, KA>(n, W, sc[u], rc[u], invB, args, lp[u]);
   }
   upd_wave_sync();
   UPD_CMARK(2)
@@ -1952,21 +1996,49 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
               v4 = vreg[i];
             }
             const float4 g4 = PARK ? *reinterpret_cast<const float4*>(park + 4 * q) : gq[i];
+            // torch AdamW (decoupled decay; lerp for m; addcmul for v) with fused multiply-adds.
+            // 8 waves: two elements per packed-f32 instruction (v_pk_mul / v_pk_fma: the same
+            // operations per element, so the same bits as the scalar form; sqrt / rcp scalar):
+            // CartPole mb 512 AdamW 1.32 -> 1.23 us; the 4-wave Pendulum kernel (14 quads per
+            // thread) measured slower packed (2.03 -> 2.36 us) and keeps the scalar form
+            if constexpr (NW == 4) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float gr = f4get(g4, e) * clipc;
-              float m = f4get(m4, e), v = f4get(v4, e), p = f4get(pw, e);
-              // torch AdamW (decoupled decay; lerp for m; addcmul for v) with fused multiply-adds
+              for (int e = 0; e < 4; ++e) {
+                const float gr = f4get(g4, e) * clipc;
+                float m = f4get(m4, e), v = f4get(v4, e), p = f4get(pw, e);
+                p = p * decay;
+                m = fmaf(omb1, gr - m, m);
+                v = fmaf(omb2 * gr, gr, v * b2);
+                const float denom = fmaf(__builtin_amdgcn_sqrtf(v), inv_bc2_sqrt, args.eps);
+                float rq = __builtin_amdgcn_rcpf(denom);
+                rq = fmaf(rq, fmaf(-denom, rq, 1.0f), rq);   // one Newton step: ~0.5 ulp
+                p = fmaf(-step_size, m * rq, p);
+                f4set(m4, e, m);
+                f4set(v4, e, v);
+                f4set(pw, e, p);
+              }
+            } else {
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              const upd_f2 gr = upd_f2{f4get(g4, 2 * hh), f4get(g4, 2 * hh + 1)} * clipc;
+              upd_f2 m = upd_f2{f4get(m4, 2 * hh), f4get(m4, 2 * hh + 1)};
+              upd_f2 v = upd_f2{f4get(v4, 2 * hh), f4get(v4, 2 * hh + 1)};
+              upd_f2 p = upd_f2{f4get(pw, 2 * hh), f4get(pw, 2 * hh + 1)};
               p = p * decay;
-              m = fmaf(omb1, gr - m, m);
-              v = fmaf(omb2 * gr, gr, v * b2);
-              const float denom = fmaf(__builtin_amdgcn_sqrtf(v), inv_bc2_sqrt, args.eps);
-              float rq = __builtin_amdgcn_rcpf(denom);
-              rq = fmaf(rq, fmaf(-denom, rq, 1.0f), rq);   // one Newton step: ~0.5 ulp
-              p = fmaf(-step_size, m * rq, p);
-              f4set(m4, e, m);
-              f4set(v4, e, v);
-              f4set(pw, e, p);
+              m = upd_pkfma(upd_f2{omb1, omb1}, gr - m, m);
+              v = upd_pkfma((upd_f2)(omb2 * gr), gr, v * b2);
+              const upd_f2 sq{__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
+              const upd_f2 denom = upd_pkfma(sq, upd_f2{inv_bc2_sqrt, inv_bc2_sqrt}, upd_f2{args.eps, args.eps});
+              upd_f2 rq{__builtin_amdgcn_rcpf(denom.x), __builtin_amdgcn_rcpf(denom.y)};
+              rq = upd_pkfma(rq, upd_pkfma(-denom, rq, upd_f2{1.0f, 1.0f}), rq);   // one Newton step: ~0.5 ulp
+              p = upd_pkfma(upd_f2{-step_size, -step_size}, m * rq, p);
+              f4set(m4, 2 * hh, m.x);
+              f4set(m4, 2 * hh + 1, m.y);
+              f4set(v4, 2 * hh, v.x);
+              f4set(v4, 2 * hh + 1, v.y);
+              f4set(pw, 2 * hh, p.x);
+              f4set(pw, 2 * hh + 1, p.y);
+            }
             }
             if constexpr (TP) {
               if (q >= (int)((int64_t)Qtot * g / G) && q < (int)((int64_t)Qtot * (g + 1) / G)) {   // my slice
