@@ -654,9 +654,15 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
             const bool mine = jA >= hi.oc && jA < hi.oc + hi.no;
             const float* wr = W + hi.Lw2 + (mine ? jA - hi.oc : 0) * WD_HS;
             const float* gr = Gs + x * WD_GS + 64 * h;
+            // K order per step (sg, i): lane q <-> channel 16 sg + 4 q + i, so each operand is
+            // one 16-B LDS read per four MFMAs (was a 4-B read per MFMA and operand)
 #pragma unroll
-            for (int s = 0; s < 16; ++s)
-              o = wd_mma(mine ? wr[4 * s + q] : 0.f, gr[4 * s + q], o);
+            for (int sg = 0; sg < 4; ++sg) {
+              const wd_v4 av = mine ? wd_ld4(wr + 16 * sg + 4 * q) : z4;
+              const wd_v4 bv = wd_ld4(gr + 16 * sg + 4 * q);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) o = wd_mma(av[i], bv[i], o);
+            }
           }
         }
       }
