@@ -58,7 +58,7 @@ struct WdNet {
   int Lg0, Lb0, Lw1[WD_MAXH], Lg1[WD_MAXH], Lb1[WD_MAXH], Lw2[WD_MAXH], Lb2[WD_MAXH], Lp;
 };
 
-bool wd_layout(int D, int A, int discrete, WdNet& n) {
+__host__ __device__ constexpr bool wd_layout(int D, int A, int discrete, WdNet& n) {
   n = WdNet{};
   if (D < 1 || A < 1 || A > WD_MAXA) return false;
   n.D = D;
@@ -101,6 +101,14 @@ bool wd_layout(int D, int A, int discrete, WdNet& n) {
   n.Lp = lds;
   return true;
 }
+__host__ __device__ constexpr WdNet wd_make(int D, int A, int discrete) {
+  WdNet n{};
+  wd_layout(D, A, discrete, n);
+  return n;
+}
+// the specialised shape: C5's Humanoid-shaped net (D 348, A 17, continuous): its whole layout a
+// compile-time constant (every LDS / flat offset an immediate, no net struct in SGPRs)
+constexpr int WD_C5_D = 348, WD_C5_A = 17;
 
 // tile scratch after the parameter image (floats)
 __host__ __device__ inline int wd_xs(int KSM) { return 4 * KSM + 4; }   // X row stride (== 4 mod 32)
@@ -456,12 +464,11 @@ __device__ inline void wd_stage_x(const WdNet& n, const WdArgs& a, int64_t row0,
 // all N rows, writing each row's log-prob and value instead of a gradient — PPO.learn's
 // policy_old pass for the rows the wide step then updates on, so the first minibatch's ratio is
 // exactly 1 (as in the reference, where both come from one get_evaluate).
-template <int KSM, bool SPLIT, bool EVAL = false>
-__global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) {
+template <int KSM, bool SPLIT, bool EVAL>
+__device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs& a) {
   constexpr int KE = SPLIT ? 1 : KSM / 4;   // 16-column blocks of dW0
   extern __shared__ float4 wd_lds4[];
   float* lds = reinterpret_cast<float*>(wd_lds4);
-  const WdNet& n = a.net;
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   const int D = n.D, nh = n.nh;
   // X buffers: row stride D (unpadded, global_load_lds prefetch) when D % 4 == 0 and S is 16-B
@@ -937,6 +944,17 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
   }
 }
 
+// KSPEC: the C5 specialisation (constexpr layout); else the runtime layout from the argument
+template <int KSM, bool SPLIT, bool EVAL = false, bool KSPEC = false>
+__global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) {
+  if constexpr (KSPEC) {
+    constexpr WdNet N = wd_make(WD_C5_D, WD_C5_A, 0);
+    ppo_wide_grad_body<KSM, SPLIT, EVAL>(N, a);
+  } else {
+    ppo_wide_grad_body<KSM, SPLIT, EVAL>(a.net, a);
+  }
+}
+
 // Split form, second pass: dW0[c][d] = sum over the minibatch's rows of dH0[row][c] X[row][d]
 // (K = rows).  Workgroup g takes 32-row tiles g, g + G2, ...; wave w owns channels 16w .. 16w+15
 // (22 16 x 16 accumulators for D = 348).  The next tile's X and dH0 rows are loaded into
@@ -1116,6 +1134,14 @@ __global__ __launch_bounds__(256) void ppo_wide_reduce_kernel(const float* __res
 
 // KSM instantiated for D <= 128 and D <= 352
 int wd_ksm(int D) { return D <= 128 ? 32 : (D <= 352 ? 88 : 0); }
+// the constexpr-layout kernel runs this shape (PRL_WIDE_SPEC=0: the runtime-layout kernel, A/B)
+bool wd_spec(const WdNet& n) {
+  static const bool on = [] {
+    const char* e = getenv("PRL_WIDE_SPEC");
+    return !(e && e[0] == '0');
+  }();
+  return on && n.D == WD_C5_D && n.A == WD_C5_A && !n.discrete;
+}
 
 int wd_grid(int64_t mb);
 int wd_grid2(int64_t mb) {
@@ -1183,20 +1209,22 @@ extern "C" int prl_ppo_wide_evaluate(const float* params, int32_t D, int32_t A, 
   a.eval_logp = logp_out;
   a.eval_V = V_out;
   hipStream_t st = as_stream(stream);
-  static unsigned long long lds_set[2] = {0ull, 0ull};   // bit = device ordinal
+  static unsigned long long lds_set[3] = {0ull, 0ull, 0ull};   // bit = device ordinal
   int dev_ord = 0;
   PRL_HIP_TRY(hipGetDevice(&dev_ord));
   const unsigned long long dev_bit = 1ull << (dev_ord & 63);
-#define WD_ELAUNCH(K, slot)                                                                       \
+#define WD_ELAUNCH(K, SPEC, slot)                                                                 \
   do {                                                                                         \
     if (!(lds_set[slot] & dev_bit)) {                                                          \
-      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<K, true, true>), \
+      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<K, true, true, SPEC>), \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));   \
       lds_set[slot] |= dev_bit;                                                                \
     }                                                                                          \
-    hipLaunchKernelGGL((ppo_wide_grad_kernel<K, true, true>), dim3(a.G), dim3(WD_THREADS), lds, st, a); \
+    hipLaunchKernelGGL((ppo_wide_grad_kernel<K, true, true, SPEC>), dim3(a.G), dim3(WD_THREADS), lds, st, a); \
   } while (0)
-  if (KSM == 32) WD_ELAUNCH(32, 0); else WD_ELAUNCH(88, 1);
+  if (KSM == 32) WD_ELAUNCH(32, false, 0);
+  else if (wd_spec(n)) WD_ELAUNCH(88, true, 2);
+  else WD_ELAUNCH(88, false, 1);
 #undef WD_ELAUNCH
   PRL_LAUNCH_CHECK("ppo_wide_evaluate");
   return PRL_OK;
@@ -1264,23 +1292,25 @@ extern "C" int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A,
   hipStream_t st = as_stream(stream);
   // the kernels' dynamic-LDS limit is raised once per process AND device (the attribute is
   // per device; not a stream operation, but kept out of the per-step path that graphs capture)
-  static unsigned long long lds_set[4] = {0ull, 0ull, 0ull, 0ull};   // bit = device ordinal
+  static unsigned long long lds_set[5] = {0ull, 0ull, 0ull, 0ull, 0ull};   // bit = device ordinal
   int dev_ord = 0;
   PRL_HIP_TRY(hipGetDevice(&dev_ord));
   const unsigned long long dev_bit = 1ull << (dev_ord & 63);
-#define WD_LAUNCH(K, SP, slot)                                                                  \
+#define WD_LAUNCH(K, SP, SPEC, slot)                                                            \
   do {                                                                                       \
     if (!(lds_set[slot] & dev_bit)) {                                                        \
-      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<K, SP>), \
+      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<K, SP, false, SPEC>), \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); \
       lds_set[slot] |= dev_bit;                                                              \
     }                                                                                        \
-    hipLaunchKernelGGL((ppo_wide_grad_kernel<K, SP>), dim3(G), dim3(WD_THREADS), lds, st, a);  \
+    hipLaunchKernelGGL((ppo_wide_grad_kernel<K, SP, false, SPEC>), dim3(G), dim3(WD_THREADS), lds, st, a); \
   } while (0)
   if (KSM == 32) {
-    if (split) WD_LAUNCH(32, true, 0); else WD_LAUNCH(32, false, 1);
+    if (split) WD_LAUNCH(32, true, false, 0); else WD_LAUNCH(32, false, false, 1);
+  } else if (wd_spec(n) && split) {
+    WD_LAUNCH(88, true, true, 4);
   } else {
-    if (split) WD_LAUNCH(88, true, 2); else WD_LAUNCH(88, false, 3);
+    if (split) WD_LAUNCH(88, true, false, 2); else WD_LAUNCH(88, false, false, 3);
   }
 #undef WD_LAUNCH
   PRL_LAUNCH_CHECK("ppo_wide_grad");
