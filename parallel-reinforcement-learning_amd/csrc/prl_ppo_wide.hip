@@ -964,14 +964,13 @@ __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) 
 constexpr int WD2_GRID_MAX = 256;
 constexpr int WD2_RT = 32;
 template <int KSM>
-__global__ __launch_bounds__(WD_THREADS, 2) void ppo_wide_dw0_kernel(WdArgs a, float* part2, int G2) {
+__device__ __forceinline__ void ppo_wide_dw0_body(const WdNet& n, const WdArgs& a, float* part2, int G2) {
   constexpr int KE = KSM / 4;
   constexpr int XS2 = 4 * KSM + 4;
   constexpr int HS = 68;
   constexpr int NPF = (WD2_RT * 4 * KSM / 4 + WD_THREADS - 1) / WD_THREADS;   // float4 per thread
   __shared__ float Xs[WD2_RT * XS2];
   __shared__ float Hs[WD2_RT * HS];
-  const WdNet& n = a.net;
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   const int D = n.D;
   const int64_t j = *a.cursor;
@@ -1061,6 +1060,15 @@ __global__ __launch_bounds__(WD_THREADS, 2) void ppo_wide_dw0_kernel(WdArgs a, f
 #pragma unroll
       for (int i = 0; i < 4; ++i) out[(16 * w + 4 * q + i) * D + d] = acc[e][i];
     }
+  }
+}
+template <int KSM, bool KSPEC = false>
+__global__ __launch_bounds__(WD_THREADS, 2) void ppo_wide_dw0_kernel(WdArgs a, float* part2, int G2) {
+  if constexpr (KSPEC) {
+    constexpr WdNet N = wd_make(WD_C5_D, WD_C5_A, 0);
+    ppo_wide_dw0_body<KSM>(N, a, part2, G2);
+  } else {
+    ppo_wide_dw0_body<KSM>(a.net, a, part2, G2);
   }
 }
 
@@ -1323,7 +1331,10 @@ extern "C" int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A,
     if (KSM == 32)
       hipLaunchKernelGGL(ppo_wide_dw0_kernel<32>, dim3(G2), dim3(WD_THREADS), 0, st, a, part2, G2);
     else
-      hipLaunchKernelGGL(ppo_wide_dw0_kernel<88>, dim3(G2), dim3(WD_THREADS), 0, st, a, part2, G2);
+      if (wd_spec(n))
+        hipLaunchKernelGGL((ppo_wide_dw0_kernel<88, true>), dim3(G2), dim3(WD_THREADS), 0, st, a, part2, G2);
+      else
+        hipLaunchKernelGGL((ppo_wide_dw0_kernel<88, false>), dim3(G2), dim3(WD_THREADS), 0, st, a, part2, G2);
     PRL_LAUNCH_CHECK("ppo_wide_dw0");
     const int P2 = WD_H * n.D;   // 64 D: a multiple of 4
     hipLaunchKernelGGL(ppo_wide_reduce_kernel, dim3((unsigned)cdiv((P2 + 4) / 4, WR_QUADS)), dim3(256),
