@@ -1076,11 +1076,16 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
         if (h < nh) {
           const float* Zh = sc.Zs + h * UPD_RT * UPD_ZS + x * UPD_ZS;
           const float* Wh = W + n.w1[h].lds + 16 * b + x;
+          // the B operands of a lane's 16 steps are 4 runs of 4 consecutive channels: four
+          // 16-B reads up front (same steps, same order)
+          upd_v4 zb[4];
+#pragma unroll
+          for (int sg = 0; sg < 4; ++sg) zb[sg] = upd_ld4(Zh + 16 * sg + 4 * q);
 #pragma unroll
           for (int s = 0; s < 16; ++s) {
             const int o = 16 * (s & 3) + 4 * q + (s >> 2);
-            if (s & 1) d1 = upd_mma(Wh[o * UPD_HS], Zh[o], d1);
-            else d0 = upd_mma(Wh[o * UPD_HS], Zh[o], d0);
+            if (s & 1) d1 = upd_mma(Wh[o * UPD_HS], zb[s & 3][s >> 2], d1);
+            else d0 = upd_mma(Wh[o * UPD_HS], zb[s & 3][s >> 2], d0);
           }
         }
       }

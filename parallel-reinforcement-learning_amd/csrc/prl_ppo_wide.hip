@@ -814,11 +814,15 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
           const WdHead hi = wd_head(n, h);
           const float* Zh = Zs + h * WD_RT * WD_FS + x * WD_FS;
           const float* Wh = W + hi.Lw1 + 16 * w + x;
+          // B operands: four 16-B reads up front (a lane's steps read 4 runs of 4 channels)
+          wd_v4 zb[4];
+#pragma unroll
+          for (int sg = 0; sg < 4; ++sg) zb[sg] = wd_ld4(Zh + 16 * sg + 4 * q);
 #pragma unroll
           for (int s = 0; s < 16; ++s) {
             const int o = 16 * (s & 3) + 4 * q + (s >> 2);
-            if (s & 1) d1 = wd_mma(Wh[o * WD_HS], Zh[o], d1);
-            else d0 = wd_mma(Wh[o * WD_HS], Zh[o], d0);
+            if (s & 1) d1 = wd_mma(Wh[o * WD_HS], zb[s & 3][s >> 2], d1);
+            else d0 = wd_mma(Wh[o * WD_HS], zb[s & 3][s >> 2], d0);
           }
         }
       }
