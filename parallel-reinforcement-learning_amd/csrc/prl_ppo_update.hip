@@ -1153,287 +1153,6 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
 #undef UPD_CMARK
 }
 
-// T tiles in flight (the throughput form of the 4-wave kernels): upd_tile's stages, each run for
-// tiles u = 0 .. T-1 back to back (innermost where chains are independent), so one tile's
-// latency-bound stretches (the per-row loss, GroupNorm, LDS transposes) issue between the other's
-// MFMAs, and the three workgroup barriers are paid once per T tiles.  Every gradient entry still
-// adds its per-tile sums in tile order, so the bits equal T sequential upd_tile<.., RG> calls.
-// A tile with rc = 0 (odd tile count) runs on zero inputs and adds exact zeros.  Scratch sc[u]
-// per tile (the caller alternates the trunk-output buffers between groups).
-template <int KD, int KA, int T>
-__device__ void upd_tileT(const UpdNet& n, const UpdArgs& args, const float* W, const UpdScr* sc,
-                          const UpdIn<upd_ksm<KA>()>* in, const int* rc, float invB,
-                          unsigned long long* tm, UpdGradOf<KD, KA>& gr) {
-  constexpr int KSM = upd_ksm<KA>(), NW = 4, HPW = UPD_MAXH;
-  static_assert(upd_nw<KD, KA>() == 4, "the T-tile form runs the 4-wave kernels");
-  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
-  const int b = w;
-  const int D = n.D, KS = (D + 3) >> 2;
-  const int nh = upd_nh<KD>(n);
-  const bool timer = args.profile && blockIdx.x == 0 && t == 0;
-  unsigned long long tl = timer ? __builtin_amdgcn_s_memrealtime() : 0ull;
-#define UPD_CMARK(i)                                                   \
-  if (timer) {                                                         \
-    const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();  \
-    tm[i] += now_ - tl;                                                \
-    tl = now_;                                                         \
-  }
-  UpdFwd<KSM, HPW> f[T];
-  // ---- trunk block b of every tile -> Fs
-#pragma unroll
-  for (int u = 0; u < T; ++u) {
-    upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* wr = W + n.w0.lds + (16 * b + x) * n.w0.stride;
-#pragma unroll
-    for (int s = 0; s < KSM; ++s) {
-      if (s < KS) {
-        const int d = 4 * s + q;
-        acc = upd_mma(d < D ? wr[d] : 0.0f, in[u].xin[s], acc);
-      }
-    }
-    upd_gn_fwd_frag(acc, upd_ld4(W + n.g0.lds + 16 * b + 4 * q), upd_ld4(W + n.b0.lds + 16 * b + 4 * q),
-                    f[u].xh0, f[u].r0, f[u].Fw);
-    upd_st4(sc[u].Fs + x * UPD_ZS + 16 * b + 4 * q, f[u].Fw);
-  }
-  __syncthreads();   // #0: Fs
-  // ---- heads and the output layer's partial over block b
-  {
-    upd_v4 F[T][4], z[T][HPW];
-#pragma unroll
-    for (int u = 0; u < T; ++u) {
-#pragma unroll
-      for (int bb = 0; bb < 4; ++bb) F[u][bb] = upd_ld4(sc[u].Fs + x * UPD_ZS + 16 * bb + 4 * q);
-#pragma unroll
-      for (int hs = 0; hs < HPW; ++hs) z[u][hs] = upd_v4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
-#pragma unroll
-      for (int hs = 0; hs < HPW; ++hs) {
-        if (hs < nh) {
-          const UpdHead hi = upd_head_info(n, hs);
-          const upd_v4 wa = upd_ld4(W + hi.w1 + (16 * b + x) * UPD_HS + 16 * bb + 4 * q);
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int u = 0; u < T; ++u) z[u][hs] = upd_mma(wa[e], F[u][bb][e], z[u][hs]);
-        }
-      }
-    }
-    upd_v4 o[T];
-#pragma unroll
-    for (int u = 0; u < T; ++u) o[u] = upd_v4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int hs = 0; hs < HPW; ++hs) {
-      if (hs < nh) {
-        const UpdHead hi = upd_head_info(n, hs);
-        const upd_v4 gw = upd_ld4(W + hi.g1 + 16 * b + 4 * q), gb = upd_ld4(W + hi.b1 + 16 * b + 4 * q);
-        const int oc = hi.oc, no = hi.no;
-        const bool mine = x >= oc && x < oc + no;
-        const upd_v4 wv = mine ? upd_ld4(W + hi.w2 + (x - oc) * UPD_HS + 16 * b + 4 * q)
-                               : upd_v4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < T; ++u)
-          upd_gn_fwd_frag(z[u][hs], gw, gb, f[u].xh[hs], f[u].rh[hs], f[u].G[hs]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int u = 0; u < T; ++u) o[u] = upd_mma(wv[e], f[u].G[hs][e], o[u]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < T; ++u) {
-      upd_st4(sc[u].Op + (w * 16 + x) * 16 + 4 * q, o[u]);
-      if (t < UPD_RT * UPD_RIN) sc[u].Rin[t] = in[u].rin;
-    }
-  }
-  UPD_CMARK(0)
-  __syncthreads();   // #1: Op, Rin
-  UPD_CMARK(1)
-  // ---- loss of row x of every tile (lanes q == 0 of every wave)
-  float lp[T][3];
-#pragma unroll
-  for (int u = 0; u < T; ++u) {
-    lp[u][0] = lp[u][1] = lp[u][2] = 0.f;
-    upd_tile_loss<NW, KD, KA>(n, W, sc[u], rc[u], invB, args, lp[u]);
-  }
-  upd_wave_sync();
-  UPD_CMARK(2)
-  const int TS = upd_ts(n);
-  float* Tw[T];
-#pragma unroll
-  for (int u = 0; u < T; ++u) {
-    Tw[u] = sc[u].Ts + w * TS * UPD_RT * 16;
-#pragma unroll
-    for (int hs = 0; hs < HPW; ++hs)
-      if (hs < TS && hs < nh) upd_st4(Tw[u] + hs * UPD_RT * 16 + x * 16 + 4 * q, f[u].G[hs]);
-  }
-  upd_wave_sync();
-  // ---- heads backward: dW2, dG -> GroupNorm + SiLU backward -> dZ (Zs), GN column sums
-#pragma unroll
-  for (int hs = 0; hs < HPW; ++hs) {
-    if (hs < nh) {
-      const UpdHead hi = upd_head_info(n, hs);
-      const int oc = hi.oc, no = hi.no;
-      const int slot = TS == 1 ? 0 : hs;
-      if (hs >= TS) {   // the shared slot is free once the previous head has read it
-        upd_wave_sync();
-#pragma unroll
-        for (int u = 0; u < T; ++u) upd_st4(Tw[u] + x * 16 + 4 * q, f[u].G[hs]);
-        upd_wave_sync();
-      }
-      const upd_v4 gw = upd_ld4(W + hi.g1 + 16 * b + 4 * q), gb = upd_ld4(W + hi.b1 + 16 * b + 4 * q);
-      upd_v4 acc[T], dg[T];
-#pragma unroll
-      for (int u = 0; u < T; ++u) acc[u] = dg[u] = upd_v4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-#pragma unroll
-        for (int u = 0; u < T; ++u) {
-          const float* dOw = sc[u].dOs + w * 16 * 16;
-          const float a = x < no ? dOw[(4 * s + q) * 16 + oc + x] : 0.0f;
-          acc[u] = upd_mma(a, Tw[u][slot * UPD_RT * 16 + (4 * s + q) * 16 + x], acc[u]);
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < UPD_MAXA / 4; ++s) {
-        if (4 * s < no) {
-          const int j = 4 * s + q;
-          const float a = j < no ? W[hi.w2 + j * UPD_HS + 16 * b + x] : 0.0f;
-#pragma unroll
-          for (int u = 0; u < T; ++u) {
-            const float* dOw = sc[u].dOs + w * 16 * 16;
-            dg[u] = upd_mma(a, j < no ? dOw[x * 16 + oc + j] : 0.0f, dg[u]);
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < T; ++u) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (i < upd_nomax(n)) gr.w2[hs][i] += acc[u][i];
-        upd_v4 dy;
-        const upd_v4 dz = upd_gn_bwd_frag(dg[u], f[u].xh[hs], gw, gb, f[u].rh[hs], dy);
-        upd_st4(sc[u].Zs + hs * UPD_RT * UPD_ZS + x * UPD_ZS + 16 * b + 4 * q, dz);
-        upd_v4 dyx;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dyx[i] = dy[i] * f[u].xh[hs][i];
-        upd_colsum_acc(dyx, gr, 8 * hs);
-        upd_colsum_acc(dy, gr, 8 * hs + 4);
-      }
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < T; ++u)
-#pragma unroll
-    for (int s = 0; s < KSM; ++s)
-      if (s < KS && (s % NW) == w) sc[u].Xs[x * sc[u].XS + 4 * s + q] = in[u].xin[s];
-  UPD_CMARK(3)
-  __syncthreads();   // #2: Zs, Fs, Xs
-  UPD_CMARK(4)
-  // ---- dW1_h[16b + 4q + i][16bb + x] += sum_rows dZ_h[row][out] F[row][in]
-#pragma unroll
-  for (int h = 0; h < UPD_MAXH; ++h) {
-    if (h < nh) {
-      upd_v4 acc[T][4];
-#pragma unroll
-      for (int u = 0; u < T; ++u)
-#pragma unroll
-        for (int bb = 0; bb < 4; ++bb) acc[u][bb] = upd_v4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-#pragma unroll
-        for (int u = 0; u < T; ++u) {
-          const float a = sc[u].Zs[h * UPD_RT * UPD_ZS + (4 * s + q) * UPD_ZS + 16 * b + x];
-#pragma unroll
-          for (int bb = 0; bb < 4; ++bb)
-            acc[u][bb] = upd_mma(a, sc[u].Fs[(4 * s + q) * UPD_ZS + 16 * bb + x], acc[u][bb]);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < T; ++u)
-#pragma unroll
-        for (int bb = 0; bb < 4; ++bb) gr.w1(h, bb) += acc[u][bb];
-    }
-  }
-  UPD_CMARK(5)
-  // ---- dF^T block b = sum_h W1_h^T dZ_h^T, trunk GroupNorm + SiLU backward, its column sums
-  upd_v4 dH0[T];
-  {
-    upd_v4 d0[T], d1[T];
-#pragma unroll
-    for (int u = 0; u < T; ++u) d0[u] = d1[u] = upd_v4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int h = 0; h < UPD_MAXH; ++h) {
-      if (h < nh) {
-        const float* Wh = W + n.w1[h].lds + 16 * b + x;
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const int o = 16 * (s & 3) + 4 * q + (s >> 2);
-          const float a = Wh[o * UPD_HS];
-#pragma unroll
-          for (int u = 0; u < T; ++u) {
-            const float zb = sc[u].Zs[h * UPD_RT * UPD_ZS + x * UPD_ZS + o];
-            if (s & 1) d1[u] = upd_mma(a, zb, d1[u]);
-            else d0[u] = upd_mma(a, zb, d0[u]);
-          }
-        }
-      }
-    }
-    const upd_v4 g0w = upd_ld4(W + n.g0.lds + 16 * b + 4 * q), g0b = upd_ld4(W + n.b0.lds + 16 * b + 4 * q);
-#pragma unroll
-    for (int u = 0; u < T; ++u) {
-      upd_v4 dF, dy0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dF[i] = d0[u][i] + d1[u][i];
-      dH0[u] = upd_gn_bwd_frag(dF, f[u].xh0, g0w, g0b, f[u].r0, dy0);
-      upd_v4 dyx;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dyx[i] = dy0[i] * f[u].xh0[i];
-      upd_colsum_acc(dyx, gr, 8 * HPW);
-      upd_colsum_acc(dy0, gr, 8 * HPW + 4);
-    }
-  }
-  UPD_CMARK(6)
-  // ---- dW0[16b + 4q + i][16e + x] += sum_rows dH0[row][ch] X[row][d]  (dH0 transposed via Tw)
-#pragma unroll
-  for (int u = 0; u < T; ++u) upd_st4(Tw[u] + x * 16 + 4 * q, dH0[u]);
-  upd_wave_sync();
-#pragma unroll
-  for (int e = 0; e < (KSM + 3) / 4; ++e) {
-    if (16 * e < D) {
-      const int d = 16 * e + x;
-      upd_v4 acc[T];
-#pragma unroll
-      for (int u = 0; u < T; ++u) acc[u] = upd_v4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int u = 0; u < T; ++u)
-          acc[u] = upd_mma(Tw[u][(4 * s + q) * 16 + x], d < D ? sc[u].Xs[(4 * s + q) * sc[u].XS + d] : 0.0f, acc[u]);
-#pragma unroll
-      for (int u = 0; u < T; ++u) gr.w0(e) += acc[u];
-    }
-  }
-  // ---- output biases and loss partials (the last wave)
-  if (w == NW - 1) {
-#pragma unroll
-    for (int u = 0; u < T; ++u) {
-      if (l < n.nout) {   // f64 sum: the softmax outputs' dO cancel across rows
-        const float* dOw = sc[u].dOs + w * 16 * 16;
-        double acc = 0.0;
-#pragma unroll
-        for (int r = 0; r < UPD_RT; ++r) acc += (double)dOw[r * 16 + l];
-        gr.bias += (float)acc;
-      }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) gr.loss[k] += upd_rsum16(lp[u][k]);
-    }
-  }
-  UPD_CMARK(7)
-#undef UPD_CMARK
-}
-
 // TP: store this lane's register gradient into the workgroup's partial (rs = its base), at the
 // image entries the LDS form would have written (the others were zeroed at launch start).
 // Lanes x of one register i store 16 consecutive words.
@@ -1718,13 +1437,11 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
 // registers (UpdGrad, no LDS image) and the moments streamed from device memory in phase C
 // instead of held in registers — the owner of each slice writes its new moments to the other of
 // two buffers (the step's source for the next step) — so the tiles run with ~110 more registers
-// and without the image's LDS traffic.  Needs >= 2 steps (upd_run).  TPM = T >= 2: T tiles in
-// flight per wave (upd_tileT; 4-wave kernels), T scratch regions.
+// and without the image's LDS traffic.  Needs >= 2 steps (upd_run).  TPM: 1 = the throughput form.
 template <int NQ, int KD, int KA, bool DP, int TPM = 0>
 __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& args) {
   constexpr int NW = upd_nw<KD, KA>(), NT = 64 * NW;
   constexpr bool TP = TPM > 0;
-  constexpr int TT = TPM > 1 ? TPM : 1;   // tiles in flight
   extern __shared__ __align__(16) float upd_lds[];
   const int t = threadIdx.x, g = blockIdx.x, G = args.G;
   const int Lp = n.Lp;
@@ -1736,12 +1453,9 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
   // (no base registers kept live across the step loop)
   float* scratch = upd_lds + UPD_HDR;                                   // tile activations
   const int scr_floats = (upd_scratch_floats(n.D, NW, upd_ts(n)) + 3) & ~3;
-  float* W = scratch + TT * scr_floats;                                  // [Lp]
+  float* W = scratch + scr_floats;                                       // [Lp]
   float* Ga = W + Lp;                                                    // [Lp + 4]
   const UpdScr sc = upd_scr(scratch, n.D, NW);
-  UpdScr scT[TT];
-#pragma unroll
-  for (int u = 0; u < TT; ++u) scT[u] = upd_scr(scratch + u * scr_floats, n.D, NW);
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
   float* s_adam = hdr + 10;         // [2] this step's AdamW step size, 1 / sqrt(bc2)
 
@@ -1794,19 +1508,11 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       pts[7] = now;
     }
   };
-  UpdIn<upd_ksm<KA>()> nin[TT];   // inputs of the next tile(s) to run (prefetched)
-  // load the TT tiles from row0 (rows_left rows of this workgroup's share from there on; with
-  // TT > 1 a tile past them loads zeros and runs as a zero tile)
+  UpdIn<upd_ksm<KA>()> nin[1];   // inputs of the next tile to run (prefetched)
+  // load the tile at row0 (rows_left rows of this workgroup's share from there on)
   auto load_next = [&](int64_t row0, int rows_left) {
-    if constexpr (TT == 1) {
-      upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret, row0,
-                            std::min(UPD_RT, rows_left), nin[0]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < TT; ++u)
-        upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret, row0 + u * UPD_RT,
-                              std::max(0, std::min(UPD_RT, rows_left - u * UPD_RT)), nin[u]);
-    }
+    upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret, row0,
+                          std::min(UPD_RT, rows_left), nin[0]);
   };
   unsigned long long* const tm = reinterpret_cast<unsigned long long*>(hdr + 16);
   for (int s = 0; s < args.total_steps; ++s) {
@@ -1824,36 +1530,19 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     if (!TP && myrows == 0) {   // no rows this step: publish zeros
       for (int k = t; k < Lp + 4; k += NT) Ga[k] = 0.0f;
     }
-    if constexpr (TT > 1) {
-      for (int c0 = 0; c0 < myrows; c0 += TT * UPD_RT) {
-        UpdIn<upd_ksm<KA>()> cur[TT];
-        int rcs[TT];
-        UpdScr scg[TT];
-#pragma unroll
-        for (int u = 0; u < TT; ++u) {
-          cur[u] = nin[u];
-          rcs[u] = std::max(0, std::min(UPD_RT, myrows - c0 - u * UPD_RT));
-          scg[u] = upd_scr_tile(scT[u], c0 / (TT * UPD_RT));   // trunk buffers alternate by group
-        }
-        if (c0 + TT * UPD_RT < myrows)   // prefetch the next group of this step
-          load_next(myrow0 + c0 + TT * UPD_RT, myrows - c0 - TT * UPD_RT);
-        upd_tileT<KD, KA, TT>(n, args, W, scg, cur, rcs, invB, tm, gr);
-      }
-    } else {
-      for (int c0 = 0; c0 < myrows; c0 += UPD_RT) {
-        const UpdIn<upd_ksm<KA>()> cur = nin[0];
-        if (c0 + UPD_RT < myrows)   // prefetch the next tile of this step
-          load_next(myrow0 + c0 + UPD_RT, myrows - c0 - UPD_RT);
-        if constexpr (TP)
-          upd_tile<KD, KA, false, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0),
-                                        invB, tm, gr);
-        else if (c0 == 0)
-          upd_tile<KD, KA, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0), invB,
-                                 tm, gr);
-        else
-          upd_tile<KD, KA, false>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0), invB,
-                                  tm, gr);
-      }
+    for (int c0 = 0; c0 < myrows; c0 += UPD_RT) {
+      const UpdIn<upd_ksm<KA>()> cur = nin[0];
+      if (c0 + UPD_RT < myrows)   // prefetch the next tile of this step
+        load_next(myrow0 + c0 + UPD_RT, myrows - c0 - UPD_RT);
+      if constexpr (TP)
+        upd_tile<KD, KA, false, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0),
+                                      invB, tm, gr);
+      else if (c0 == 0)
+        upd_tile<KD, KA, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0), invB,
+                               tm, gr);
+      else
+        upd_tile<KD, KA, false>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0), invB,
+                                tm, gr);
     }
     if constexpr (!TP) __syncthreads();
     mark(0);   // phase A compute
@@ -2432,36 +2121,26 @@ const void* upd_kernel_for(const UpdNet& n, bool dp = false) {
   if (nq <= 20) return reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0>);
   return nullptr;
 }
-// The throughput form's kernel for this shape: T = 2 tiles in flight on the 4-wave kernels
-// (PRL_UPD_T=1: one tile, and CartPole's 8-wave head-split kernel); the runtime-layout kernel
-// runs one tile (it spills registers already).
+// The throughput form's kernel for this shape: the 8-wave head-split kernels for CartPole and
+// Pendulum (PRL_UPD_WAVES=4: the 4-wave ones); none for other shapes (null: the latency form).
 struct UpdPlan {
   const void* kern;
   int nw, tiles;
 };
-int g_tp_tiles = [] {
-  const char* e = getenv("PRL_UPD_T");
-  return (e && e[0] == '2') ? 2 : 1;
-}();
 UpdPlan upd_tp_plan(const UpdNet& n) {
   const int qp = n.Lp / 4;
-  const bool two = g_tp_tiles == 2;
   if (!upd_force_generic()) {
-    if (upd_is_cartpole(n) && two && cdiv(qp, 256) <= 10)
-      return {reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4, false, 2>), 4, 2};
     if (upd_is_cartpole(n) && upd_waves8_enabled() && cdiv(qp, 512) <= 5)
       return {reinterpret_cast<const void*>(ppo_update_kernel<5, 2, 2, 4, false, 1>), 8, 1};
     if (upd_is_cartpole(n) && cdiv(qp, 256) <= 10)
       return {reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4, false, 1>), 4, 1};
     const bool pend = !n.discrete && n.A == 1 && n.D == 3;
-    if (pend && !two && upd_waves8_enabled() && cdiv(qp, 512) <= 7)
+    if (pend && upd_waves8_enabled() && cdiv(qp, 512) <= 7)
       return {reinterpret_cast<const void*>(ppo_update_kernel<7, 3, 1, 3, false, 1>), 8, 1};
     if (pend && cdiv(qp, 256) <= 14)
-      return two ? UpdPlan{reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3, false, 2>), 4, 2}
-                 : UpdPlan{reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3, false, 1>), 4, 1};
+      return {reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3, false, 1>), 4, 1};
   }
-  if (cdiv(qp, 256) <= 20) return {reinterpret_cast<const void*>(ppo_update_kernel<20, -1, 0, 0, false, 1>), 4, 1};
-  return {nullptr, 4, 1};
+  return {nullptr, 4, 1};   // (the runtime-layout kernel spills more in this form: latency form)
 }
 size_t upd_lds_bytes_plan(const UpdNet& n, int nw, bool tp, int tiles) {
   return sizeof(float) * (size_t)(UPD_HDR + (tp ? n.Lp : 2 * n.Lp + 4) +
@@ -2649,9 +2328,13 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   args.tp_v0 = ws.mv + L4;
   args.tp_m1 = ws.mv + 2 * L4;
   args.tp_v1 = ws.mv + 3 * L4;
-  const bool tp = upd_tp_host(args.R, args.total_steps, dp != nullptr);
+  bool tp = upd_tp_host(args.R, args.total_steps, dp != nullptr);
   UpdPlan plan{upd_kernel_for(args.net, dp != nullptr), upd_nw_host(args.net, true), 1};
-  if (tp) plan = upd_tp_plan(args.net);
+  if (tp) {
+    const UpdPlan p2 = upd_tp_plan(args.net);
+    if (p2.kern) plan = p2;
+    else tp = false;
+  }
   const size_t lds = upd_lds_bytes_plan(args.net, plan.nw, tp, plan.tiles);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_update: %zu B of LDS needed", lds);
   hipStream_t st = as_stream(stream);
