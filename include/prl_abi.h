@@ -287,6 +287,12 @@ int prl_ppo_wide_grad(const float* params, int32_t D, int32_t A, int32_t discret
                       const float* ret, int64_t N, int64_t mini_batch, const int64_t* cursor,
                       const float* scales, float clip, float vf_coef, float ent_coef, float* grad,
                       float* loss_out, float* part, int64_t part_floats, void* stream);
+/* ActorCritic.dist_params (PPO/ActorCritic.py: the rollout's sampling input; AsyncPPO.py:120-141
+ * calls the policy on every vector step) for the wide nets: out = [N][A] softmax probabilities
+ * (discrete) or [N][2A] = [mu | softplus(clamp(log_std, -2, 2))] (continuous), from the wide
+ * kernel's forward; params flat in torch parameters() order.  One launch, graph-capturable. */
+int prl_ppo_wide_dist(const float* params, int32_t D, int32_t A, int32_t discrete, const float* S,
+                      int64_t N, float* out, void* stream);
 /* policy_old.get_evaluate over all N rows for the wide nets (PPO/PPO.py:127-154,
  * ActorCritic.py:118-146): log_prob into logp_out [N] and the state value into V_out [N], with
  * exactly prl_ppo_wide_grad's forward and row arithmetic, so the first minibatch of learn() sees

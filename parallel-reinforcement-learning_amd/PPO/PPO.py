@@ -184,8 +184,38 @@ class PPO:
 
     @torch.no_grad()
     def dist_params(self, obs: torch.Tensor) -> torch.Tensor:
-        """Distribution rows for the fused device worker step (probs, or [mu | std])."""
-        return self.policy_old.dist_params(obs)
+        """Distribution rows for the fused device worker step (probs, or [mu | std]).  Wide nets
+        (outside the persistent engine: C5's D = 348) on the native path: one prl_ppo_wide_dist
+        launch instead of ~12 PyTorch / hipBLASLt kernels per vector step."""
+        flat = self._dist_flat(obs)
+        if flat is None:
+            return self.policy_old.dist_params(obs)
+        A = self.action_dim
+        out = torch.empty(obs.shape[0], A if not self.is_continuous else 2 * A,
+                          dtype=torch.float32, device=obs.device)
+        prl_native.ppo_wide_dist(flat, obs.shape[1], A, not self.is_continuous,
+                                 obs.contiguous(), out)
+        return out
+
+    def _dist_flat(self, obs):
+        """policy_old's parameters gathered into one persistent flat buffer for
+        prl_ppo_wide_dist, or None when the native distribution path does not apply.  The gather
+        runs on every call (one small kernel) so a CUDA graph that captured it (AsyncPPO's
+        vector step) always reads the current weights."""
+        if (not obs.is_cuda or obs.dtype != torch.float32 or obs.dim() != 2
+                or os.environ.get("PRL_WIDE_DIST", "1") != "1"):
+            return None
+        from .update import wide_info
+        if wide_info(self, obs.shape[1]) is None:
+            return None
+        params = [p.detach().reshape(-1) for p in self.policy_old.parameters()]
+        n = sum(p.numel() for p in params)
+        flat = getattr(self, "_dist_flat_buf", None)
+        if flat is None or flat.numel() != n or flat.device != obs.device:
+            flat = torch.empty(n, dtype=torch.float32, device=obs.device)
+            self._dist_flat_buf = flat
+        torch.cat(params, out=flat)
+        return flat
 
     def batch_packer(self, values, batch_size: int):  # PPO.py:98-105 (DataLoader, no shuffle)
         def split(v):

@@ -144,6 +144,7 @@ struct WdArgs {
   float* dh0;              // split form: [mb][64] trunk pre-activation gradients (dW0 kernel input)
   float* eval_logp;        // evaluate form: [N] log-prob and state value per row
   float* eval_V;
+  float* dist_out;         // distribution form: [N][A] probs or [N][2A] mu | std per row
 };
 
 typedef float wd_v4 __attribute__((ext_vector_type(4)));
@@ -365,6 +366,41 @@ __device__ inline void wd_tile_loss(const WdNet& n, const float* Os, const float
   }
 }
 
+// The distribution form's row output (ActorCritic.dist_params, the rollout's sampling input):
+// row r = t >> 4 on its DPP row of 16 lanes, lane c taking outputs k = c and c + 16: discrete
+// softmax probabilities (max-shifted exp, DPP row sums), continuous [mu | softplus(clamp(log_std,
+// -2, 2))].  Rows >= rc are not written.
+__device__ inline void wd_tile_dist(const WdNet& n, const float* Os, float* out, int64_t row0, int rc) {
+  const int t = threadIdx.x, r = t >> 4, c = t & 15;
+  const int A = n.A;
+  const int k0 = c, k1 = c + 16;
+  const bool ok0 = k0 < A, ok1 = k1 < A;
+  const float* O = Os + r * WD_OS;
+  if (n.discrete) {
+    const float o0 = ok0 ? O[k0] : -FLT_MAX, o1 = ok1 ? O[k1] : -FLT_MAX;
+    const float mx = wd_rmax16(fmaxf(o0, o1));
+    const float e0 = ok0 ? wd_exp(o0 - mx) : 0.f, e1 = ok1 ? wd_exp(o1 - mx) : 0.f;
+    const float rs = wd_rcp(wd_rsum16(e0 + e1));
+    if (r < rc) {
+      float* o = out + (row0 + r) * A;
+      if (ok0) o[k0] = e0 * rs;
+      if (ok1) o[k1] = e1 * rs;
+    }
+  } else if (r < rc) {
+    float* o = out + (row0 + r) * 2 * A;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = u ? k1 : k0;
+      if (u ? ok1 : ok0) {
+        const float lsr = O[A + k];
+        const float lsc = lsr < -2.0f ? -2.0f : (lsr > 2.0f ? 2.0f : lsr);
+        o[k] = O[k];
+        o[A + k] = wd_log(1.0f + wd_exp(lsc));
+      }
+    }
+  }
+}
+
 // Next-tile prefetch (D % 4 == 0, 16-B aligned S; the X buffers then have row stride D): the X
 // tile — 16 consecutive rows of S, one contiguous block — is copied global -> LDS by 16-B
 // global_load_lds (no VGPR destination; a wave-instruction writes 1 KiB contiguously), issued
@@ -393,8 +429,8 @@ __device__ inline void wd_rin_load(const WdNet& n, const WdArgs& a, int64_t row0
     float v = 0.f;
     if (e < WD_RT * WD_RS && r < rc) {
       const int64_t row = row0 + r;
-      if (k < WD_MAXA) v = k < Aw ? a.act[row * Aw + k] : 0.f;
-      else if (a.old_logp == nullptr) v = 0.f;   // evaluate form: actions only
+      if (k < WD_MAXA) v = (k < Aw && a.act) ? a.act[row * Aw + k] : 0.f;
+      else if (a.old_logp == nullptr) v = 0.f;   // evaluate / distribution forms
       else if (k == 32) v = a.old_logp[row];
       else if (k == 33) v = a.adv[row];
       else if (k == 34) v = a.ret[row];
@@ -428,8 +464,8 @@ __device__ inline void wd_stage(const WdNet& n, const WdArgs& a, int64_t row0, i
     float v = 0.f;
     if (r < rc) {
       const int64_t row = row0 + r;
-      if (k < WD_MAXA) v = k < Aw ? a.act[row * Aw + k] : 0.f;
-      else if (a.old_logp == nullptr) v = 0.f;   // evaluate form: actions only
+      if (k < WD_MAXA) v = (k < Aw && a.act) ? a.act[row * Aw + k] : 0.f;
+      else if (a.old_logp == nullptr) v = 0.f;   // evaluate / distribution forms
       else if (k == 32) v = a.old_logp[row];
       else if (k == 33) v = a.adv[row];
       else if (k == 34) v = a.ret[row];
@@ -464,8 +500,9 @@ __device__ inline void wd_stage_x(const WdNet& n, const WdArgs& a, int64_t row0,
 // all N rows, writing each row's log-prob and value instead of a gradient — PPO.learn's
 // policy_old pass for the rows the wide step then updates on, so the first minibatch's ratio is
 // exactly 1 (as in the reference, where both come from one get_evaluate).
-template <int KSM, bool SPLIT, bool EVAL>
+template <int KSM, bool SPLIT, bool EVAL, bool DIST = false>
 __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs& a) {
+  static_assert(!DIST || EVAL, "the distribution form is an evaluate form");
   constexpr int KE = SPLIT ? 1 : KSM / 4;   // 16-column blocks of dW0
   extern __shared__ float4 wd_lds4[];
   float* lds = reinterpret_cast<float*>(wd_lds4);
@@ -702,7 +739,9 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
       wd_rin_load(n, a, r0n, rcn, pr);
     }
     // ---- per-row loss and dO: row t >> 4, 16 lanes per row
-    {
+    if (DIST) {
+      wd_tile_dist(n, Os, a.dist_out, row0, rc);
+    } else {
       float lp[3], logp_r, v_r;
       wd_tile_loss(n, Os, Rin, dOs, invB, a.clip, a.vf_coef, lp, logp_r, v_r);
       if (EVAL) {
@@ -949,13 +988,13 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
 }
 
 // KSPEC: the C5 specialisation (constexpr layout); else the runtime layout from the argument
-template <int KSM, bool SPLIT, bool EVAL = false, bool KSPEC = false>
+template <int KSM, bool SPLIT, bool EVAL = false, bool KSPEC = false, bool DIST = false>
 __global__ __launch_bounds__(WD_THREADS, 1) void ppo_wide_grad_kernel(WdArgs a) {
   if constexpr (KSPEC) {
     constexpr WdNet N = wd_make(WD_C5_D, WD_C5_A, 0);
-    ppo_wide_grad_body<KSM, SPLIT, EVAL>(N, a);
+    ppo_wide_grad_body<KSM, SPLIT, EVAL, DIST>(N, a);
   } else {
-    ppo_wide_grad_body<KSM, SPLIT, EVAL>(a.net, a);
+    ppo_wide_grad_body<KSM, SPLIT, EVAL, DIST>(a.net, a);
   }
 }
 
@@ -1195,6 +1234,50 @@ extern "C" int prl_ppo_wide_info(int32_t D, int32_t A, int32_t discrete, int64_t
   if (n_params) *n_params = n.P;
   if (part_floats) *part_floats = wd_part_floats(n, mini_batch);
   if (grid) *grid = G;
+  return PRL_OK;
+}
+
+// ActorCritic.dist_params over N rows (the rollout's sampling input, AsyncPPO's vector step): the
+// wide kernel's forward, then per row the softmax probabilities [N][A] (discrete) or
+// [mu | softplus(clamp(log_std, -2, 2))] [N][2A] (continuous).  One launch; capturable.
+extern "C" int prl_ppo_wide_dist(const float* params, int32_t D, int32_t A, int32_t discrete,
+                                 const float* S, int64_t N, float* out, void* stream) {
+  WdNet n;
+  PRL_REQUIRE(N >= 0, "prl_ppo_wide_dist: N < 0");
+  PRL_REQUIRE(wd_layout(D, A, discrete, n) && wd_ksm(D) > 0,
+              "prl_ppo_wide_dist: shape D=%d A=%d outside the wide kernel", D, A);
+  PRL_REQUIRE(params && S && out, "prl_ppo_wide_dist: null pointer");
+  if (N == 0) return PRL_OK;
+  const int KSM = wd_ksm(D);
+  const size_t lds = wd_lds_bytes(n, KSM);
+  PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_wide_dist: LDS %zu bytes", lds);
+  WdArgs a{};
+  a.net = n;
+  a.params = params;
+  a.S = S;
+  a.N = N;
+  a.mb = N;
+  a.G = wd_grid(N);
+  a.dist_out = out;
+  hipStream_t st = as_stream(stream);
+  static unsigned long long lds_set[3] = {0ull, 0ull, 0ull};   // bit = device ordinal
+  int dev_ord = 0;
+  PRL_HIP_TRY(hipGetDevice(&dev_ord));
+  const unsigned long long dev_bit = 1ull << (dev_ord & 63);
+#define WD_DLAUNCH(K, SPEC, slot)                                                                 \
+  do {                                                                                         \
+    if (!(lds_set[slot] & dev_bit)) {                                                          \
+      PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_wide_grad_kernel<K, true, true, SPEC, true>), \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));   \
+      lds_set[slot] |= dev_bit;                                                                \
+    }                                                                                          \
+    hipLaunchKernelGGL((ppo_wide_grad_kernel<K, true, true, SPEC, true>), dim3(a.G), dim3(WD_THREADS), lds, st, a); \
+  } while (0)
+  if (KSM == 32) WD_DLAUNCH(32, false, 0);
+  else if (wd_spec(n)) WD_DLAUNCH(88, true, 2);
+  else WD_DLAUNCH(88, false, 1);
+#undef WD_DLAUNCH
+  PRL_LAUNCH_CHECK("ppo_wide_dist");
   return PRL_OK;
 }
 

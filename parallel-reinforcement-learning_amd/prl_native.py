@@ -54,6 +54,7 @@ SIGNATURES = {
     "prl_ppo_wide_grad_prof": [_P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I64, _P, _P,
                                _F32, _F32, _F32, _P, _P, _P, _I64, _P, _P],
     "prl_ppo_wide_evaluate": [_P, _I32, _I32, _I32, _P, _P, _I64, _P, _P, _P],
+    "prl_ppo_wide_dist": [_P, _I32, _I32, _I32, _P, _I64, _P, _P],
     "prl_categorical_fwd": [_P, _P, _I64, _I32, _P, _P, _P],
     "prl_categorical_bwd": [_P, _P, _P, _I64, _I32, _P, _P],
     "prl_ppo_update_info": [_I32, _I32, _I32, _I64, _P, _P, _P],
@@ -466,6 +467,15 @@ def ppo_wide_evaluate(params, D, A, discrete, S, actions, logp, V):
         _dev(S, torch.float32, "S"), _dev(actions, torch.float32, "actions"), int(S.shape[0]),
         _dev(logp, torch.float32, "logp"), _dev(V, torch.float32, "V"), _stream()),
         "prl_ppo_wide_evaluate")
+
+
+def ppo_wide_dist(params, D, A, discrete, S, out):
+    """ActorCritic.dist_params for the wide nets (prl_ppo_wide_dist): out = [N][A] probs or
+    [N][2A] = [mu | std], from the wide kernel's forward."""
+    _check(lib().prl_ppo_wide_dist(
+        _dev(params, torch.float32, "params"), int(D), int(A), int(bool(discrete)),
+        _dev(S, torch.float32, "S"), int(S.shape[0]), _dev(out, torch.float32, "out"), _stream()),
+        "prl_ppo_wide_dist")
 
 
 def ppo_update(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp, adv,

@@ -257,3 +257,66 @@ def test_wide_evaluate_matches_get_evaluate_and_row_placement(cont, D, A):
     ev_ = float((V.cpu().double() - v64).abs().max()) / (1.0 + float(v64.abs().max()))
     print(f"logp {el:.1e}, V {ev_:.1e}")
     assert el <= 2e-6 and ev_ <= 2e-6, (el, ev_)
+
+
+@pytest.mark.parametrize("cont,D,A,N", [(True, 348, 17, 1000), (True, 348, 17, 7),
+                                        (False, 100, 5, 1000), (True, 201, 3, 1)])
+def test_wide_dist_matches_dist_params(cont, D, A, N):
+    """prl_ppo_wide_dist (the rollout's sampling input for the wide nets, AsyncPPO's vector step)
+    against float64 ActorCritic.dist_params: probabilities / [mu | std] within 2e-6 of the
+    largest entry (float32 rounding); every row depends only on itself (a shifted slice gives
+    the same bits)."""
+    import prl_native
+    pol = _policy(cont, D, A, seed=5)
+    torch.manual_seed(11)
+    S = torch.randn(N, D, device="cuda")
+    flat = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
+    W = 2 * A if cont else A
+
+    def dist(lo):
+        out = torch.full((N - lo, W), float("nan"), device="cuda")
+        prl_native.ppo_wide_dist(flat, D, A, not cont, S[lo:].contiguous(), out)
+        return out
+
+    out = dist(0)
+    if N > 3:
+        out3 = dist(3)
+        torch.cuda.synchronize()
+        assert torch.equal(out[3:], out3)
+    p64 = copy.deepcopy(pol).cpu().double()
+    with torch.no_grad():
+        ref = p64.dist_params(S.cpu().double())
+    err = float((out.cpu().double() - ref).abs().max()) / (1.0 + float(ref.abs().max()))
+    print(f"dist {err:.1e}")
+    assert err <= 2e-6, err
+
+
+def test_ppo_dist_params_native_and_graph_sees_new_weights():
+    """PPO.dist_params routes the wide nets through prl_ppo_wide_dist; a CUDA graph that captured
+    it (AsyncPPO's vector step) reads policy_old's current weights after load_state_dict."""
+    from PPO.PPO import PPO
+    ppo = PPO(True, 348, 17, action_scaling=1.0, mini_batch_size=512)
+    assert ppo._dist_flat(torch.zeros(2, 348, device="cuda")) is not None
+    torch.manual_seed(2)
+    S = torch.randn(64, 348, device="cuda")
+    with torch.no_grad():
+        ref = ppo.policy_old.dist_params(S)
+    assert float((ppo.dist_params(S) - ref).abs().max()) <= 2e-6 * (1 + float(ref.abs().max()))
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ppo.dist_params(S)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = ppo.dist_params(S)
+    with torch.no_grad():
+        for p in ppo.policy.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    ppo.policy_old.load_state_dict(ppo.policy.state_dict())
+    g.replay()
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        ref2 = ppo.policy_old.dist_params(S)
+    assert not torch.allclose(ref, ref2)
+    assert float((out - ref2).abs().max()) <= 2e-6 * (1 + float(ref2.abs().max()))
