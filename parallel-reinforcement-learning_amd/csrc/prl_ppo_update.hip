@@ -1378,6 +1378,14 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
 // all-reduce) into red, where phase C reads the reduced gradient.  xbuf is double-buffered by
 // step parity: a rank rewrites xbuf[par] two steps later, by which time every rank has raised
 // the flag of the step in between, i.e. has finished reading this one.
+// Ordering: the flag store and the polls are RELAXED system-scope atomics on purpose.  The slice
+// stores before it are system-scope (sc0 sc1: written through to memory) and drained by the
+// caller's s_waitcnt vmcnt(0) before this store issues; the slice loads after the poll are
+// system-scope too (they miss every cache), and the __syncthreads below orders them after the
+// poll.  A formal system-scope release / acquire would add buffer_wbl2 / buffer_inv of the whole
+// L2 per workgroup per step, writing back or dropping the minibatch rows every workgroup keeps
+// in L2, for ordering the encodings already give.
+
 __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t rs_red, int Qtot,
                                    int g, int G, unsigned long long gstep, int par, int* s_abort) {
   const int t = threadIdx.x, NT = blockDim.x;

@@ -404,39 +404,74 @@ __device__ inline void wd_tile_dist(const WdNet& n, const float* Os, float* out,
 // Next-tile prefetch (D % 4 == 0, 16-B aligned S; the X buffers then have row stride D): the X
 // tile — 16 consecutive rows of S, one contiguous block — is copied global -> LDS by 16-B
 // global_load_lds (no VGPR destination; a wave-instruction writes 1 KiB contiguously), issued
-// before the loss and drained at the barrier after it; the row records go through 3 registers.
+// by one wave after the heads' forward and drained at the barrier after the loss; the row
+// records go through 3 registers (loaded at the same point by every wave).
 __device__ inline void wd_glds_x(const WdNet& n, const WdArgs& a, int64_t row0, int rc, float* Xs) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int t = threadIdx.x, l = t & 63;
   const int tot = WD_RT * n.D, have = rc * n.D;
   const float* src = a.S + row0 * n.D;
   const int nchunk = (tot + 255) >> 8;   // 256-float chunks, one wave-instruction each
-  for (int c = w; c < nchunk; c += 4) {
+  for (int c = 0; c < nchunk; ++c) {     // one wave issues them all (the caller's)
     const int f = (c << 8) + 4 * l;
     const int fs = f < have ? f : 0;     // past the minibatch's rows / the tile: any valid row
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + fs),
-                                     reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                         reinterpret_cast<uintptr_t>(Xs + (c << 8))),
-                                     16, 0, 0);
+    // inline asm, not __builtin_amdgcn_global_load_lds: the compiler puts an s_waitcnt vmcnt(0)
+    // in front of the next LDS read after the builtin (the copy writes LDS it cannot tell apart),
+    // which exposed the whole copy wherever it was issued; the explicit wait before the barrier
+    // after the loss is the only one it needs (no instruction reads the other X buffer before)
+    const unsigned m = __builtin_amdgcn_readfirstlane(
+        (unsigned)reinterpret_cast<uintptr_t>(Xs + (c << 8)));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // m0: nothing else in these kernels uses it
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(src + fs), "s"(m) : "memory", "m0");
+#pragma clang diagnostic pop
   }
 }
-__device__ inline void wd_rin_load(const WdNet& n, const WdArgs& a, int64_t row0, int rc, float (&pr)[3]) {
+// The row records' slots a thread loads: slot i (e = t + 256 i) is row r, column k of the
+// [16][36] record; its source column (act[k] / old_logp / adv / ret) depends only on the thread,
+// so it is resolved once per launch: base == nullptr for an empty slot.  (Loaded by one wave
+// instead — 9 slots per lane — the outputs stage waited for that wave: 268 vs 253 us per step.)
+struct WdRinSlots {
+  const float* base[3];
+  int stride[3], r[3];
+};
+__device__ inline WdRinSlots wd_rin_slots(const WdNet& n, const WdArgs& a) {
   const int t = threadIdx.x;
   const int Aw = n.discrete ? 1 : n.A;
+  WdRinSlots sl;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int e = t + WD_THREADS * i;
     const int r = e / WD_RS, k = e - r * WD_RS;
-    float v = 0.f;
-    if (e < WD_RT * WD_RS && r < rc) {
-      const int64_t row = row0 + r;
-      if (k < WD_MAXA) v = (k < Aw && a.act) ? a.act[row * Aw + k] : 0.f;
-      else if (a.old_logp == nullptr) v = 0.f;   // evaluate / distribution forms
-      else if (k == 32) v = a.old_logp[row];
-      else if (k == 33) v = a.adv[row];
-      else if (k == 34) v = a.ret[row];
+    const float* b = nullptr;
+    int st = 1;
+    if (e < WD_RT * WD_RS) {
+      if (k < WD_MAXA) { b = (k < Aw && a.act) ? a.act + k : nullptr; st = Aw; }
+      else if (a.old_logp == nullptr) b = nullptr;   // evaluate / distribution forms
+      else if (k == 32) b = a.old_logp;
+      else if (k == 33) b = a.adv;
+      else if (k == 34) b = a.ret;
     }
-    pr[i] = v;
+    sl.base[i] = b;
+    sl.stride[i] = st;
+    sl.r[i] = r;
   }
+  return sl;
+}
+// pr[i] = the raw loaded words; bit i of *ok says whether slot i is real (else 0 is stored): the
+// select happens where pr is stored, so nothing waits for the loads before then.  One load per
+// slot from a selected address (a valid dummy when the slot is empty): no branches, so no
+// write-after-write wait on the destination between divergent paths.
+__device__ inline void wd_rin_load(const WdRinSlots& sl, const WdArgs& a, int64_t row0, int rc,
+                                   float (&pr)[3], unsigned* ok) {
+  unsigned m = 0u;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const bool real = sl.base[i] != nullptr && sl.r[i] < rc;
+    pr[i] = *(real ? sl.base[i] + (row0 + sl.r[i]) * sl.stride[i] : a.S);
+    m |= real ? 1u << i : 0u;
+  }
+  *ok = m;
 }
 
 // Stage tile rows [row0, row0 + rc) of S into Xs (rows >= rc and columns >= D stay / become 0)
@@ -584,6 +619,9 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
       }
       w0v[sg] = wv;
     }
+    // landed before the tile loop: the trunk's MFMAs then carry no vmcnt wait for them, which
+    // would also wait out the stores / prefetches the loop leaves in flight
+    __builtin_amdgcn_s_waitcnt(0);
   }
   // gradient accumulators
   wd_v4 gW0[KE];
@@ -611,6 +649,7 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
     tm[i] += now_ - tl;                                                \
     tl = now_;                                                         \
   }
+  const WdRinSlots rin_slots = wd_rin_slots(n, a);
   int it = 0;
   for (int tile = blockIdx.x; tile < ntile; tile += a.G, ++it) {
     const int64_t row0 = row_lo + (int64_t)tile * WD_RT;
@@ -656,6 +695,11 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
     }
     __syncthreads();   // #2: Fs
     WD_MARK(1)
+    // ---- next tile's inputs go in flight after the heads' forward (the other X buffer was last
+    //      read by the previous tile's trunk); issued before the loss, as in round 2, its first
+    //      wait exposed the whole copy
+    const int tile_n = tile + a.G;
+    const bool has_next = pfv && tile_n < ntile;
     // ---- heads: Z_h^T block w = W1_h block w F^T, GroupNorm + SiLU -> G_h
     wd_v4 F[4];
 #pragma unroll
@@ -685,6 +729,18 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
     }
     __syncthreads();   // #3: Gs
     WD_MARK(2)
+    // the next tile's X copy, issued by wave 3, which forms no outputs: a wave's LDS reads queue
+    // behind its own in-flight LDS copies (issued by all four waves at the heads' start, the
+    // copy's latency moved into the heads' forward), and here it lands under the outputs
+    float pr[3];
+    unsigned pr_ok = 0u;
+    if (has_next) {
+      const int64_t rn = rows - (int64_t)tile_n * WD_RT;
+      const int rcn = (int)(rn < WD_RT ? rn : WD_RT);
+      const int64_t r0n = row_lo + (int64_t)tile_n * WD_RT;
+      if (w == 3) wd_glds_x(n, a, r0n, rcn, Xs0 + ((it + 1) & 1) * XBUF);
+      wd_rin_load(rin_slots, a, r0n, rcn, pr, &pr_ok);
+    }
     // ---- output layer: wave m < 3 forms outputs 16m .. 16m+15 of every row (K = each
     //      overlapping head's 64 channels): lane (x = row, q) reg i = O[row x][16m + 4q + i]
     if (w < 3 && 16 * w < n.nout) {
@@ -727,17 +783,6 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
     }
     __syncthreads();   // #4: Os
     WD_MARK(3)
-    // ---- next tile's inputs in flight under the loss (written to the other buffers after it)
-    const int tile_n = tile + a.G;
-    const bool has_next = pfv && tile_n < ntile;
-    float pr[3];
-    if (has_next) {
-      const int64_t rn = rows - (int64_t)tile_n * WD_RT;
-      const int rcn = (int)(rn < WD_RT ? rn : WD_RT);
-      const int64_t r0n = row_lo + (int64_t)tile_n * WD_RT;
-      wd_glds_x(n, a, r0n, rcn, Xs0 + ((it + 1) & 1) * XBUF);
-      wd_rin_load(n, a, r0n, rcn, pr);
-    }
     // ---- per-row loss and dO: row t >> 4, 16 lanes per row
     if (DIST) {
       wd_tile_dist(n, Os, a.dist_out, row0, rc);
@@ -765,7 +810,7 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
       float* Rn = Rin0 + ((it + 1) & 1) * WD_RT * WD_RS;
 #pragma unroll
       for (int i = 0; i < 3; ++i)
-        if (t + WD_THREADS * i < WD_RT * WD_RS) Rn[t + WD_THREADS * i] = pr[i];
+        if (t + WD_THREADS * i < WD_RT * WD_RS) Rn[t + WD_THREADS * i] = (pr_ok >> i) & 1u ? pr[i] : 0.f;
       __builtin_amdgcn_s_waitcnt(0);   // the global_load_lds copies, before the barrier
     }
     __syncthreads();   // #5: dOs
