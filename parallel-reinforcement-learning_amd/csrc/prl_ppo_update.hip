@@ -649,13 +649,28 @@ __device__ inline UpdHead upd_head_info(const UpdNet& n, int h) {
 
 // A tile's global inputs, loaded into registers ahead of the tile (prefetch): the B fragments
 // of the observations X[row x][4 s + q] and one word of the row-input record (thread t < 192:
-// row t / 12, field t % 12 = act[0..7], old_logp, adv, ret, pad).
+// row t / 12, field t % 12 = act[0..7], old_logp, adv, ret, pad).  Every slot is ONE load from a
+// selected address (a valid dummy for an empty slot) with its validity in `ok` (bit s: xin[s],
+// bit 31: rin); upd_in_real zeroes the empty ones.  The persistent kernel's prefetch applies it
+// only when the tile starts: with the zeroing in divergent branches around the loads, the
+// compiler joined the paths with copies that waited for the loads at once — right before the
+// step's arrival at counter A, which put a global load's latency on every step's critical path.
 template <int KSM>
 struct UpdIn {
   float xin[KSM];
   float rin;
+  unsigned ok;
 };
-template <int KD, int KA>
+template <int KSM>
+__device__ inline UpdIn<KSM> upd_in_real(const UpdIn<KSM>& in) {
+  UpdIn<KSM> o;
+#pragma unroll
+  for (int s = 0; s < KSM; ++s) o.xin[s] = (in.ok >> s) & 1u ? in.xin[s] : 0.0f;
+  o.rin = (in.ok >> 31) & 1u ? in.rin : 0.0f;
+  o.ok = in.ok;
+  return o;
+}
+template <int KD, int KA, bool RAW = false>
 __device__ inline void upd_tile_load(const UpdNet& n, const float* Sg, const float* actg,
                                      const float* oldg, const float* advg, const float* retg,
                                      int64_t row0, int rc, UpdIn<upd_ksm<KA>()>& in) {
@@ -663,22 +678,29 @@ __device__ inline void upd_tile_load(const UpdNet& n, const float* Sg, const flo
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4;
   const int D = n.D, KS = (D + 3) >> 2;
   const bool rowok = x < rc;
+  unsigned ok = 0u;
 #pragma unroll
   for (int s = 0; s < KSM; ++s) {
     const int d = 4 * s + q;
-    in.xin[s] = (s < KS && rowok && d < D) ? Sg[(row0 + x) * D + d] : 0.0f;
+    const bool v = s < KS && rowok && d < D;
+    in.xin[s] = *(v ? Sg + (row0 + x) * D + d : Sg);
+    ok |= v ? 1u << s : 0u;
   }
-  in.rin = 0.f;
+  const float* src = nullptr;
   if (t < UPD_RT * UPD_RIN) {
     const int r = t / UPD_RIN, k = t % UPD_RIN;
     const int Aw = n.discrete ? 1 : n.A;
     if (r < rc) {
-      if (k < UPD_MAXA) in.rin = k < Aw ? actg[(row0 + r) * Aw + k] : 0.0f;
-      else if (k == 8 && oldg) in.rin = oldg[row0 + r];
-      else if (k == 9 && advg) in.rin = advg[row0 + r];
-      else if (k == 10 && retg) in.rin = retg[row0 + r];
+      if (k < UPD_MAXA) src = k < Aw ? actg + (row0 + r) * Aw + k : nullptr;
+      else if (k == 8 && oldg) src = oldg + row0 + r;
+      else if (k == 9 && advg) src = advg + row0 + r;
+      else if (k == 10 && retg) src = retg + row0 + r;
     }
   }
+  in.rin = *(src ? src : Sg);
+  ok |= src ? 1u << 31 : 0u;
+  in.ok = ok;
+  if constexpr (!RAW) in = upd_in_real(in);
 }
 
 // Forward of one tile (rows row0 .. row0 + rc - 1, rc <= 16) up to the output-layer partials:
@@ -1519,10 +1541,22 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
   UpdIn<upd_ksm<KA>()> nin[1];   // inputs of the next tile to run (prefetched)
   // load the tile at row0 (rows_left rows of this workgroup's share from there on)
   auto load_next = [&](int64_t row0, int rows_left) {
-    upd_tile_load<KD, KA>(n, args.S, args.act, args.old_logp, args.adv, args.ret, row0,
-                          std::min(UPD_RT, rows_left), nin[0]);
+    upd_tile_load<KD, KA, true>(n, args.S, args.act, args.old_logp, args.adv, args.ret, row0,
+                                std::min(UPD_RT, rows_left), nin[0]);
   };
   unsigned long long* const tm = reinterpret_cast<unsigned long long*>(hdr + 16);
+  // step s's first tile: its rows of minibatch s % nb (0 rows: every slot a dummy load)
+  auto first_row = [&](int s) { return (int64_t)(s % args.nb) * args.mb + (int64_t)g * R; };
+  auto first_rows = [&](int s) {
+    const int64_t fmb0 = (int64_t)(s % args.nb) * args.mb;
+    const int fB = (int)std::min<int64_t>(args.mb, args.N - fmb0);
+    return args.profile == 2 ? 0 : std::max(0, std::min(R, fB - g * R));
+  };
+  auto load_first = [&](int s) { load_next(first_row(s), first_rows(s)); };
+  // Every prefetch is unconditional (clamped arguments instead of branches around it): a load
+  // under a branch made the compiler join nin's paths with copies that waited for the loads on
+  // the spot.
+  load_first(0);
   for (int s = 0; s < args.total_steps; ++s) {
     const int j = s % args.nb;
     const int64_t mb0 = (int64_t)j * args.mb;
@@ -1532,16 +1566,18 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     const int myrows = args.profile == 2 ? 0 : std::max(0, std::min(R, B - g * R));
     const int64_t myrow0 = mb0 + (int64_t)g * R;
     // ---- phase A: partial gradient of this workgroup's rows ------------------------------------
-    if (s == 0 && myrows > 0) load_next(myrow0, myrows);
     UpdGradOf<KD, KA> gr;
     if constexpr (TP) gr.zero();
     if (!TP && myrows == 0) {   // no rows this step: publish zeros
       for (int k = t; k < Lp + 4; k += NT) Ga[k] = 0.0f;
     }
     for (int c0 = 0; c0 < myrows; c0 += UPD_RT) {
-      const UpdIn<upd_ksm<KA>()> cur = nin[0];
-      if (c0 + UPD_RT < myrows)   // prefetch the next tile of this step
-        load_next(myrow0 + c0 + UPD_RT, myrows - c0 - UPD_RT);
+      const UpdIn<upd_ksm<KA>()> cur = upd_in_real(nin[0]);
+      // prefetch the next tile to run: this step's next one, else the next step's first (runs
+      // under this tile and the step's hand-offs)
+      const bool more = c0 + UPD_RT < myrows;
+      load_next(more ? myrow0 + c0 + UPD_RT : first_row(s + 1),
+                more ? myrows - c0 - UPD_RT : first_rows(s + 1));
       if constexpr (TP)
         upd_tile<KD, KA, false, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0),
                                       invB, tm, gr);
@@ -1564,12 +1600,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     mark(1);   // publish partials
-    if (s + 1 < args.total_steps) {   // prefetch the next step's first tile(s) (runs under the waits)
-      const int64_t nmb0 = (int64_t)((s + 1) % args.nb) * args.mb;
-      const int nB = (int)std::min<int64_t>(args.mb, args.N - nmb0);
-      const int nrows = std::max(0, std::min(R, nB - g * R));
-      if (nrows > 0) load_next(nmb0 + (int64_t)g * R, nrows);
-    }
+    if (myrows == 0) load_first(s + 1);   // (no tile ran: the next step's first tile here)
     if (t < 64) {
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_A, g);
       const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));
