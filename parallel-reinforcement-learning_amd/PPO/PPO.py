@@ -208,6 +208,12 @@ class PPO:
         from .update import wide_info
         if wide_info(self, obs.shape[1]) is None:
             return None
+        # the persistent engine's small nets (C2 / C3: D <= 64) keep the PyTorch forward: the
+        # wide tile kernel (16-row tiles over 256 workgroups) took 61.5 us per C2 vector step,
+        # the rollout 151 -> 143 M env-steps/s (profiles/r03_final_bench_kernel_stats.md)
+        if prl_native.ppo_update_info(obs.shape[1], self.action_dim, not self.is_continuous,
+                                      self.mini_batch_size) is not None:
+            return None
         params = [p.detach().reshape(-1) for p in self.policy_old.parameters()]
         n = sum(p.numel() for p in params)
         flat = getattr(self, "_dist_flat_buf", None)

@@ -1576,8 +1576,12 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       // prefetch the next tile to run: this step's next one, else the next step's first (runs
       // under this tile and the step's hand-offs)
       const bool more = c0 + UPD_RT < myrows;
-      load_next(more ? myrow0 + c0 + UPD_RT : first_row(s + 1),
-                more ? myrows - c0 - UPD_RT : first_rows(s + 1));
+      if constexpr (TP) {   // many tiles per step: the next step's first after the publish
+        if (more) load_next(myrow0 + c0 + UPD_RT, myrows - c0 - UPD_RT);
+      } else {
+        load_next(more ? myrow0 + c0 + UPD_RT : first_row(s + 1),
+                  more ? myrows - c0 - UPD_RT : first_rows(s + 1));
+      }
       if constexpr (TP)
         upd_tile<KD, KA, false, true>(n, args, W, Ga, upd_scr_tile(sc, c0 / UPD_RT), cur, std::min(UPD_RT, myrows - c0),
                                       invB, tm, gr);
@@ -1600,7 +1604,10 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     mark(1);   // publish partials
-    if (myrows == 0) load_first(s + 1);   // (no tile ran: the next step's first tile here)
+    // the latency form prefetched the next step's first tile at its tile's start (no tile ran:
+    // here); the throughput form here, under the waits (at the last tile's start its loads
+    // were still in flight at the publish drain: +0.7-0.9 us per step at mb 65,536)
+    if (TP || myrows == 0) load_first(s + 1);
     if (t < 64) {
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_A, g);
       const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));

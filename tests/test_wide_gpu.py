@@ -297,6 +297,9 @@ def test_ppo_dist_params_native_and_graph_sees_new_weights():
     from PPO.PPO import PPO
     ppo = PPO(True, 348, 17, action_scaling=1.0, mini_batch_size=512)
     assert ppo._dist_flat(torch.zeros(2, 348, device="cuda")) is not None
+    # the persistent engine's nets (C2 CartPole, C3 Pendulum) keep the PyTorch forward
+    assert PPO(False, 4, 2, mini_batch_size=512)._dist_flat(torch.zeros(2, 4, device="cuda")) is None
+    assert PPO(True, 3, 1, mini_batch_size=512)._dist_flat(torch.zeros(2, 3, device="cuda")) is None
     torch.manual_seed(2)
     S = torch.randn(64, 348, device="cuda")
     with torch.no_grad():
