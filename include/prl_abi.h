@@ -293,6 +293,13 @@ int prl_ppo_wide_grad(const float* params, int32_t D, int32_t A, int32_t discret
  * kernel's forward; params flat in torch parameters() order.  One launch, graph-capturable. */
 int prl_ppo_wide_dist(const float* params, int32_t D, int32_t A, int32_t discrete, const float* S,
                       int64_t N, float* out, void* stream);
+/* prl_ppo_wide_dist on rows [k*rows, (k+1)*rows) of S ([N][D]), k = step_dev[0] read on the
+ * device: the rollout's captured vector step samples from traj_obs[k] in place (reference
+ * AsyncPPO.worker's get_action on the current observations, AsyncTools/AsyncPPO.py:120-141,
+ * PPO/PPO.py:81-96).  out is [rows][A] or [rows][2A]. */
+int prl_ppo_wide_dist_at(const float* params, int32_t D, int32_t A, int32_t discrete,
+                         const float* S, int64_t N, int64_t rows, const int64_t* step_dev,
+                         float* out, void* stream);
 /* policy_old.get_evaluate over all N rows for the wide nets (PPO/PPO.py:127-154,
  * ActorCritic.py:118-146): log_prob into logp_out [N] and the state value into V_out [N], with
  * exactly prl_ppo_wide_grad's forward and row arithmetic, so the first minibatch of learn() sees

@@ -281,8 +281,11 @@ class AsyncPPO:  # AsyncPPO.py:104-165
 
     def _vector_step(self, k, obs, seed, scaling, active_after):
         """Policy forward on this step's observations + the fused rollout step kernel."""
+        self._step_kernel(k, self.ppo.dist_params(obs), seed, scaling, active_after)
+
+    def _step_kernel(self, k, dist, seed, scaling, active_after):
+        """The fused rollout step kernel on this step's distribution rows."""
         spec, env, tr = self.env.spec, self.env, self._traj
-        dist = self.ppo.dist_params(obs)
         if dist.dtype != torch.float32 or not dist.is_contiguous():
             dist = dist.float().contiguous()
         prl_native.rollout_step(spec.kind, k, env.phys, env.t_elapsed, env.terminal, dist,
@@ -307,10 +310,21 @@ class AsyncPPO:  # AsyncPPO.py:104-165
         try:
             # thread_local: other threads' HIP calls (e.g. the nccl process group's watchdog
             # querying its events on data-parallel ranks) must not invalidate this capture
+            # wide nets: the distribution kernel reads traj_obs[k_dev] in place (no per-step
+            # copy of the E x D rows; policy_old's flat parameters gathered once per rollout)
+            at = (getattr(self.ppo, "dist_params_at", None)
+                  if os.environ.get("PRL_ROLLOUT_DIST_AT", "1") != "0" else None)
+            if at is not None:
+                with torch.no_grad():
+                    self.ppo.refresh_dist_params(tr.obs[0])
             with torch.no_grad(), torch.cuda.graph(g, capture_error_mode="thread_local"):
-                obs = tr.obs.index_select(0, k_dev).view(E, D)
+                dist = at(tr.obs, k_dev, E) if at is not None else None
                 now.zero_()
-                self._vector_step(0, obs, seed, scaling, now)
+                if dist is not None:
+                    self._step_kernel(0, dist, seed, scaling, now)
+                else:
+                    obs = tr.obs.index_select(0, k_dev).view(E, D)
+                    self._vector_step(0, obs, seed, scaling, now)
                 tr.active_after.index_copy_(0, k_dev, now)
                 k_dev.add_(1)
         except RuntimeError as e:   # e.g. a host sync inside a duck-typed policy

@@ -197,11 +197,33 @@ class PPO:
                                  obs.contiguous(), out)
         return out
 
-    def _dist_flat(self, obs):
+    @torch.no_grad()
+    def dist_params_at(self, traj_obs: torch.Tensor, step_dev: torch.Tensor, rows: int):
+        """dist_params(traj_obs[k]) with k = step_dev[0] read on the device (AsyncPPO's captured
+        vector step): the wide nets' prl_ppo_wide_dist_at reads the rows in place.  The flat
+        parameter buffer is NOT re-gathered here: the caller refreshes it once per rollout
+        (refresh_dist_params).  None when the native distribution path does not apply."""
+        D = traj_obs.shape[-1]
+        S = traj_obs.reshape(-1, D)
+        flat = self._dist_flat(S[:rows], gather=False)
+        if flat is None:
+            return None
+        A = self.action_dim
+        out = torch.empty(rows, A if not self.is_continuous else 2 * A,
+                          dtype=torch.float32, device=S.device)
+        prl_native.ppo_wide_dist_at(flat, D, A, not self.is_continuous, S, rows, step_dev, out)
+        return out
+
+    @torch.no_grad()
+    def refresh_dist_params(self, obs: torch.Tensor) -> None:
+        """Gather policy_old's current parameters into the flat buffer dist_params_at reads."""
+        self._dist_flat(obs)
+
+    def _dist_flat(self, obs, gather: bool = True):
         """policy_old's parameters gathered into one persistent flat buffer for
         prl_ppo_wide_dist, or None when the native distribution path does not apply.  The gather
-        runs on every call (one small kernel) so a CUDA graph that captured it (AsyncPPO's
-        vector step) always reads the current weights."""
+        runs on every dist_params call (one small kernel) so a CUDA graph that captured it
+        always reads the current weights; dist_params_at (gather=False) leaves it to the caller."""
         if (not obs.is_cuda or obs.dtype != torch.float32 or obs.dim() != 2
                 or os.environ.get("PRL_WIDE_DIST", "1") != "1"):
             return None
@@ -220,7 +242,9 @@ class PPO:
         if flat is None or flat.numel() != n or flat.device != obs.device:
             flat = torch.empty(n, dtype=torch.float32, device=obs.device)
             self._dist_flat_buf = flat
-        torch.cat(params, out=flat)
+            gather = True
+        if gather:
+            torch.cat(params, out=flat)
         return flat
 
     def batch_packer(self, values, batch_size: int):  # PPO.py:98-105 (DataLoader, no shuffle)

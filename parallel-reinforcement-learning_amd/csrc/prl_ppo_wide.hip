@@ -564,7 +564,9 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
   float* Gn = p;
 
   // ---- minibatch of this step
-  const int64_t j = EVAL ? 0 : *a.cursor;
+  // (distribution form: an optional device step index selects rows [j*mb, (j+1)*mb) of S, the
+  // rollout's traj_obs[k] read in place; out rows are relative to row_lo)
+  const int64_t j = DIST ? (a.cursor ? *a.cursor : 0) : EVAL ? 0 : *a.cursor;
   const int64_t row_lo = j * a.mb;
   const int64_t rows = row_lo < a.N ? (a.N - row_lo < a.mb ? a.N - row_lo : a.mb) : 0;
   const float invB = rows > 0 ? (a.scales ? a.scales[j] : 1.0f) / (float)rows : 0.f;
@@ -785,7 +787,7 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
     WD_MARK(3)
     // ---- per-row loss and dO: row t >> 4, 16 lanes per row
     if (DIST) {
-      wd_tile_dist(n, Os, a.dist_out, row0, rc);
+      wd_tile_dist(n, Os, a.dist_out, row0 - row_lo, rc);
     } else {
       float lp[3], logp_r, v_r;
       wd_tile_loss(n, Os, Rin, dOs, invB, a.clip, a.vf_coef, lp, logp_r, v_r);
@@ -1285,14 +1287,15 @@ extern "C" int prl_ppo_wide_info(int32_t D, int32_t A, int32_t discrete, int64_t
 // ActorCritic.dist_params over N rows (the rollout's sampling input, AsyncPPO's vector step): the
 // wide kernel's forward, then per row the softmax probabilities [N][A] (discrete) or
 // [mu | softplus(clamp(log_std, -2, 2))] [N][2A] (continuous).  One launch; capturable.
-extern "C" int prl_ppo_wide_dist(const float* params, int32_t D, int32_t A, int32_t discrete,
-                                 const float* S, int64_t N, float* out, void* stream) {
+static int wd_dist_launch(const float* params, int32_t D, int32_t A, int32_t discrete,
+                          const float* S, int64_t N, int64_t rows, const int64_t* step,
+                          float* out, void* stream) {
   WdNet n;
-  PRL_REQUIRE(N >= 0, "prl_ppo_wide_dist: N < 0");
+  PRL_REQUIRE(N >= 0 && rows >= 0, "prl_ppo_wide_dist: N < 0 or rows < 0");
   PRL_REQUIRE(wd_layout(D, A, discrete, n) && wd_ksm(D) > 0,
               "prl_ppo_wide_dist: shape D=%d A=%d outside the wide kernel", D, A);
   PRL_REQUIRE(params && S && out, "prl_ppo_wide_dist: null pointer");
-  if (N == 0) return PRL_OK;
+  if (N == 0 || rows == 0) return PRL_OK;
   const int KSM = wd_ksm(D);
   const size_t lds = wd_lds_bytes(n, KSM);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_wide_dist: LDS %zu bytes", lds);
@@ -1301,8 +1304,9 @@ extern "C" int prl_ppo_wide_dist(const float* params, int32_t D, int32_t A, int3
   a.params = params;
   a.S = S;
   a.N = N;
-  a.mb = N;
-  a.G = wd_grid(N);
+  a.mb = rows;
+  a.cursor = step;
+  a.G = wd_grid(rows);
   a.dist_out = out;
   hipStream_t st = as_stream(stream);
   static unsigned long long lds_set[3] = {0ull, 0ull, 0ull};   // bit = device ordinal
@@ -1324,6 +1328,21 @@ extern "C" int prl_ppo_wide_dist(const float* params, int32_t D, int32_t A, int3
 #undef WD_DLAUNCH
   PRL_LAUNCH_CHECK("ppo_wide_dist");
   return PRL_OK;
+}
+
+extern "C" int prl_ppo_wide_dist(const float* params, int32_t D, int32_t A, int32_t discrete,
+                                 const float* S, int64_t N, float* out, void* stream) {
+  return wd_dist_launch(params, D, A, discrete, S, N, N, nullptr, out, stream);
+}
+
+// The rollout's graphed vector step: rows [k*rows, (k+1)*rows) of the trajectory's observation
+// store S ([N][D], N = (T+1) * rows), k read from the device (step_dev[0]), so one captured graph
+// serves every step without a per-step copy of traj_obs[k].  A k past the store gives no rows.
+extern "C" int prl_ppo_wide_dist_at(const float* params, int32_t D, int32_t A, int32_t discrete,
+                                    const float* S, int64_t N, int64_t rows,
+                                    const int64_t* step_dev, float* out, void* stream) {
+  PRL_REQUIRE(step_dev != nullptr, "prl_ppo_wide_dist_at: null step index");
+  return wd_dist_launch(params, D, A, discrete, S, N, rows, step_dev, out, stream);
 }
 
 extern "C" int prl_ppo_wide_evaluate(const float* params, int32_t D, int32_t A, int32_t discrete,

@@ -55,6 +55,7 @@ SIGNATURES = {
                                _F32, _F32, _F32, _P, _P, _P, _I64, _P, _P],
     "prl_ppo_wide_evaluate": [_P, _I32, _I32, _I32, _P, _P, _I64, _P, _P, _P],
     "prl_ppo_wide_dist": [_P, _I32, _I32, _I32, _P, _I64, _P, _P],
+    "prl_ppo_wide_dist_at": [_P, _I32, _I32, _I32, _P, _I64, _I64, _P, _P, _P],
     "prl_categorical_fwd": [_P, _P, _I64, _I32, _P, _P, _P],
     "prl_categorical_bwd": [_P, _P, _P, _I64, _I32, _P, _P],
     "prl_ppo_update_info": [_I32, _I32, _I32, _I64, _P, _P, _P],
@@ -476,6 +477,19 @@ def ppo_wide_dist(params, D, A, discrete, S, out):
         _dev(params, torch.float32, "params"), int(D), int(A), int(bool(discrete)),
         _dev(S, torch.float32, "S"), int(S.shape[0]), _dev(out, torch.float32, "out"), _stream()),
         "prl_ppo_wide_dist")
+
+
+def ppo_wide_dist_at(params, D, A, discrete, S, rows, step_dev, out):
+    """prl_ppo_wide_dist on rows [k*rows, (k+1)*rows) of S with k = step_dev[0] (a device int64):
+    the rollout graph's sampling input straight from traj_obs[k], no per-step copy.  S is any
+    contiguous [..., D] store (e.g. traj_obs [T+1][E][D])."""
+    if S.shape[-1] != D:
+        raise ValueError(f"S's last dimension {S.shape[-1]} != D {D}")
+    _check(lib().prl_ppo_wide_dist_at(
+        _dev(params, torch.float32, "params"), int(D), int(A), int(bool(discrete)),
+        _dev(S, torch.float32, "S"), int(S.numel() // int(D)), int(rows),
+        _dev(step_dev, torch.int64, "step_dev"), _dev(out, torch.float32, "out"), _stream()),
+        "prl_ppo_wide_dist_at")
 
 
 def ppo_update(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp, adv,

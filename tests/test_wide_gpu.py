@@ -323,3 +323,58 @@ def test_ppo_dist_params_native_and_graph_sees_new_weights():
         ref2 = ppo.policy_old.dist_params(S)
     assert not torch.allclose(ref, ref2)
     assert float((out - ref2).abs().max()) <= 2e-6 * (1 + float(ref2.abs().max()))
+
+
+def test_wide_dist_at_reads_the_step_in_place():
+    """prl_ppo_wide_dist_at (AsyncPPO's captured vector step for the wide nets): rows
+    [k*E, (k+1)*E) of the whole [T+1][E][D] observation store with k read on the device give
+    exactly prl_ppo_wide_dist's bits on that slice; a k past the store writes nothing."""
+    import prl_native
+    pol = _policy(True, 348, 17, seed=3)
+    flat = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
+    T1, E, D, W = 5, 300, 348, 34
+    torch.manual_seed(4)
+    S = torch.randn(T1, E, D, device="cuda")
+    k_dev = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for k in (0, 2, T1 - 1):
+        k_dev.fill_(k)
+        out = torch.full((E, W), float("nan"), device="cuda")
+        prl_native.ppo_wide_dist_at(flat, D, 17, False, S, E, k_dev, out)
+        ref = torch.full((E, W), float("nan"), device="cuda")
+        prl_native.ppo_wide_dist(flat, D, 17, False, S[k].contiguous(), ref)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), k
+    k_dev.fill_(T1)
+    out = torch.full((E, W), float("nan"), device="cuda")
+    prl_native.ppo_wide_dist_at(flat, D, 17, False, S, E, k_dev, out)
+    torch.cuda.synchronize()
+    assert bool(torch.isnan(out).all())
+
+
+def test_wide_graphed_rollout_equals_eager_rollout(monkeypatch):
+    """C5's net on the synthetic env: the graphed rollout (distribution read from traj_obs[k] in
+    place, parameters gathered once per rollout) gives the eager rollout's memory and scores
+    bit for bit, including after learn() changed policy_old between rollouts."""
+    from AsyncTools.AsyncPPO import AsyncPPO
+    from PPO import PPO
+    outs = []
+    for graphed in ("1", "0"):
+        monkeypatch.setenv("PRL_ROLLOUT_GRAPH", graphed)
+        torch.manual_seed(0)
+        p = PPO(True, 348, 17, action_scaling=1.0, batch_size=10**9, mini_batch_size=512)
+        a = AsyncPPO("SyntheticHumanoid-v0", p, num_envs=200, seed=5)
+        rec = []
+        for it in range(3):
+            n = a.worker()
+            rec.append((n, float(a.reward_score)))
+            if it == 1:   # new policy_old weights before the third rollout
+                with torch.no_grad():
+                    for q in p.policy.parameters():
+                        q.add_(0.02 * torch.randn_like(q))
+                p.policy_old.load_state_dict(p.policy.state_dict())
+        assert (a._graph is not None) == (graphed == "1")
+        outs.append((rec, [x.cpu() for x in p.memory.device_tensors("cuda")]))
+    (r1, m1), (r0, m0) = outs
+    assert r1 == r0
+    for x, y in zip(m1, m0):
+        assert torch.equal(x, y)
