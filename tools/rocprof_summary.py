@@ -4,6 +4,8 @@
       -> markdown table: kernel (template arguments elided), calls, avg/min/max us, total ms, %
   python tools/rocprof_summary.py trace <kernel_trace.csv> --match gae_kernel
       -> JSON per (kernel, grid): dispatch count and avg/median/min/max duration
+  python tools/rocprof_summary.py timeline <kernel_trace.csv> --match flatten_wide [--upto X]
+      -> busy / idle-gap table per kernel from the last matching dispatch on, and the sequence
   python tools/rocprof_summary.py pmc <counter_collection.csv> [<more.csv> ...] --match gae_kernel
       -> JSON per (kernel, grid): dispatches, mean counter values per dispatch; FETCH_SIZE is
          also reported doubled (gfx950: FETCH_SIZE counts 1/2 of a wide streaming read,
@@ -107,18 +109,62 @@ def trace(path, match, last=0):
     print(json.dumps(out, indent=1))
 
 
+def timeline(path, match, upto=""):
+    """The GPU timeline from the last dispatch matching `match` (e.g. the rollout's flatten, right
+    before learn()) to the end or to the next `upto` dispatch: per kernel, dispatches, busy time
+    and the idle gap before its dispatches (host launch / sync time), then the run-length-
+    compressed sequence."""
+    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"], 70))
+                for r in csv.DictReader(open(path)))
+    i0 = max(i for i, e in enumerate(ev) if match in e[2])
+    ev = ev[i0:]
+    if upto:
+        ends = [i for i, e in enumerate(ev) if i > 0 and upto in e[2]]
+        if ends:
+            ev = ev[:ends[0]]
+    per = defaultdict(lambda: [0, 0.0, 0.0])
+    seq = []
+    prev_end = ev[0][0]
+    for st, en, k in ev:
+        gap = max(0.0, (st - prev_end) / 1e3)
+        prev_end = max(prev_end, en)
+        p_ = per[k]
+        p_[0] += 1
+        p_[1] += (en - st) / 1e3
+        p_[2] += gap
+        if seq and seq[-1][0] == k:
+            seq[-1][1] += 1
+            seq[-1][2] += (en - st) / 1e3
+            seq[-1][3] += gap
+        else:
+            seq.append([k, 1, (en - st) / 1e3, gap])
+    win = (ev[-1][1] - ev[0][0]) / 1e3
+    busy = sum(v[1] for v in per.values())
+    print(f"window {win / 1e3:.3f} ms, busy {busy / 1e3:.3f} ms, idle {(win - busy) / 1e3:.3f} ms, "
+          f"{len(ev)} dispatches")
+    print("| kernel | n | busy us | gap before us |\n|---|---:|---:|---:|")
+    for k, (n, b, g) in sorted(per.items(), key=lambda kv: -(kv[1][1] + kv[1][2])):
+        print(f"| `{k}` | {n} | {b:.1f} | {g:.1f} |")
+    print("\nsequence (kernel x n: busy us, gap us):")
+    for k, n, b, g in seq[:160]:
+        print(f"  {k} x{n}: {b:.1f}, gap {g:.1f}")
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["stats", "pmc", "trace"])
+    ap.add_argument("mode", choices=["stats", "pmc", "trace", "timeline"])
     ap.add_argument("paths", nargs="+")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--match", default="")
     ap.add_argument("--n", type=int, default=0, help="pmc: transitions per launch (recorded)")
+    ap.add_argument("--upto", default="", help="timeline: stop at the next matching dispatch")
     ap.add_argument("--last", type=int, default=0, help="trace: average the last N dispatches")
     a = ap.parse_args()
     if a.mode == "stats":
         stats(a.paths[0], a.top)
     elif a.mode == "pmc":
         pmc(a.paths, a.match, a.n)
+    elif a.mode == "timeline":
+        timeline(a.paths[0], a.match, a.upto)
     else:
         trace(a.paths[0], a.match, a.last)
