@@ -102,6 +102,14 @@ int prl_rollout_step(int kind, int64_t E, int32_t step, double* phys, int32_t* t
                      float action_scaling, uint64_t sample_seed, int32_t t_max, float* traj_obs,
                      float* traj_act, float* traj_rew, uint8_t* traj_done, int32_t* ep_len,
                      int32_t* active_after, double* reward_sum, void* stream);
+/* prl_rollout_step with the step index read on the device (step_dev[0]): the count goes to
+ * active_after[step_dev[0]].  AsyncPPO's captured vector step (same reference lines). */
+int prl_rollout_step_at(int kind, int64_t E, const int64_t* step_dev, double* phys,
+                        int32_t* t_elapsed, uint8_t* terminal, const float* dist,
+                        int64_t dist_stride, float action_scaling, uint64_t sample_seed,
+                        int32_t t_max, float* traj_obs, float* traj_act, float* traj_rew,
+                        uint8_t* traj_done, int32_t* ep_len, int32_t* active_after,
+                        double* reward_sum, void* stream);
 
 /* ---- mask / compaction / flatten (replace AsyncTools/utils.py) ----------------------------- */
 /* utils.indexes_of_active_environments + number_of_active_environments (utils.py:3-7):

@@ -284,26 +284,26 @@ class AsyncPPO:  # AsyncPPO.py:104-165
         self._step_kernel(k, self.ppo.dist_params(obs), seed, scaling, active_after)
 
     def _step_kernel(self, k, dist, seed, scaling, active_after):
-        """The fused rollout step kernel on this step's distribution rows."""
+        """The fused rollout step kernel on this step's distribution rows (k: the step index, an
+        int, or a device int64 [1] tensor for the captured step)."""
         spec, env, tr = self.env.spec, self.env, self._traj
         if dist.dtype != torch.float32 or not dist.is_contiguous():
             dist = dist.float().contiguous()
-        prl_native.rollout_step(spec.kind, k, env.phys, env.t_elapsed, env.terminal, dist,
-                                scaling, seed, tr.T, tr.obs, tr.act, tr.rew, tr.done,
-                                tr.ep_len, active_after, tr.reward_sum)
+        step = prl_native.rollout_step_at if isinstance(k, torch.Tensor) else prl_native.rollout_step
+        step(spec.kind, k, env.phys, env.t_elapsed, env.terminal, dist, scaling, seed, tr.T,
+             tr.obs, tr.act, tr.rew, tr.done, tr.ep_len, active_after, tr.reward_sum)
 
     def _capture_step(self, seed, scaling):
         """One vector step as a HIP graph for this rollout's sampling key: the step index k lives
-        on the device (k_dev, advanced by the graph), the policy reads traj_obs[k_dev] through a
-        gather, the kernel counts the still-active envs into a scalar that the graph then
-        writes to active_after[k_dev].  Same kernels and arguments as the eager step, so the
-        same bits.  None if capture fails (eager launches then)."""
+        on the device (k_dev, advanced by the graph), the policy reads traj_obs[k_dev] (in place
+        for the wide nets, prl_ppo_wide_dist_at; through a gather otherwise), the step kernel
+        adds the still-active count to active_after[k_dev] (prl_rollout_step_at).  Same per-row
+        arithmetic as the eager step, so the same bits.  None if capture fails (eager then)."""
         tr, E, D = self._traj, self.num_envs, self.env.spec.obs_dim
         dev = tr.obs.device
         if getattr(self, "_k_dev", None) is None:
             self._k_dev = torch.zeros(1, dtype=torch.int64, device=dev)
-            self._active_now = torch.zeros(1, dtype=torch.int32, device=dev)
-        k_dev, now = self._k_dev, self._active_now
+        k_dev = self._k_dev
         self._graph = None
         k_dev.zero_()
         g = torch.cuda.CUDAGraph()
@@ -317,15 +317,14 @@ class AsyncPPO:  # AsyncPPO.py:104-165
             if at is not None:
                 with torch.no_grad():
                     self.ppo.refresh_dist_params(tr.obs[0])
+            # the step kernel adds its still-active count to active_after[k_dev] itself
+            # (zeroed at rollout start), so the graph holds no scalar fill / index copy
             with torch.no_grad(), torch.cuda.graph(g, capture_error_mode="thread_local"):
                 dist = at(tr.obs, k_dev, E) if at is not None else None
-                now.zero_()
-                if dist is not None:
-                    self._step_kernel(0, dist, seed, scaling, now)
-                else:
+                if dist is None:
                     obs = tr.obs.index_select(0, k_dev).view(E, D)
-                    self._vector_step(0, obs, seed, scaling, now)
-                tr.active_after.index_copy_(0, k_dev, now)
+                    dist = self.ppo.dist_params(obs)
+                self._step_kernel(k_dev, dist, seed, scaling, tr.active_after)
                 k_dev.add_(1)
         except RuntimeError as e:   # e.g. a host sync inside a duck-typed policy
             warnings.warn(f"rollout step not capturable ({e}); eager launches")

@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(
     float action_scaling, uint64_t seed, int32_t t_max, float* __restrict__ traj_obs,
     float* __restrict__ traj_act, float* __restrict__ traj_rew, uint8_t* __restrict__ traj_done,
     int32_t* __restrict__ ep_len, int32_t* __restrict__ active_after_step,
-    double* __restrict__ reward_sum) {
+    double* __restrict__ reward_sum, const int64_t* __restrict__ step_dev) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int still_active = 0;
   double rew = 0.0;
@@ -352,7 +352,8 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(
   if (threadIdx.x == 0) {
     const int ct = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
     const double rt = s_rew[0] + s_rew[1] + s_rew[2] + s_rew[3];
-    if (ct) atomicAdd(active_after_step, ct);
+    // (graphed rollout: the step index lives on the device, active_after_step is the base)
+    if (ct) atomicAdd(step_dev ? active_after_step + *step_dev : active_after_step, ct);
     if (rt != 0.0) atomicAdd(reward_sum, rt);
   }
 }
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(256) void synth_rollout_step_kernel(
     float action_scaling, uint64_t seed, int32_t t_max, float* __restrict__ traj_obs,
     float* __restrict__ traj_act, float* __restrict__ traj_rew, uint8_t* __restrict__ traj_done,
     int32_t* __restrict__ ep_len, int32_t* __restrict__ active_after_step,
-    double* __restrict__ reward_sum) {
+    double* __restrict__ reward_sum, const int64_t* __restrict__ step_dev) {
   const int64_t e = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __shared__ float s_a2[4][64];
@@ -410,7 +411,8 @@ __global__ __launch_bounds__(256) void synth_rollout_step_kernel(
   if (threadIdx.x == 0) {
     const int ct = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
     const double rt = s_rew[0] + s_rew[1] + s_rew[2] + s_rew[3];
-    if (ct) atomicAdd(active_after_step, ct);
+    // (graphed rollout: the step index lives on the device, active_after_step is the base)
+    if (ct) atomicAdd(step_dev ? active_after_step + *step_dev : active_after_step, ct);
     if (rt != 0.0) atomicAdd(reward_sum, rt);
   }
 }
@@ -509,12 +511,13 @@ extern "C" int prl_env_step_compact(int kind, int64_t E, double* phys, int32_t* 
   return PRL_OK;
 }
 
-extern "C" int prl_rollout_step(int kind, int64_t E, int32_t step, double* phys, int32_t* t_elapsed,
-                                uint8_t* terminal, const float* dist, int64_t dist_stride,
-                                float action_scaling, uint64_t sample_seed, int32_t t_max,
-                                float* traj_obs, float* traj_act, float* traj_rew,
-                                uint8_t* traj_done, int32_t* ep_len, int32_t* active_after,
-                                double* reward_sum, void* stream) {
+static int rollout_step_launch(int kind, int64_t E, int32_t step, const int64_t* step_dev,
+                               double* phys, int32_t* t_elapsed, uint8_t* terminal,
+                               const float* dist, int64_t dist_stride, float action_scaling,
+                               uint64_t sample_seed, int32_t t_max, float* traj_obs,
+                               float* traj_act, float* traj_rew, uint8_t* traj_done,
+                               int32_t* ep_len, int32_t* active_after, double* reward_sum,
+                               void* stream) {
   PRL_REQUIRE(E >= 0 && step >= 0 && t_max > 0, "prl_rollout_step: bad sizes");
   if (E == 0) return PRL_OK;
   PRL_REQUIRE(phys && t_elapsed && terminal && dist && traj_obs && traj_act && traj_rew &&
@@ -529,23 +532,50 @@ extern "C" int prl_rollout_step(int kind, int64_t E, int32_t step, double* phys,
       hipLaunchKernelGGL((rollout_step_kernel<CartPole, true>), dim3((unsigned)cdiv(E, 256)),
                          dim3(256), 0, s, E, phys, t_elapsed, terminal, dist, dist_stride,
                          action_scaling, sample_seed, t_max, traj_obs, traj_act, traj_rew,
-                         traj_done, ep_len, aa, reward_sum);
+                         traj_done, ep_len, aa, reward_sum, step_dev);
       break;
     case PRL_ENV_PENDULUM:
       PRL_REQUIRE(dist_stride >= 2, "prl_rollout_step: dist_stride < 2 for Pendulum mu/std");
       hipLaunchKernelGGL((rollout_step_kernel<Pendulum, false>), dim3((unsigned)cdiv(E, 256)),
                          dim3(256), 0, s, E, phys, t_elapsed, terminal, dist, dist_stride,
                          action_scaling, sample_seed, t_max, traj_obs, traj_act, traj_rew,
-                         traj_done, ep_len, aa, reward_sum);
+                         traj_done, ep_len, aa, reward_sum, step_dev);
       break;
     case PRL_ENV_SYNTH_HUMANOID:
       PRL_REQUIRE(dist_stride >= 2 * Synth::A, "prl_rollout_step: dist_stride < 34 for synth mu/std");
       hipLaunchKernelGGL(synth_rollout_step_kernel, dim3((unsigned)cdiv(E, 4)), dim3(256), 0, s, E,
                          phys, t_elapsed, terminal, dist, dist_stride, action_scaling, sample_seed,
-                         t_max, traj_obs, traj_act, traj_rew, traj_done, ep_len, aa, reward_sum);
+                         t_max, traj_obs, traj_act, traj_rew, traj_done, ep_len, aa, reward_sum,
+                         step_dev);
       break;
     default: return set_error(PRL_ERR_ARG, "prl_rollout_step: unknown env kind %d", kind);
   }
   PRL_LAUNCH_CHECK("rollout_step");
   return PRL_OK;
+}
+
+extern "C" int prl_rollout_step(int kind, int64_t E, int32_t step, double* phys, int32_t* t_elapsed,
+                                uint8_t* terminal, const float* dist, int64_t dist_stride,
+                                float action_scaling, uint64_t sample_seed, int32_t t_max,
+                                float* traj_obs, float* traj_act, float* traj_rew,
+                                uint8_t* traj_done, int32_t* ep_len, int32_t* active_after,
+                                double* reward_sum, void* stream) {
+  return rollout_step_launch(kind, E, step, nullptr, phys, t_elapsed, terminal, dist, dist_stride,
+                             action_scaling, sample_seed, t_max, traj_obs, traj_act, traj_rew,
+                             traj_done, ep_len, active_after, reward_sum, stream);
+}
+
+// The graphed vector step: the count goes to active_after[step_dev[0]] (step index read on the
+// device), so the captured graph needs no per-step scalar, zero fill or index copy.
+extern "C" int prl_rollout_step_at(int kind, int64_t E, const int64_t* step_dev, double* phys,
+                                   int32_t* t_elapsed, uint8_t* terminal, const float* dist,
+                                   int64_t dist_stride, float action_scaling,
+                                   uint64_t sample_seed, int32_t t_max, float* traj_obs,
+                                   float* traj_act, float* traj_rew, uint8_t* traj_done,
+                                   int32_t* ep_len, int32_t* active_after, double* reward_sum,
+                                   void* stream) {
+  PRL_REQUIRE(step_dev != nullptr, "prl_rollout_step_at: null step index");
+  return rollout_step_launch(kind, E, 0, step_dev, phys, t_elapsed, terminal, dist, dist_stride,
+                             action_scaling, sample_seed, t_max, traj_obs, traj_act, traj_rew,
+                             traj_done, ep_len, active_after, reward_sum, stream);
 }

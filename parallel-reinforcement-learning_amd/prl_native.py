@@ -32,6 +32,8 @@ SIGNATURES = {
     "prl_env_step_compact": [_INT, _I64, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P],
     "prl_rollout_step": [_INT, _I64, _I32, _P, _P, _P, _P, _I64, _F32, _U64, _I32, _P, _P, _P,
                          _P, _P, _P, _P, _P],
+    "prl_rollout_step_at": [_INT, _I64, _P, _P, _P, _P, _P, _I64, _F32, _U64, _I32, _P, _P, _P,
+                         _P, _P, _P, _P, _P],
     "prl_active_indices": [_P, _I64, _P, _P, _P, _P],
     "prl_mask_update": [_P, _I64, _P, _I64, _P, _P],
     "prl_compact_rows": [_P, _I64, _I64, _P, _P, _P, _P, _P],
@@ -233,6 +235,27 @@ def rollout_step(kind, step, phys, t_elapsed, terminal, dist, action_scaling, se
                                   _dev(active_after, torch.int32, "active_after"),
                                   _dev(reward_sum, torch.float64, "reward_sum"), _stream()),
            "prl_rollout_step")
+
+
+def rollout_step_at(kind, step_dev, phys, t_elapsed, terminal, dist, action_scaling, seed, t_max,
+                    traj_obs, traj_act, traj_rew, traj_done, ep_len, active_after, reward_sum):
+    """rollout_step with the step index on the device (step_dev: int64 [1]); the still-active
+    count goes to active_after[step_dev[0]] (the captured vector step)."""
+    E = t_elapsed.numel()
+    _check(lib().prl_rollout_step_at(kind, E, _dev(step_dev, torch.int64, "step_dev"),
+                                     _dev(phys, torch.float64, "phys"),
+                                     _dev(t_elapsed, torch.int32, "t"),
+                                     _dev(terminal, torch.uint8, "terminal"),
+                                     _dev(dist, torch.float32, "dist"), int(dist.stride(0)),
+                                     float(action_scaling), int(seed) & (2**64 - 1), int(t_max),
+                                     _dev(traj_obs, torch.float32, "traj_obs"),
+                                     _dev(traj_act, torch.float32, "traj_act"),
+                                     _dev(traj_rew, torch.float32, "traj_rew"),
+                                     _dev(traj_done, torch.uint8, "traj_done"),
+                                     _dev(ep_len, torch.int32, "ep_len"),
+                                     _dev(active_after, torch.int32, "active_after"),
+                                     _dev(reward_sum, torch.float64, "reward_sum"), _stream()),
+           "prl_rollout_step_at")
 
 
 # ------------------------------------------------------------------------- masks / buffers
