@@ -316,12 +316,15 @@ def test_graphed_update_equals_eager_update(cont):
     assert float(loss_g) == float(loss_e)
 
 
-@pytest.mark.parametrize("env,cont", [("CartPole-v1", False), ("Pendulum-v1", True)])
-def test_graphed_rollout_equals_eager_rollout(env, cont, monkeypatch):
+@pytest.mark.parametrize("env,cont,step_at", [("CartPole-v1", False, "0"), ("Pendulum-v1", True, "0"),
+                                              ("CartPole-v1", False, "1")])
+def test_graphed_rollout_equals_eager_rollout(env, cont, step_at, monkeypatch):
     """From the second rollout on, the device worker replays one captured HIP graph per vector
     step (policy forward + rollout step kernel, step index on the device).  Three rollouts with a
     real PPO policy: the graphed runner's memory and scores equal an eager runner's
-    (PRL_ROLLOUT_GRAPH=0) bit for bit."""
+    (PRL_ROLLOUT_GRAPH=0) bit for bit.  step_at "1": the captured step counts into
+    active_after[k] itself (prl_rollout_step_at, PRL_ROLLOUT_STEP_AT=1)."""
+    monkeypatch.setenv("PRL_ROLLOUT_STEP_AT", step_at)
     from AsyncTools.AsyncPPO import AsyncPPO
     from PPO import PPO
     outs = []
