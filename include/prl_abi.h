@@ -55,6 +55,10 @@ enum prl_op {
 /* ---- housekeeping ------------------------------------------------------------------------- */
 int prl_abi_version(void);
 const char* prl_last_error(void);
+/* sha256 (hex) of the csrc sources + headers this library was built from (csrc/build.py stamps
+ * it); prl_native refuses a library whose stamp differs from the sources next to it, so a stale
+ * build cannot run silently.  No reference counterpart. */
+const char* prl_source_id(void);
 /* Bytes of device workspace an op needs for n elements (host call, no GPU work). */
 int64_t prl_workspace_bytes(int op, int64_t n);
 /* Host call: static geometry of an env kind (AsyncPPO.py:45-46 action_space/observation_space). */
@@ -102,9 +106,12 @@ int prl_rollout_step(int kind, int64_t E, int32_t step, double* phys, int32_t* t
                      float action_scaling, uint64_t sample_seed, int32_t t_max, float* traj_obs,
                      float* traj_act, float* traj_rew, uint8_t* traj_done, int32_t* ep_len,
                      int32_t* active_after, double* reward_sum, void* stream);
-/* prl_rollout_step with the step index read on the device (step_dev[0]): the count goes to
- * active_after[step_dev[0]].  AsyncPPO's captured vector step (same reference lines). */
-int prl_rollout_step_at(int kind, int64_t E, const int64_t* step_dev, double* phys,
+/* prl_rollout_step with the step index on the device: step_dev = int64 {k, arrivals} (arrivals 0
+ * between launches).  The count goes to active_after[k] (nothing when k is outside [0, t_max)),
+ * and the launch's last block sets k = k + 1 and re-arms arrivals, so a captured vector step
+ * replayed T times walks k = 0..T-1 with no separate increment.  AsyncPPO's captured vector step
+ * (same reference lines). */
+int prl_rollout_step_at(int kind, int64_t E, int64_t* step_dev, double* phys,
                         int32_t* t_elapsed, uint8_t* terminal, const float* dist,
                         int64_t dist_stride, float action_scaling, uint64_t sample_seed,
                         int32_t t_max, float* traj_obs, float* traj_act, float* traj_rew,
@@ -397,6 +404,12 @@ uint32_t prl_dp_set_spin_limit(uint32_t polls);
  * Per process (initial value from PRL_UPD_TP); returns the previous mode.  No reference
  * counterpart (performance knob / tests). */
 int32_t prl_ppo_update_set_tp(int32_t mode);
+/* What the last prl_ppo_update / prl_ppo_update_dpx call in this process launched:
+ * out[0] = 1 for the throughput form, 0 for the latency form; out[1] = waves per workgroup;
+ * out[2] = workgroups; out[3] = 16-row tiles per workgroup and step (ceil of rows / 16 / G);
+ * out[4] = 1 for a compile-time-layout (CartPole / Pendulum) kernel, 0 for the runtime layout.
+ * All -1 before the first launch.  No reference counterpart (tests assert which kernel ran). */
+void prl_ppo_update_last_plan(int32_t out[5]);
 int prl_dp_xbuf_alloc(int64_t bytes, void** out);
 int prl_dp_xbuf_free(void* p);
 int prl_dp_ipc_handle(void* p, uint8_t* out, int64_t out_bytes);   /* out: 64 bytes */

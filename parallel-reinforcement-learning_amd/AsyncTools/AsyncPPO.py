@@ -297,15 +297,18 @@ class AsyncPPO:  # AsyncPPO.py:104-165
         """One vector step as a HIP graph for this rollout's sampling key: the step index k lives
         on the device (k_dev, advanced by the graph), the policy reads traj_obs[k_dev] (in place
         for the wide nets, prl_ppo_wide_dist_at; through a gather otherwise), the step kernel
-        counts the still-active envs into a scalar the graph copies to active_after[k_dev]
-        (PRL_ROLLOUT_STEP_AT=1: into active_after[k_dev] directly, prl_rollout_step_at).  Same per-row
-        arithmetic as the eager step, so the same bits.  None if capture fails (eager then)."""
+        counts the still-active envs into active_after[k_dev] and advances k_dev itself
+        (prl_rollout_step_at; the graph is the policy's kernels + one step kernel).
+        PRL_ROLLOUT_STEP_AT=0 keeps round 3's form: the count goes to a scalar the graph copies
+        to active_after[k_dev], then an increment node.  Same per-row arithmetic as the eager
+        step, so the same bits.  None if capture fails (eager then)."""
         tr, E, D = self._traj, self.num_envs, self.env.spec.obs_dim
         dev = tr.obs.device
         if getattr(self, "_k_dev", None) is None:
-            self._k_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+            self._k_dev = torch.zeros(2, dtype=torch.int64, device=dev)   # {k, arrivals}
             self._active_now = torch.zeros(1, dtype=torch.int32, device=dev)
         k_dev, now = self._k_dev, self._active_now
+        k1 = k_dev[:1]
         self._graph = None
         k_dev.zero_()
         g = torch.cuda.CUDAGraph()
@@ -319,21 +322,21 @@ class AsyncPPO:  # AsyncPPO.py:104-165
             if at is not None:
                 with torch.no_grad():
                     self.ppo.refresh_dist_params(tr.obs[0])
-            # PRL_ROLLOUT_STEP_AT=1: the step kernel adds its still-active count to
-            # active_after[k_dev] itself (zeroed at rollout start), no scalar fill / index copy
-            # (opt-in until a GPU run has checked it)
+            # the step kernel adds its still-active count to active_after[k_dev] (zeroed at
+            # rollout start) and its last block advances k_dev: no scalar fill, index copy or
+            # increment node (graphed == eager: test_graphed_rollout_equals_eager_rollout)
             with torch.no_grad(), torch.cuda.graph(g, capture_error_mode="thread_local"):
-                dist = at(tr.obs, k_dev, E) if at is not None else None
+                dist = at(tr.obs, k1, E) if at is not None else None
                 if dist is None:
-                    obs = tr.obs.index_select(0, k_dev).view(E, D)
+                    obs = tr.obs.index_select(0, k1).view(E, D)
                     dist = self.ppo.dist_params(obs)
-                if os.environ.get("PRL_ROLLOUT_STEP_AT", "0") == "1":
+                if os.environ.get("PRL_ROLLOUT_STEP_AT", "1") != "0":
                     self._step_kernel(k_dev, dist, seed, scaling, tr.active_after)
                 else:   # the count goes to a scalar the graph copies to active_after[k_dev]
                     now.zero_()
                     self._step_kernel(0, dist, seed, scaling, now)
-                    tr.active_after.index_copy_(0, k_dev, now)
-                k_dev.add_(1)
+                    tr.active_after.index_copy_(0, k1, now)
+                    k1.add_(1)
         except RuntimeError as e:   # e.g. a host sync inside a duck-typed policy
             warnings.warn(f"rollout step not capturable ({e}); eager launches")
             self._graph_failed = True

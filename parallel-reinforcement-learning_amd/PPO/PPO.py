@@ -286,7 +286,11 @@ class PPO:
     def _evaluate_old(self, S, A, world=1):
         """policy_old.get_evaluate over the batch (PPO.py:127-154).  When the fused engine runs
         the update, it also evaluates here, so both log-probs come from the same arithmetic and
-        the first minibatch sees ratio == 1 exactly, as in the reference."""
+        the first minibatch sees ratio == 1 exactly, as in the reference.  The same holds for
+        the wide nets (prl_ppo_wide_evaluate) on every minibatch the wide step runs: all of them
+        on one GPU; with world > 1, the graphed full minibatches only — the ragged tail after
+        n_graph runs _eager_step's autograd forward, whose first-step ratios are 1 to float32
+        rounding (~1e-7), not bit-exactly."""
         if self._fused_path(world) and S.is_cuda:
             eng = self._fused_engine()
             if eng is not None:

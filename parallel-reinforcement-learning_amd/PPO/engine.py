@@ -19,6 +19,10 @@ import prl_native
 
 
 class FusedUpdate:
+    # test injection point: called with this rank's index right before the data-parallel
+    # persistent launch (tests make one rank late); None in production
+    before_dp_launch = None
+
     def __init__(self, ppo, mini_batch: int):
         pol = ppo.policy
         self.ppo = ppo
@@ -344,26 +348,31 @@ class FusedUpdate:
         # the ranks' launches must overlap: line them up (the cross-rank wait also absorbs skew)
         torch.cuda.synchronize()
         tdist.barrier()
-        delay = os.environ.get("PRL_DP_TEST_DELAY", "")   # test-only: "rank:seconds"
-        if delay and int(delay.split(":")[0]) == self._dp_rank:
-            import time
-            time.sleep(float(delay.split(":")[1]))
+        if self.before_dp_launch is not None:   # test injection point (a late rank)
+            self.before_dp_launch(self._dp_rank)
         if self.events is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        prl_native.ppo_update_dpx(
-            self.flat, self.m, self.v, self.step, self.D, self.A, self.discrete,
-            S.contiguous(), A2.contiguous(), old_logp.contiguous(), adv.contiguous(),
-            ret.contiguous(), mb, k_epochs, nb, inv, self.ppo.policy_clip, self.ppo.value_coef,
-            self.ppo.entropy_coef, group["lr"], beta1, beta2, group["eps"],
-            group["weight_decay"], 2.0, self.loss, world, self._dp_rank, xb,
-            self._dp_seq, self.ws)
+        try:
+            prl_native.ppo_update_dpx(
+                self.flat, self.m, self.v, self.step, self.D, self.A, self.discrete,
+                S.contiguous(), A2.contiguous(), old_logp.contiguous(), adv.contiguous(),
+                ret.contiguous(), mb, k_epochs, nb, inv, self.ppo.policy_clip,
+                self.ppo.value_coef, self.ppo.entropy_coef, group["lr"], beta1, beta2,
+                group["eps"], group["weight_decay"], 2.0, self.loss, world, self._dp_rank, xb,
+                self._dp_seq, self.ws)
+            launch_error = None
+        except (RuntimeError, ValueError) as e:
+            # this rank did not launch (e.g. an argument check): it still joins the gather
+            # below with a nonzero status, so every rank takes the same restore / fallback
+            launch_error = e
         self._dp_seq += int(k_epochs) * nb
         if self.events is not None:
             ev[1].record()
             self.events.append(("ppo_update_kernel_dp", ev[0], ev[1],
                                 int(S.shape[0]) * int(k_epochs), int(k_epochs) * nb))
-        status = max(prl_native.ppo_update_status(self.ws).tolist())
+        status = (max(prl_native.ppo_update_status(self.ws).tolist()) if launch_error is None
+                  else -1)
         res = [None] * world
         tdist.all_gather_object(res, (status, self._dp_checksum(self.flat) if status == 0 else None))
         sums = [c for _, c in res]
@@ -372,7 +381,7 @@ class FusedUpdate:
             return self.loss.reshape(())
         # a rank timed out or the ranks diverged: restore, and take the stepped loop from here
         warnings.warn(f"data-parallel persistent launch failed (status / checksum per rank: "
-                      f"{res}); restoring the pre-launch state and re-running this update on "
+                      f"{res}{'; this rank: ' + str(launch_error) if launch_error else ''}); restoring the pre-launch state and re-running this update on "
                       "the stepped loop")
         self.flat.copy_(snap[0])
         self.m.copy_(snap[1])

@@ -25,6 +25,11 @@ extern "C" int prl_abi_version(void) { return PRL_ABI_VERSION; }
 
 extern "C" const char* prl_last_error(void) { return prl::g_err; }
 
+#ifndef PRL_SOURCE_ID
+#define PRL_SOURCE_ID "unstamped"
+#endif
+extern "C" const char* prl_source_id(void) { return PRL_SOURCE_ID; }
+
 extern "C" int64_t prl_workspace_bytes(int op, int64_t n) {
   if (n < 0) n = 0;
   switch (op) {

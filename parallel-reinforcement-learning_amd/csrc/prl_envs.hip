@@ -281,6 +281,29 @@ __global__ void synth_step_compact_kernel(int64_t E, double* phys, int32_t* t_el
 }
 
 // ---------------------------------------------------------------------------------------------
+// End of a rollout step block (thread 0): add the block's still-active count to the step's slot.
+// Eager form (step_dev null): active_after_step is the slot.  Captured form (prl_rollout_step_at):
+// step_dev = {k, arrivals}; the count goes to active_after[k] (skipped outside [0, t_max): a
+// stale k never writes past the store), and the last block to arrive advances k and re-arms the
+// arrival counter, so the captured vector step needs no separate increment node.
+__device__ __forceinline__ void rollout_count_and_advance(int ct, int32_t* active_after_step,
+                                                          int64_t* step_dev, int32_t t_max) {
+  if (!step_dev) {
+    if (ct) atomicAdd(active_after_step, ct);
+    return;
+  }
+  const int64_t k = step_dev[0];
+  if (ct && k >= 0 && k < t_max) atomicAdd(active_after_step + k, ct);
+  __threadfence();   // this block's read of k (and its count) before its arrival
+  const unsigned long long prev =
+      atomicAdd(reinterpret_cast<unsigned long long*>(step_dev + 1), 1ull);
+  if (prev == (unsigned long long)gridDim.x - 1) {   // every other block has read k
+    step_dev[1] = 0;
+    step_dev[0] = k + 1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // The fused rollout step (thread per env) for the classic-control envs.
 template <class Env, bool DISCRETE>
 __global__ __launch_bounds__(256) void rollout_step_kernel(
@@ -289,7 +312,7 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(
     float action_scaling, uint64_t seed, int32_t t_max, float* __restrict__ traj_obs,
     float* __restrict__ traj_act, float* __restrict__ traj_rew, uint8_t* __restrict__ traj_done,
     int32_t* __restrict__ ep_len, int32_t* __restrict__ active_after_step,
-    double* __restrict__ reward_sum, const int64_t* __restrict__ step_dev) {
+    double* __restrict__ reward_sum, int64_t* step_dev) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int still_active = 0;
   double rew = 0.0;
@@ -352,9 +375,8 @@ __global__ __launch_bounds__(256) void rollout_step_kernel(
   if (threadIdx.x == 0) {
     const int ct = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
     const double rt = s_rew[0] + s_rew[1] + s_rew[2] + s_rew[3];
-    // (graphed rollout: the step index lives on the device, active_after_step is the base)
-    if (ct) atomicAdd(step_dev ? active_after_step + *step_dev : active_after_step, ct);
     if (rt != 0.0) atomicAdd(reward_sum, rt);
+    rollout_count_and_advance(ct, active_after_step, step_dev, t_max);
   }
 }
 
@@ -366,7 +388,7 @@ __global__ __launch_bounds__(256) void synth_rollout_step_kernel(
     float action_scaling, uint64_t seed, int32_t t_max, float* __restrict__ traj_obs,
     float* __restrict__ traj_act, float* __restrict__ traj_rew, uint8_t* __restrict__ traj_done,
     int32_t* __restrict__ ep_len, int32_t* __restrict__ active_after_step,
-    double* __restrict__ reward_sum, const int64_t* __restrict__ step_dev) {
+    double* __restrict__ reward_sum, int64_t* step_dev) {
   const int64_t e = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   __shared__ float s_a2[4][64];
@@ -411,9 +433,8 @@ __global__ __launch_bounds__(256) void synth_rollout_step_kernel(
   if (threadIdx.x == 0) {
     const int ct = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
     const double rt = s_rew[0] + s_rew[1] + s_rew[2] + s_rew[3];
-    // (graphed rollout: the step index lives on the device, active_after_step is the base)
-    if (ct) atomicAdd(step_dev ? active_after_step + *step_dev : active_after_step, ct);
     if (rt != 0.0) atomicAdd(reward_sum, rt);
+    rollout_count_and_advance(ct, active_after_step, step_dev, t_max);
   }
 }
 
@@ -511,7 +532,7 @@ extern "C" int prl_env_step_compact(int kind, int64_t E, double* phys, int32_t* 
   return PRL_OK;
 }
 
-static int rollout_step_launch(int kind, int64_t E, int32_t step, const int64_t* step_dev,
+static int rollout_step_launch(int kind, int64_t E, int32_t step, int64_t* step_dev,
                                double* phys, int32_t* t_elapsed, uint8_t* terminal,
                                const float* dist, int64_t dist_stride, float action_scaling,
                                uint64_t sample_seed, int32_t t_max, float* traj_obs,
@@ -566,8 +587,9 @@ extern "C" int prl_rollout_step(int kind, int64_t E, int32_t step, double* phys,
 }
 
 // The graphed vector step: the count goes to active_after[step_dev[0]] (step index read on the
-// device), so the captured graph needs no per-step scalar, zero fill or index copy.
-extern "C" int prl_rollout_step_at(int kind, int64_t E, const int64_t* step_dev, double* phys,
+// device) and the kernel advances step_dev[0] itself, so the captured graph needs no per-step
+// scalar, zero fill, index copy or increment.
+extern "C" int prl_rollout_step_at(int kind, int64_t E, int64_t* step_dev, double* phys,
                                    int32_t* t_elapsed, uint8_t* terminal, const float* dist,
                                    int64_t dist_stride, float action_scaling,
                                    uint64_t sample_seed, int32_t t_max, float* traj_obs,

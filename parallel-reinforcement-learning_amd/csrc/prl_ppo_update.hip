@@ -2293,6 +2293,7 @@ struct UpdDp {
 // the slice buffers [2][Qtot * 4] f32, then the per-workgroup step flags [G] u64
 size_t upd_xbuf_flags_off(const UpdNet& n) { return (((size_t)n.Lp / 4 + 1) * 32 + 255) & ~(size_t)255; }
 unsigned g_dp_spin_limit = UPD_DP_SPIN_LIMIT;
+int32_t g_last_plan[5] = {-1, -1, -1, -1, -1};   // prl_ppo_update_last_plan
 
 int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, int32_t D,
             int32_t A, int32_t discrete, const float* S, const float* actions,
@@ -2386,6 +2387,12 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   hipStream_t st = as_stream(stream);
   const void* kern = plan.kern;
   PRL_REQUIRE(kern, "prl_ppo_update: %d parameter quads per thread not built", upd_nq(args.net));
+  g_last_plan[0] = tp ? 1 : 0;
+  g_last_plan[1] = plan.nw;
+  g_last_plan[2] = G;
+  g_last_plan[3] = args.R / UPD_RT;
+  g_last_plan[4] = (!upd_force_generic() && (upd_is_cartpole(args.net) ||
+                                             (!args.net.discrete && args.net.A == 1 && args.net.D == 3))) ? 1 : 0;
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr + UPD_CTR_A, 0, 4 * (UPD_CTR_WORDS - UPD_CTR_A), st));
@@ -2436,6 +2443,10 @@ extern "C" int32_t prl_ppo_update_set_tp(int32_t mode) {
   const int prev = g_tp_mode;
   g_tp_mode = (mode >= 0 && mode <= 2) ? mode : 2;
   return prev;
+}
+
+extern "C" void prl_ppo_update_last_plan(int32_t out[5]) {
+  for (int i = 0; i < 5; ++i) out[i] = g_last_plan[i];
 }
 
 extern "C" uint32_t prl_dp_set_spin_limit(uint32_t polls) {

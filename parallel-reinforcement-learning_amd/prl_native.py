@@ -76,6 +76,8 @@ SIGNATURES = {
     "prl_dp_xbuf_bytes": [_I32, _I32, _I32, _I32],
     "prl_dp_set_spin_limit": [ctypes.c_uint32],
     "prl_ppo_update_set_tp": [_I32],
+    "prl_ppo_update_last_plan": [_P],
+    "prl_source_id": [],
     "prl_dp_xbuf_alloc": [_I64, _P],
     "prl_dp_xbuf_free": [_P],
     "prl_dp_ipc_handle": [_P, _P, _I64],
@@ -92,12 +94,26 @@ SIGNATURES = {
     "prl_ppo_grad_fold_step": [_P] * 7 + [_I64, _F32, _I32, _I32, _I32] + [_P] * 5
                               + [_I64, _I32, _I64] + [_F32] * 10 + [_P, _P, _P, _I64, _P],
 }
-_RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,
+_RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_source_id": ctypes.c_char_p,
+             "prl_ppo_update_last_plan": None,"prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,
              "prl_dp_set_spin_limit": ctypes.c_uint32, "prl_ppo_update_set_tp": _I32,
              "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
 
 _lib = None
 _lock = threading.Lock()
+
+
+def _sources_id():
+    """The stamp the in-tree sources would give (csrc/build.py source_id), or None when the
+    library is not the in-tree one or the sources are not next to it."""
+    csrc = os.path.join(_HERE, "csrc")
+    if "PRL_HIP_LIB" in os.environ or not os.path.exists(os.path.join(csrc, "build.py")):
+        return None
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_prl_csrc_build", os.path.join(csrc, "build.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.source_id(csrc)
 
 
 def lib():
@@ -117,6 +133,13 @@ def lib():
                     fn.restype = _RESTYPES.get(name, ctypes.c_int)
                 if L.prl_abi_version() != 1:
                     raise RuntimeError("libprl_hip.so ABI version mismatch")
+                want = _sources_id()
+                got = L.prl_source_id().decode()
+                if want is not None and got != want:
+                    raise RuntimeError(
+                        f"{LIB_PATH} was built from other sources (stamp {got[:12]}, sources "
+                        f"{want[:12]}): rebuild it with parallel-reinforcement-learning_amd/csrc/"
+                        "build.py")
                 _lib = L
     return _lib
 
@@ -239,9 +262,12 @@ def rollout_step(kind, step, phys, t_elapsed, terminal, dist, action_scaling, se
 
 def rollout_step_at(kind, step_dev, phys, t_elapsed, terminal, dist, action_scaling, seed, t_max,
                     traj_obs, traj_act, traj_rew, traj_done, ep_len, active_after, reward_sum):
-    """rollout_step with the step index on the device (step_dev: int64 [1]); the still-active
-    count goes to active_after[step_dev[0]] (the captured vector step)."""
+    """rollout_step with the step index on the device (step_dev: int64 [2] = {k, arrivals},
+    arrivals 0); the still-active count goes to active_after[k] and the kernel advances k by one
+    (the captured vector step)."""
     E = t_elapsed.numel()
+    if step_dev.numel() < 2:
+        raise ValueError("step_dev must hold {k, arrivals} (int64 [2])")
     _check(lib().prl_rollout_step_at(kind, E, _dev(step_dev, torch.int64, "step_dev"),
                                      _dev(phys, torch.float64, "phys"),
                                      _dev(t_elapsed, torch.int32, "t"),
@@ -621,6 +647,17 @@ def ppo_update_set_tp(mode: int) -> int:
     """Form of the fused update engine: 0 latency form, 1 throughput form (launches of >= 2
     steps), 2 auto (default); returns the previous mode.  Both forms give the same bits."""
     return int(lib().prl_ppo_update_set_tp(int(mode)))
+
+
+def ppo_update_last_plan() -> dict:
+    """What the last prl_ppo_update / _dpx launch in this process ran: form ("throughput" /
+    "latency"), waves per workgroup, workgroups, 16-row tiles per workgroup and step, and
+    whether the kernel was a compile-time-layout specialisation."""
+    out = (ctypes.c_int32 * 5)()
+    lib().prl_ppo_update_last_plan(out)
+    tp, nw, G, tiles, spec = list(out)
+    return {"form": {1: "throughput", 0: "latency"}.get(tp), "waves": nw, "grid": G,
+            "tiles": tiles, "specialised": bool(spec == 1)}
 
 
 def dp_xbuf_alloc(nbytes: int) -> ctypes.c_void_p:

@@ -423,6 +423,16 @@ def main():
                                              tag="learn_rnd_c5mb", N=65536 + 3000, mb=65536,
                                              k_epochs=2, use_rnd=True, D=348, A=17,
                                              store_inputs=False, light=True),
+        # the large-minibatch update C2's second row and C3 run (mini_batch 65,536: the engine's
+        # throughput form, 256 workgroups x 16 tiles): two full minibatches and a ragged third,
+        # two epochs, CartPole and Pendulum (inputs regenerated by learn_inputs.py)
+        "learn_mb65536": lambda: make_learn(torch, ppo_pkg, continuous=False, tag="learn_mb65536",
+                                            N=2 * 65536 + 9000, mb=65536, k_epochs=2,
+                                            store_inputs=False, light=True),
+        "learn_cont_mb65536": lambda: make_learn(torch, ppo_pkg, continuous=True,
+                                                 tag="learn_cont_mb65536", N=2 * 65536 + 9000,
+                                                 mb=65536, k_epochs=2, store_inputs=False,
+                                                 light=True),
         "rnd": lambda: make_rnd(torch, ppo_pkg),
         "worker": lambda: make_worker(apo, utils, ppo_pkg),
         "envs": lambda: make_envs(apo),

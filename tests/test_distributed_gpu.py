@@ -409,11 +409,12 @@ def _dpx_fail_worker(rank, world, port, mb, nb, k, out_dir, persistent):
         p.learn()                                   # healthy launch (default wait limit)
         paths = [str(p.last_update_path)]
         if persistent:   # second learn: rank 1 launches 2 s late, the wait limit is ~ms
+            import time
             prl_native.dp_set_spin_limit(1 << 12)
-            os.environ["PRL_DP_TEST_DELAY"] = "1:2.0"
+            p._engine.before_dp_launch = lambda r: time.sleep(2.0) if r == 1 else None
         p.memory.push_device(*data)
         p.learn()
-        os.environ.pop("PRL_DP_TEST_DELAY", None)
+        p._engine.before_dp_launch = None
         prl_native.dp_set_spin_limit(0)
         paths.append(str(p.last_update_path))
         torch.cuda.synchronize()

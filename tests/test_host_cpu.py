@@ -15,18 +15,20 @@ from conftest import ROOT
 # ---------------------------------------------------------------------------------- C-ABI
 def _declared_symbols():
     hdr = open(os.path.join(ROOT, "include", "prl_abi.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|uint32_t|const char\*)\s+(prl_\w+)\s*\(", hdr, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|uint32_t|void|const char\*)\s+(prl_\w+)\s*\(", hdr, re.M)))
 
 
 def test_abi_library_exports_every_declared_symbol():
     import prl_native
     L = prl_native.lib()
     syms = _declared_symbols()
-    assert len(syms) == len(prl_native.SIGNATURES) == 57
+    assert len(syms) == len(prl_native.SIGNATURES) == 59
     for s in syms:
         assert hasattr(L, s), s
         assert s in prl_native.SIGNATURES, f"{s} has no ctypes signature"
     assert L.prl_abi_version() == 1
+    # the library was built from the sources next to it (csrc/build.py stamps them)
+    assert L.prl_source_id().decode() == prl_native._sources_id()
 
 
 def test_abi_host_calls_without_gpu():

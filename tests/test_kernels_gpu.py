@@ -348,8 +348,10 @@ def test_synth_env_vs_oracle():
         mask[idx] = d_r | tr_r
 
 
-def _run_rollout(kind, E, seeds, seed, probs_fn, scaling=1.0):
-    """Drive prl_rollout_step with host-provided distribution rows; returns device results."""
+def _run_rollout(kind, E, seeds, seed, probs_fn, scaling=1.0, at=False):
+    """Drive prl_rollout_step with host-provided distribution rows; returns device results.
+    at=True: prl_rollout_step_at with the step index {k, arrivals} on the device (the kernel
+    advances k), checked against the host's k after every step."""
     N = native()
     dims = N.env_dims(kind)
     D, A, TM = dims["obs_dim"], dims["act_dim"], dims["max_episode_steps"]
@@ -364,11 +366,17 @@ def _run_rollout(kind, E, seeds, seed, probs_fn, scaling=1.0):
     rsum = torch.zeros(1, dtype=torch.float64, device=DEV)
     N.env_reset(kind, phys, rng, t, term, traj_obs[0], D)
     dists = []
+    k_dev = torch.zeros(2, dtype=torch.int64, device=DEV)
     for k in range(TM):
         dist = T(probs_fn(k))
         dists.append(dist)
-        N.rollout_step(kind, k, phys, t, term, dist, scaling, seed, TM, traj_obs, traj_act,
-                       traj_rew, traj_done, ep_len, active_after, rsum)
+        if at:
+            N.rollout_step_at(kind, k_dev, phys, t, term, dist, scaling, seed, TM, traj_obs,
+                              traj_act, traj_rew, traj_done, ep_len, active_after, rsum)
+            assert k_dev.tolist() == [k + 1, 0]
+        else:
+            N.rollout_step(kind, k, phys, t, term, dist, scaling, seed, TM, traj_obs, traj_act,
+                           traj_rew, traj_done, ep_len, active_after, rsum)
         if k % 16 == 15 and int(active_after[k]) == 0:
             break
     torch.cuda.synchronize()
@@ -414,6 +422,43 @@ def test_cartpole_rollout_step_bit_exact_vs_oracle():
     np.testing.assert_array_equal(out["term"].cpu().numpy().astype(bool), mask)
     np.testing.assert_array_equal(out["active_after"].cpu().numpy()[: out["steps"]], active_after)
     assert float(out["rsum"]) == float(ep_len.sum())
+
+
+@pytest.mark.parametrize("kind,E", [(0, 4099), (1, 700), (2, 37)])
+def test_rollout_step_at_equals_rollout_step(kind, E):
+    """prl_rollout_step_at (the captured vector step: k read on the device, advanced by the
+    launch's last block) writes the same bits as prl_rollout_step with k from the host, every
+    buffer; and a stale k past the store (k >= t_max) adds nothing to active_after."""
+    N = native()
+    seeds = np.arange(E) * 5 + 3
+    dims = N.env_dims(kind)
+    width = 2 if kind != 2 else 2 * dims["act_dim"]
+    prng = np.random.default_rng(9)
+    rows = [(prng.dirichlet([1, 1], E) if kind == 0 else
+             np.concatenate([prng.normal(0, 1, (E, width // 2)),
+                             np.full((E, width // 2), 0.5)], 1)).astype(np.float32)
+            for _ in range(dims["max_episode_steps"])]
+    a = _run_rollout(kind, E, seeds, 77, lambda k: rows[k], scaling=2.0 if kind == 1 else 1.0)
+    b = _run_rollout(kind, E, seeds, 77, lambda k: rows[k], scaling=2.0 if kind == 1 else 1.0,
+                     at=True)
+    assert a["steps"] == b["steps"]
+    for key in ("traj_obs", "traj_act", "traj_rew", "traj_done", "ep_len", "active_after", "rsum",
+                "term"):
+        assert torch.equal(a[key], b[key]), key
+    # k beyond the store: the launch counts nothing, still advances k
+    TM = dims["max_episode_steps"]
+    phys, rng, t, term, _ = _make_env_state(kind, E, seeds, dims["obs_dim"])
+    traj = [torch.zeros(TM + 1, E, dims["obs_dim"], device=DEV),
+            torch.zeros(TM, E, 1 if dims["discrete"] else dims["act_dim"], device=DEV),
+            torch.zeros(TM, E, device=DEV), torch.zeros(TM, E, dtype=torch.uint8, device=DEV),
+            torch.zeros(E, dtype=torch.int32, device=DEV)]
+    store = torch.zeros(TM + 8, dtype=torch.int32, device=DEV)   # guard words past [0, TM)
+    N.env_reset(kind, phys, rng, t, term, traj[0][0], dims["obs_dim"])
+    k_dev = torch.tensor([TM, 0], dtype=torch.int64, device=DEV)
+    N.rollout_step_at(kind, k_dev, phys, t, term, T(rows[0]), 1.0, 77, TM, *traj, store[:TM],
+                      torch.zeros(1, dtype=torch.float64, device=DEV))
+    torch.cuda.synchronize()
+    assert k_dev.tolist() == [TM + 1, 0] and int(store.abs().sum()) == 0
 
 
 def test_pendulum_rollout_step_vs_oracle():

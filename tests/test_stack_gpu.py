@@ -316,14 +316,15 @@ def test_graphed_update_equals_eager_update(cont):
     assert float(loss_g) == float(loss_e)
 
 
-@pytest.mark.parametrize("env,cont,step_at", [("CartPole-v1", False, "0"), ("Pendulum-v1", True, "0"),
-                                              ("CartPole-v1", False, "1")])
+@pytest.mark.parametrize("env,cont,step_at", [("CartPole-v1", False, "1"), ("Pendulum-v1", True, "1"),
+                                              ("CartPole-v1", False, "0")])
 def test_graphed_rollout_equals_eager_rollout(env, cont, step_at, monkeypatch):
     """From the second rollout on, the device worker replays one captured HIP graph per vector
     step (policy forward + rollout step kernel, step index on the device).  Three rollouts with a
     real PPO policy: the graphed runner's memory and scores equal an eager runner's
-    (PRL_ROLLOUT_GRAPH=0) bit for bit.  step_at "1": the captured step counts into
-    active_after[k] itself (prl_rollout_step_at, PRL_ROLLOUT_STEP_AT=1)."""
+    (PRL_ROLLOUT_GRAPH=0) bit for bit.  step_at "1" (default): the captured step kernel counts
+    into active_after[k] and advances k itself (prl_rollout_step_at); "0": round 3's scalar +
+    index copy + increment nodes (PRL_ROLLOUT_STEP_AT=0)."""
     monkeypatch.setenv("PRL_ROLLOUT_STEP_AT", step_at)
     from AsyncTools.AsyncPPO import AsyncPPO
     from PPO import PPO

@@ -1,0 +1,143 @@
+"""The fused engine's THROUGHPUT form — the update C2's mini_batch 65,536 row and C3 run — pinned
+to the reference (/root/reference/PPO/PPO.py:216-255).
+
+At mini_batch >= 8,192 every workgroup takes >= 2 16-row tiles per optimizer step, and
+prl_ppo_update runs ppo_update_kernel's throughput form (gradient in registers, AdamW moments
+streamed through the workspace; 8-wave head-split kernels for CartPole and Pendulum:
+csrc/prl_ppo_update.hip upd_tp_plan).  Each test asserts that form ran (prl_ppo_update_last_plan).
+
+  * test_large_minibatch_learn_matches_reference_learn: tests/golden/learn_mb65536.npz and
+    learn_cont_mb65536.npz were written by the reference's own PPO.learn (make_golden.py) at
+    mini_batch 65,536, k_epochs 2, N = 2 x 65,536 + 9,000 (ragged third minibatch).  The same
+    initial policy and memory through our learn(): GAE returns, normalised advantages and the
+    weights after the 6 optimizer steps.
+  * test_throughput_form_gradient_matches_autograd: one learn-sized launch at lr = 0 (parameters
+    stay put; AdamW's first moment after steps s = 1, 2 is sum_s (1 - b1) b1^(2-s) c_s g_s, so it
+    exposes the raw clipped gradients) against float64 autograd of the reference loss, on a full
+    and a ragged minibatch, with ratios spread across the clip range.
+"""
+import copy
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+from learn_inputs import digest, learn_inputs  # noqa: E402
+from test_engine_gpu import _away_from_kinks, _data, _grad_f64, _run  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+# Weights after learn() vs the reference's CPU learn(), absolute.  Six AdamW steps of lr 1e-3 move
+# a weight by up to 6e-3.  The engine reduces each 65,536-row gradient in another order than
+# torch's CPU GEMMs (per tile, per workgroup, then per slice in float64), ~1e-7 relative; AdamW's
+# first steps are ~lr * sign(g), so those differences reach the weights as ~lr * (relative
+# gradient difference) per step plus the sign flips of near-zero gradient entries (GroupNorm's
+# scale-invariant directions), bounded by the steps' size.  CartPole: 2e-6 as at mb 512
+# (test_stack_gpu).  Pendulum: 17-dim-free but |logp| of the narrow Gaussian reaches ~10, whose
+# float32 rounding moves ratios by ~1e-6: 1e-5, <= 0.2 % of the steps' movement.
+WEIGHT_ATOL = {"learn_mb65536": 2e-6, "learn_cont_mb65536": 1e-5}
+
+
+def _sub(g, prefix):
+    return {k[len(prefix):]: torch.from_numpy(np.array(g[k])) for k in g.files if k.startswith(prefix)}
+
+
+@pytest.mark.parametrize("tag", ["learn_mb65536", "learn_cont_mb65536"])
+def test_large_minibatch_learn_matches_reference_learn(golden, tag):
+    import prl_native
+    from PPO import PPO
+    g = golden(tag)
+    cont = bool(int(g["continuous"]))
+    N, mb, D, A = int(g["N"]), int(g["mb"]), int(g["D"]), int(g["A_dim"])
+    S, Aa, _, _ = learn_inputs(N, D, A, cont)
+    Aa = Aa.astype(np.float32)
+    assert digest(S, Aa) == str(g["inputs_sha256"]), "learn_inputs() no longer reproduces the fixture"
+    p = PPO(is_continuous=cont, observ_dim=D, action_dim=A, action_scaling=2.0 if cont else None,
+            lr=1e-3, k_epochs=int(g["k_epochs"]), policy_clip=0.2, GAE_lambda=0.95, gamma=0.995,
+            batch_size=min(1024, N), mini_batch_size=mb)
+    p.show_progress = False
+    init = _sub(g, "init/")
+    p.policy.load_state_dict(init)
+    p.policy_old.load_state_dict(init)
+    p.memory.push_device(*(torch.from_numpy(np.ascontiguousarray(x)).cuda()
+                           for x in (S, Aa, g["R"], g["Dn"])))
+    p.learn()
+    torch.cuda.synchronize()
+    assert p.last_update_path == "fused"
+    plan = prl_native.ppo_update_last_plan()
+    assert plan == {"form": "throughput", "waves": 8, "grid": 256, "tiles": 16,
+                    "specialised": True}, plan
+    _, _, _, adv, returns = p._last_update_inputs
+    ret_ref, adv_ref = g["returns"].astype(np.float64), g["adv"].astype(np.float64)
+    # GAE is bit-exact against the reference (test_kernels_gpu); here it runs on our old values
+    # (GPU float32 GEMMs), hence 1e-5 relative as north_star states
+    assert np.all(np.abs(returns.cpu().double().numpy() - ret_ref) <= 1e-5 * np.abs(ret_ref) + 1e-5)
+    assert np.all(np.abs(adv.cpu().double().numpy() - adv_ref) <= 1e-5 * np.abs(adv_ref) + 1e-6)
+    sd, ref = p.policy.state_dict(), _sub(g, "final/")
+    worst = max(float((sd[k].cpu().double() - ref[k].double()).abs().max()) for k in ref)
+    moved = max(float((ref[k].double() - init[k].double()).abs().max()) for k in ref)
+    print(f"{tag}: max |w - w_ref| {worst:.3e} (the 6 steps moved weights by up to {moved:.3e})")
+    assert worst <= WEIGHT_ATOL[tag], worst
+    old = p.policy_old.state_dict()
+    for k, v in sd.items():
+        assert torch.equal(old[k], v)
+
+
+def _eng_logp(eng, policy, S, A):
+    logp, _ = eng.evaluate(policy, S, A)
+    return logp
+
+
+@pytest.mark.parametrize("cont", [False, True])
+@pytest.mark.parametrize("mb", [8192, 65536])
+@pytest.mark.parametrize("spread", [0.3, 3.0])
+def test_throughput_form_gradient_matches_autograd(cont, mb, spread):
+    """Two optimizer steps at lr = 0 — minibatch 0 full (mb rows: 2 or 16 tiles per workgroup),
+    minibatch 1 ragged — in one throughput-form launch; old_logp = logp + noise(spread) puts
+    ratios on both sides of the clip range (spread 3 also beyond the +-20 clamp's neighbourhood
+    of the kinks, which _away_from_kinks keeps rows off).  exp_avg / 0.1 after the launch is
+    0.9 c_0 g_0 + c_1 g_1 (c_s: clip_grad_norm_ coefficients); each g_s comes from float64
+    autograd of the reference loss on that minibatch at the engine's own float32 log-prob values
+    (continuous log-probs' float32 rounding is amplified by the mu gradients' cancelling sums,
+    DESIGN.md §4; the forward itself is checked against float64 separately).  Tolerance 1e-4 of
+    each tensor's largest entry, as the latency form's test_fused_gradient_off_policy."""
+    import prl_native
+    D = 3 if cont else 4
+    ragged = mb // 4 + 3
+    N = mb + ragged
+    data = _data(N, D, cont, seed=47)
+    p = _run(True, cont, data, mb, 1, lr=0.0)
+    S_, A_, old, adv, ret = p._last_update_inputs
+    g = torch.Generator(device="cuda").manual_seed(11)
+    old2 = _away_from_kinks(p, S_, A_, old + spread * torch.randn(old.shape, device="cuda", generator=g))
+    eng = p._engine
+    logp_eng = _eng_logp(eng, p.policy, S_, A_)
+    with torch.no_grad():
+        l64, _, _ = copy.deepcopy(p.policy).cpu().double().get_evaluate(S_.cpu().double(),
+                                                                          A_.cpu().double())
+    fwd = float((logp_eng.cpu().double() - l64).abs().max()) / (1.0 + float(l64.abs().max()))
+    assert fwd <= 2e-6, fwd
+    eng.m.zero_()
+    eng.v.zero_()
+    eng.step.zero_()
+    eng.run(S_, A_, old2, adv, ret, 1)
+    torch.cuda.synchronize()
+    plan = prl_native.ppo_update_last_plan()
+    assert plan["form"] == "throughput" and plan["waves"] == 8 and plan["specialised"], plan
+    assert plan["tiles"] == mb // 256 // 16, plan
+    assert float(eng.step.item()) == 2.0
+    parts = []
+    for lo, hi in ((0, mb), (mb, N)):
+        sl = slice(lo, hi)
+        parts.append(_grad_f64(p, (S_[sl], A_[sl], old2[sl], adv[sl], ret[sl]),
+                               logp_val=logp_eng[sl]))
+    per = {}
+    for i, (name, prm) in enumerate(p.policy.named_parameters()):
+        want = 0.9 * parts[0][i] + parts[1][i]
+        m = p.optimizer.state[prm]["exp_avg"].double().cpu() / 0.1
+        per[name] = float((m - want).abs().max()) / (float(want.abs().max()) + 1e-30)
+    print({n: f"{e:.1e}" for n, e in per.items()})
+    assert max(per.values()) <= 1e-4, per
