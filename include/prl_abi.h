@@ -337,6 +337,14 @@ int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A, int32_t di
 int64_t prl_colsum_partial_floats(int64_t rows, int32_t cols);
 int prl_colsum_f32(const float* x, int64_t rows, int32_t cols, float* out, float* partial,
                    int64_t partial_floats, void* stream);
+/* nn.utils.clip_grad_norm_(params, max_norm) followed by AdamW.step() (PPO/PPO.py:248-250; torch
+ * defaults, capturable: step[0] f32 on the device is incremented first) over FLAT f32 vectors of
+ * P entries in parameters() order: params, exp_avg, exp_avg_sq and grad (left clipped, as torch
+ * leaves p.grad).  The norm is summed in float64 in a fixed order (deterministic).  One launch,
+ * graph-capturable; the wide step's optimizer tail (PPO/update.py).  16-B aligned buffers. */
+int prl_flat_adamw(float* params, float* exp_avg, float* exp_avg_sq, float* step, float* grad,
+                   int64_t P, float lr, float beta1, float beta2, float eps, float weight_decay,
+                   float max_norm, void* stream);
 /* Host call: device address of the u32 status words inside an engine workspace ([0] last
  * launch, [1] sticky timeout flag). */
 int prl_ppo_update_status_ptr(void* workspace, uint32_t** status);
@@ -380,6 +388,10 @@ int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, int32_t D, 
  * sequence number of this launch's first step: 0 for the first launch on a buffer set, then
  * advanced by nb_union x k_epochs per launch, the same on every rank (the flags only grow, so
  * one buffer set serves every later launch).  All ranks' launches must be resident together.
+ * fine_grained != 0 when ANY rank's slice buffer is fine-grained memory (prl_dp_xbuf_alloc's
+ * fallback): each workgroup then orders its slice stores before its flag with a system-scope
+ * release fence and its slice loads after the poll with a system-scope acquire fence (the
+ * uncached form relies on write-through system-scope stores and cache-missing loads instead).
  * No reference counterpart (the reference is single-process). */
 int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step,
                        int32_t D, int32_t A, int32_t discrete, const float* S,
@@ -388,8 +400,8 @@ int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_sq, float* 
                        int32_t nb_union, const float* inv_count, float clip, float vf_coef,
                        float ent_coef, float lr, float beta1, float beta2, float eps,
                        float weight_decay, float max_norm, float* loss_out, int32_t world,
-                       int32_t rank, void* const* xbufs, int64_t seq0, void* workspace,
-                       int64_t workspace_bytes, void* stream);
+                       int32_t rank, void* const* xbufs, int64_t seq0, int32_t fine_grained,
+                       void* workspace, int64_t workspace_bytes, void* stream);
 int64_t prl_dp_xbuf_bytes(int32_t D, int32_t A, int32_t discrete, int32_t mini_batch);
 /* polls of prl_ppo_update_dpx's cross-rank wait before it gives up (the launch then ends with a
  * nonzero status word and the caller restores its snapshot, PPO/engine.py); 0 restores the
@@ -410,7 +422,10 @@ int32_t prl_ppo_update_set_tp(int32_t mode);
  * out[4] = 1 for a compile-time-layout (CartPole / Pendulum) kernel, 0 for the runtime layout.
  * All -1 before the first launch.  No reference counterpart (tests assert which kernel ran). */
 void prl_ppo_update_last_plan(int32_t out[5]);
-int prl_dp_xbuf_alloc(int64_t bytes, void** out);
+/* A zeroed slice buffer of its own (shareable by IPC handle).  *kind in: 0 = uncached, falling
+ * back to fine-grained memory, 1 = uncached only, 2 = fine-grained only; out: 1 = uncached,
+ * 2 = fine-grained (what the buffer is; prl_ppo_update_dpx's fine_grained follows it). */
+int prl_dp_xbuf_alloc(int64_t bytes, int32_t* kind, void** out);
 int prl_dp_xbuf_free(void* p);
 int prl_dp_ipc_handle(void* p, uint8_t* out, int64_t out_bytes);   /* out: 64 bytes */
 int prl_dp_ipc_open(const uint8_t* handle, int64_t bytes, void** out);

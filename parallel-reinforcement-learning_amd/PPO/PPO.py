@@ -424,9 +424,16 @@ class PPO:
                     loss = graphed.wide_step(j)
                     pbar.update(counts[j])
                     continue
+                fa = graphed.fa if graphed is not None else None
+                if fa is not None:   # torch's AdamW takes this step: hand it the native state
+                    fa.sync()
                 out = self._eager_step(S, A, old_logp, adv, returns, j, counts[j], world)
+                if fa is not None:
+                    fa.prepare()
                 loss = out if out is not None else loss
                 pbar.update(counts[j])
+        if graphed is not None:
+            graphed.finish()
         self.last_loss = loss.detach().clone() if loss is not None else None
         self.last_graph_replays = graphed.replays if graphed is not None else 0
         if loss is not None and self.show_progress:

@@ -132,6 +132,7 @@ class FusedUpdate:
                       enumerate(("B: partials landed", "B: slice stored", "C: gradient landed"))}
         if p[30] > 0:
             out["shader_clock_GHz"] = round(p[31] / (p[30] * 10.0), 3)
+        out["clipped_steps_frac"] = round(p[28] / steps, 4)   # clip_grad_norm_ active
         return out
 
     def run(self, S, A, old_logp, adv, ret, k_epochs: int):
@@ -239,17 +240,23 @@ class FusedUpdate:
         if not (tdist.is_available() and tdist.is_initialized()):
             return None
         world, rank = tdist.get_world_size(), tdist.get_rank()
-        own, handle = None, b""
+        own, handle, kind = None, b"", None
         if 1 < world <= 8:
             try:
-                own = prl_native.dp_xbuf_alloc(
-                    prl_native.dp_xbuf_bytes(self.D, self.A, self.discrete, self.mini_batch))
+                # PRL_DP_XBUF=fine forces the fine-grained fallback (tests), "uncached" forbids it
+                own, kind = prl_native.dp_xbuf_alloc(
+                    prl_native.dp_xbuf_bytes(self.D, self.A, self.discrete, self.mini_batch),
+                    os.environ.get("PRL_DP_XBUF", "auto"))
                 handle = prl_native.dp_ipc_handle(own)
             except (RuntimeError, ValueError) as e:
                 warnings.warn(f"data-parallel slice buffer unavailable ({e})")
-                own, handle = None, b""
+                own, handle, kind = None, b"", None
         handles = [None] * world
-        tdist.all_gather_object(handles, handle)
+        tdist.all_gather_object(handles, (handle, kind))
+        # the flags are fenced when ANY rank's buffer is fine-grained (prl_ppo_update_dpx)
+        self._dp_fine = any(k == "fine" for _, k in handles)
+        self.dp_xbuf_kinds = [k for _, k in handles]
+        handles = [h for h, _ in handles]
         ptrs, ok = [], all(len(h) > 0 for h in handles)
         if ok:
             try:
@@ -308,7 +315,7 @@ class FusedUpdate:
                 inv, self.ppo.policy_clip, self.ppo.value_coef, self.ppo.entropy_coef,
                 group["lr"], group["betas"][0], group["betas"][1], group["eps"],
                 group["weight_decay"], 2.0, loss, world, self._dp_rank, self._xbufs,
-                self._dp_seq, self.ws)
+                self._dp_seq, self.ws, fine_grained=self._dp_fine)
             self._dp_seq += 2
             torch.cuda.synchronize()
             status = max(prl_native.ppo_update_status(self.ws).tolist())
@@ -360,7 +367,7 @@ class FusedUpdate:
                 ret.contiguous(), mb, k_epochs, nb, inv, self.ppo.policy_clip,
                 self.ppo.value_coef, self.ppo.entropy_coef, group["lr"], beta1, beta2,
                 group["eps"], group["weight_decay"], 2.0, self.loss, world, self._dp_rank, xb,
-                self._dp_seq, self.ws)
+                self._dp_seq, self.ws, fine_grained=self._dp_fine)
             launch_error = None
         except (RuntimeError, ValueError) as e:
             # this rank did not launch (e.g. an argument check): it still joins the gather

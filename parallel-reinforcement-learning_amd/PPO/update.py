@@ -37,6 +37,103 @@ def wide_info(ppo, D: int):
     return info
 
 
+class FlatAdamState:
+    """The policy's parameters, gradients and AdamW state as flat f32 vectors in parameters()
+    order, for prl_flat_adamw (clip_grad_norm_(2.0) + AdamW.step() in one launch, PPO.py:248-250):
+    every Parameter's .data, every .grad (PPO._ensure_flat_grads) and the optimizer's exp_avg /
+    exp_avg_sq state tensors are VIEWS of these buffers, so torch's own optimizer, state_dict()
+    and save_weights see the same copy (as engine.FusedUpdate does for the persistent engine).
+    The step count lives in one device scalar; sync() writes it into the optimizer's per-param
+    state."""
+
+    def __init__(self, ppo):
+        self.ppo = ppo
+        self.params = [p for p in ppo.policy.parameters()]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.empty(n, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.step = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._bind()
+
+    def _views(self, buf):
+        out, off = [], 0
+        for p in self.params:
+            out.append(buf[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        return out
+
+    def _bind(self):
+        opt = self.ppo.optimizer
+        self.step.zero_()
+        with torch.no_grad():
+            for p, fv, mv, vv in zip(self.params, self._views(self.flat), self._views(self.m),
+                                     self._views(self.v)):
+                fv.copy_(p.data)
+                p.data = fv
+                st = opt.state.get(p)
+                if st and "exp_avg" in st:
+                    mv.copy_(st["exp_avg"])
+                    vv.copy_(st["exp_avg_sq"])
+                    self.step.copy_(torch.as_tensor(st["step"], dtype=torch.float32).reshape(1))
+                    st["exp_avg"], st["exp_avg_sq"] = mv, vv
+                else:
+                    mv.zero_()
+                    vv.zero_()
+
+    def bound(self) -> bool:
+        opt = self.ppo.optimizer
+        for p, fv, mv in zip(self.params, self._views(self.flat), self._views(self.m)):
+            if p.data.data_ptr() != fv.data_ptr():
+                return False
+            st = opt.state.get(p)
+            if st and "exp_avg" in st and st["exp_avg"].data_ptr() != mv.data_ptr():
+                return False
+        return True
+
+    def prepare(self):
+        """Before a learn's first step: re-bind if the parameters or the optimizer state were
+        replaced, else take the optimizer's step count (torch may have stepped in between)."""
+        if not self.bound():
+            self._bind()
+            return
+        st = self.ppo.optimizer.state.get(self.params[0])
+        if st and "step" in st:
+            self.step.copy_(torch.as_tensor(st["step"], dtype=torch.float32).reshape(1))
+
+    def launch(self, grad, max_norm=2.0):
+        group = self.ppo.optimizer.param_groups[0]
+        beta1, beta2 = group["betas"]
+        prl_native.flat_adamw(self.flat, self.m, self.v, self.step, grad, group["lr"], beta1,
+                              beta2, group["eps"], group["weight_decay"], max_norm)
+
+    def sync(self):
+        """The optimizer's state = this one's: moments as views, step counts = ours."""
+        opt = self.ppo.optimizer
+        group = opt.param_groups[0]
+        on_device = bool(group.get("capturable") or group.get("fused"))
+        for p, mv, vv in zip(self.params, self._views(self.m), self._views(self.v)):
+            st = opt.state[p]
+            st["exp_avg"], st["exp_avg_sq"] = mv, vv
+            if "step" in st and torch.is_tensor(st["step"]):
+                st["step"].copy_(self.step.reshape(st["step"].shape))
+            else:
+                st["step"] = (self.step.reshape(()).clone() if on_device
+                              else torch.tensor(float(self.step.item())))
+
+
+def flat_adam_state(ppo):
+    """ppo's FlatAdamState (built once per policy), re-armed for this learn()."""
+    fa = getattr(ppo, "_flat_adam", None)
+    params = list(ppo.policy.parameters())
+    if fa is None or len(fa.params) != len(params) or any(a is not b for a, b in zip(fa.params, params)):
+        fa = ppo._flat_adam = FlatAdamState(ppo)
+    else:
+        fa.prepare()
+    return fa
+
+
 class GraphedUpdate:
     WARMUP = 2
 
@@ -74,22 +171,33 @@ class GraphedUpdate:
         # in place) instead of ~60 PyTorch / hipBLASLt kernels.  Part of the native path
         # (ppo.use_fused); PRL_WIDE=0 or use_fused = False keeps the autograd step
         self.wide = None
+        self.fa = None
         info = wide_info(ppo, S.shape[1])
         if info is not None:
             self.wide = info
-            self.pflat = torch.empty(info[0], dtype=torch.float32, device=dev)
             self.part = torch.empty(info[1], dtype=torch.float32, device=dev)
             self.cursor_e = torch.zeros(1, dtype=torch.int64, device=dev)
             self.sources[1] = self.sources[1].float().contiguous()
+            # parameters / gradient / AdamW state as flat vectors: the kernel reads the
+            # parameters in place and clip_grad_norm_ + AdamW are one launch (prl_flat_adamw);
+            # PRL_WIDE_ADAM=0 keeps torch's clip_grad_norm_ + fused AdamW
+            if os.environ.get("PRL_WIDE_ADAM", "1") != "0":
+                self.fa = flat_adam_state(ppo)
+            else:
+                self.pflat = torch.empty(info[0], dtype=torch.float32, device=dev)
 
     def _wide_grad(self, cursor, scales):
         """Gradient of minibatch `cursor` into the flat gradient buffer (p.grad views) or, on
         data-parallel ranks, into self.flat (the all-reduce buffer); loss into loss_out."""
         ppo = self.ppo
         grads = ppo._ensure_flat_grads()
-        torch.cat([p.detach().reshape(-1) for p in self.params], out=self.pflat)
+        if self.fa is not None:
+            pflat = self.fa.flat          # the parameters themselves (views of it)
+        else:
+            pflat = self.pflat
+            torch.cat([p.detach().reshape(-1) for p in self.params], out=pflat)
         S, A2, old, adv, ret = self.sources
-        prl_native.ppo_wide_grad(self.pflat, S.shape[1], ppo.action_dim, not ppo.is_continuous,
+        prl_native.ppo_wide_grad(pflat, S.shape[1], ppo.action_dim, not ppo.is_continuous,
                                  S, A2, old, adv, ret, self.mb, cursor, scales, ppo.policy_clip,
                                  ppo.value_coef, ppo.entropy_coef,
                                  self.flat if scales is not None else grads, self.loss_out,
@@ -100,8 +208,11 @@ class GraphedUpdate:
         ragged last minibatch of an epoch)."""
         self.cursor_e.fill_(j)
         self._wide_grad(self.cursor_e, None)
-        nn.utils.clip_grad_norm_(self.params, 2.0)
-        self.ppo.optimizer.step()
+        if self.fa is not None:
+            self.fa.launch(self.ppo._flat_grad)
+        else:
+            nn.utils.clip_grad_norm_(self.params, 2.0)
+            self.ppo.optimizer.step()
         return self.loss_out
 
     def _forward_backward(self):
@@ -122,6 +233,10 @@ class GraphedUpdate:
         self.loss_out.copy_(loss.detach())
 
     def _apply(self):
+        if self.fa is not None:   # the all-reduced buffer on data-parallel ranks
+            self.fa.launch(self.flat if self.scales is not None else self.ppo._flat_grad)
+            self.cursor.add_(1)
+            return
         if self.scales is not None:
             grads = [p.grad for p in self.params]
             torch._foreach_copy_(grads, [f.view_as(g) for f, g in
@@ -130,8 +245,14 @@ class GraphedUpdate:
         self.ppo.optimizer.step()
         self.cursor.add_(1)
 
+    def finish(self):
+        """After the learn's last step: the optimizer's state reflects the native steps."""
+        if self.fa is not None:
+            self.fa.sync()
+
     def _step_eager(self):
-        self.ppo.optimizer.zero_grad(set_to_none=True)
+        if self.fa is None:
+            self.ppo.optimizer.zero_grad(set_to_none=True)
         self._forward_backward()
         if self.scales is not None:
             self.ppo.all_reduce(self.flat)
@@ -160,7 +281,8 @@ class GraphedUpdate:
             torch.cuda.current_stream().wait_stream(side)
             if done == n_steps:
                 return done
-            self.ppo.optimizer.zero_grad(set_to_none=True)
+            if self.fa is None:
+                self.ppo.optimizer.zero_grad(set_to_none=True)
             self.graph = torch.cuda.CUDAGraph()
             if self.scales is None:
                 with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):

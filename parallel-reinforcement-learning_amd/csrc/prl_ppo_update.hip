@@ -151,6 +151,7 @@ struct UpdArgs {
   const float* inv_count;    // [nb] 1 / rows of union minibatch j over all ranks (null: 1 / B)
   unsigned long long dp_seq0;   // exchange sequence number of this launch's first step
   unsigned dp_spin_limit;       // polls of the cross-rank wait before it gives up
+  int dp_fine;                  // some rank's slice buffer is fine-grained: fence the flag
   float* xbuf[UPD_MAX_RANKS];             // rank r's [2][Qtot * 4] slice buffers (peer mappings)
   unsigned long long* xflag[UPD_MAX_RANKS];   // rank r's [G] per-workgroup step flags
   float* xbuf_self;                       // == xbuf[rank] (no dynamic kernarg indexing)
@@ -1406,13 +1407,25 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
 // system-scope too (they miss every cache), and the __syncthreads below orders them after the
 // poll.  A formal system-scope release / acquire would add buffer_wbl2 / buffer_inv of the whole
 // L2 per workgroup per step, writing back or dropping the minibatch rows every workgroup keeps
-// in L2, for ordering the encodings already give.
+// in L2, for ordering the encodings already give.  That argument holds for the uncached
+// allocation only; when any rank's buffer is fine-grained (prl_dp_xbuf_alloc's fallback,
+// args.dp_fine) the flag store follows a system-scope release and the slice loads a system-scope
+// acquire.
 
 __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t rs_red, int Qtot,
                                    int g, int G, unsigned long long gstep, int par, int* s_abort) {
   const int t = threadIdx.x, NT = blockDim.x;
   const unsigned long long want = gstep + 1ull;
-  if (t == 0) __hip_atomic_store(upd_g(args.xflag_self + g), want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t == 0) {
+    if (args.dp_fine) {
+      // fine-grained slice buffers (prl_dp_xbuf_alloc's fallback) may be cached: a system-scope
+      // release makes this workgroup's drained slice stores visible before its flag (the asm
+      // wait keeps the compiler from dropping the release's wait, MI355X_MICROARCH.md)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __hip_atomic_store(upd_g(args.xflag_self + g), want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (t < 64) {
     unsigned long long* fl = args.xflag[0];   // lane r polls rank r (selected, not indexed)
 #pragma unroll
@@ -1436,6 +1449,12 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
       __builtin_amdgcn_s_sleep(1);
     }
     if (t == 0) *s_abort = ok ? 0 : 1;
+    if (args.dp_fine && ok) {
+      // ... and a system-scope acquire after the matched poll, before any slice load (the
+      // workgroup barrier below holds the other waves until it has completed)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
   if (*s_abort) return false;
@@ -1706,6 +1725,8 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       for (int w = 0; w < NW; ++w) tot += s_nrm[w];
       const float coef = args.max_norm / (sqrtf(tot) + 1e-6f);
       clipc = coef < 1.0f ? coef : 1.0f;
+      // profile: steps whose clip_grad_norm_ scaled the gradient (prof[28])
+      if (args.profile && g == 0 && t == 0 && coef < 1.0f) tm[20] += 1ull;
       if (g == 0 && t == 0 && s + 1 == args.total_steps) {
         const float4 lp = ld4_sc1(rs_red, (size_t)Qp * 4);
         loss_last = lp.x * invB + args.vf_coef * (lp.y * invB) - args.ent_coef * (lp.z * invB);
@@ -2289,6 +2310,7 @@ struct UpdDp {
   const float* inv_count;
   void* const* xbufs;
   int64_t seq0;
+  int fine;
 };
 // the slice buffers [2][Qtot * 4] f32, then the per-workgroup step flags [G] u64
 size_t upd_xbuf_flags_off(const UpdNet& n) { return (((size_t)n.Lp / 4 + 1) * 32 + 255) & ~(size_t)255; }
@@ -2362,6 +2384,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     args.inv_count = dp->inv_count;
     args.dp_seq0 = (unsigned long long)dp->seq0;
     args.dp_spin_limit = g_dp_spin_limit;
+    args.dp_fine = dp->fine ? 1 : 0;
     const size_t fo = upd_xbuf_flags_off(args.net);
     for (int r = 0; r < dp->world; ++r) {
       PRL_REQUIRE(dp->xbufs[r], "prl_ppo_update_dpx: null slice buffer of rank %d", r);
@@ -2431,9 +2454,10 @@ extern "C" int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_
                                   float ent_coef, float lr, float beta1, float beta2, float eps,
                                   float weight_decay, float max_norm, float* loss_out,
                                   int32_t world, int32_t rank, void* const* xbufs, int64_t seq0,
-                                  void* workspace, int64_t workspace_bytes, void* stream) {
+                                  int32_t fine_grained, void* workspace, int64_t workspace_bytes,
+                                  void* stream) {
   PRL_REQUIRE(nb_union > 0 && seq0 >= 0, "prl_ppo_update_dpx: nb_union <= 0 or seq0 < 0");
-  const UpdDp dp{world, rank, nb_union, inv_count, xbufs, seq0};
+  const UpdDp dp{world, rank, nb_union, inv_count, xbufs, seq0, fine_grained};
   return upd_run(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp,
                  adv, ret, N, mini_batch, k_epochs, clip, vf_coef, ent_coef, lr, beta1, beta2, eps,
                  weight_decay, max_norm, loss_out, workspace, workspace_bytes, stream, &dp);
@@ -2461,16 +2485,22 @@ extern "C" int64_t prl_dp_xbuf_bytes(int32_t D, int32_t A, int32_t discrete, int
   return (int64_t)(upd_xbuf_flags_off(net) + (size_t)upd_grid(mini_batch) * 8);
 }
 
-extern "C" int prl_dp_xbuf_alloc(int64_t bytes, void** out) {
-  PRL_REQUIRE(bytes > 0 && out, "prl_dp_xbuf_alloc: bad arguments");
+extern "C" int prl_dp_xbuf_alloc(int64_t bytes, int32_t* kind, void** out) {
+  PRL_REQUIRE(bytes > 0 && out && kind && *kind >= 0 && *kind <= 2, "prl_dp_xbuf_alloc: bad arguments");
   // Its own allocation (shareable by IPC handle), UNCACHED: other GPUs read it over xGMI while
   // this GPU writes it, and coarse-grained memory is not coherent across devices inside a
   // kernel (RCCL keeps its cross-GPU flags and FIFOs in uncached / fine-grained memory too).
+  // Fine-grained memory is the fallback (the kernel then fences the flags: dp_fine).
   void* p = nullptr;
-  if (hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached) != hipSuccess) {
+  const int want = *kind;
+  if (want != 2 && hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached) == hipSuccess) {
+    *kind = 1;
+  } else {
     (void)hipGetLastError();
     p = nullptr;
+    PRL_REQUIRE(want != 1, "prl_dp_xbuf_alloc: no uncached memory");
     PRL_HIP_TRY(hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocFinegrained));
+    *kind = 2;
   }
   const hipError_t e = hipMemset(p, 0, (size_t)bytes);
   if (e != hipSuccess) {

@@ -241,3 +241,99 @@ extern "C" int prl_colsum_f32(const float* x, int64_t rows, int32_t cols, float*
   PRL_LAUNCH_CHECK("colsum_fold");
   return PRL_OK;
 }
+
+// ---- clip_grad_norm_ + AdamW over flat buffers (the wide step's optimizer tail) --------------
+// PPO.py:248-250: nn.utils.clip_grad_norm_(policy.parameters(), max_norm) then AdamW.step()
+// (torch defaults: decoupled weight decay, lerp for exp_avg, addcmul for exp_avg_sq, bias
+// corrections from the incremented step count).  Parameters, gradient and both moments are flat
+// vectors in parameters() order (the policy's Parameters and the optimizer's state are views of
+// them, PPO/update.py FlatAdamState).  One workgroup of 1024 threads: the squared norm with float64
+// accumulators in a fixed thread -> wave -> workgroup order (deterministic), the clip coefficient
+// max_norm / (norm + 1e-6) clamped to 1 (the gradient is left clipped, as torch leaves p.grad),
+// then the elementwise update with the persistent engine's arithmetic (prl_ppo_update.hip
+// phase C).  ~37 K parameters (C5's net): a few microseconds, one launch instead of torch's
+// foreach-norm / stack / norm / coefficient / foreach-mul / fused-AdamW chain.
+constexpr int FA_THREADS = 1024;
+
+__global__ __launch_bounds__(FA_THREADS) void flat_adamw_kernel(
+    float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, float* __restrict__ step,
+    float* __restrict__ grad, int64_t P, float lr, float beta1, float beta2, float eps, float wd,
+    float max_norm) {
+  __shared__ double s_part[FA_THREADS / 64];
+  __shared__ float s_c[3];
+  const int t = threadIdx.x;
+  const int64_t Q = P / 4;
+  double acc = 0.0;
+  for (int64_t q = t; q < Q; q += FA_THREADS) {
+    const float4 x = reinterpret_cast<const float4*>(grad)[q];
+    acc = fma((double)x.x, (double)x.x, acc);
+    acc = fma((double)x.y, (double)x.y, acc);
+    acc = fma((double)x.z, (double)x.z, acc);
+    acc = fma((double)x.w, (double)x.w, acc);
+  }
+  for (int64_t k = 4 * Q + t; k < P; k += FA_THREADS) acc = fma((double)grad[k], (double)grad[k], acc);
+  acc = wave_sum(acc);
+  if ((t & 63) == 0) s_part[t >> 6] = acc;
+  const float step0 = step[0];
+  __syncthreads();
+  if (t == 0) {
+    double tot = 0.0;
+    for (int w = 0; w < FA_THREADS / 64; ++w) tot += s_part[w];
+    const float coef = max_norm / ((float)sqrt(tot) + 1e-6f);
+    s_c[0] = coef < 1.0f ? coef : 1.0f;
+    const double tstep = (double)step0 + 1.0;
+    s_c[1] = (float)((double)lr / (1.0 - pow((double)beta1, tstep)));    // step size
+    s_c[2] = (float)(1.0 / sqrt(1.0 - pow((double)beta2, tstep)));       // 1 / sqrt(bc2)
+    step[0] = step0 + 1.0f;
+  }
+  __syncthreads();
+  const float clipc = s_c[0], step_size = s_c[1], inv_bc2_sqrt = s_c[2];
+  const float decay = (float)(1.0 - (double)lr * (double)wd);
+  const float omb1 = (float)(1.0 - (double)beta1), omb2 = (float)(1.0 - (double)beta2);
+  auto upd = [&](float g, float& pw, float& mw, float& vw) {
+    const float gr = g * clipc;
+    pw = pw * decay;
+    mw = fmaf(omb1, gr - mw, mw);
+    vw = fmaf(omb2 * gr, gr, vw * beta2);
+    const float denom = fmaf(__builtin_amdgcn_sqrtf(vw), inv_bc2_sqrt, eps);
+    float rq = __builtin_amdgcn_rcpf(denom);
+    rq = fmaf(rq, fmaf(-denom, rq, 1.0f), rq);   // one Newton step: ~0.5 ulp
+    pw = fmaf(-step_size, mw * rq, pw);
+    return gr;
+  };
+  for (int64_t q = t; q < Q; q += FA_THREADS) {
+    float4 g4 = reinterpret_cast<const float4*>(grad)[q];
+    float4 p4 = reinterpret_cast<const float4*>(p)[q];
+    float4 m4 = reinterpret_cast<const float4*>(m)[q];
+    float4 v4 = reinterpret_cast<const float4*>(v)[q];
+    g4.x = upd(g4.x, p4.x, m4.x, v4.x);
+    g4.y = upd(g4.y, p4.y, m4.y, v4.y);
+    g4.z = upd(g4.z, p4.z, m4.z, v4.z);
+    g4.w = upd(g4.w, p4.w, m4.w, v4.w);
+    reinterpret_cast<float4*>(grad)[q] = g4;
+    reinterpret_cast<float4*>(p)[q] = p4;
+    reinterpret_cast<float4*>(m)[q] = m4;
+    reinterpret_cast<float4*>(v)[q] = v4;
+  }
+  for (int64_t k = 4 * Q + t; k < P; k += FA_THREADS) {
+    float pw = p[k], mw = m[k], vw = v[k];
+    grad[k] = upd(grad[k], pw, mw, vw);
+    p[k] = pw;
+    m[k] = mw;
+    v[k] = vw;
+  }
+}
+
+extern "C" int prl_flat_adamw(float* params, float* exp_avg, float* exp_avg_sq, float* step,
+                              float* grad, int64_t P, float lr, float beta1, float beta2, float eps,
+                              float weight_decay, float max_norm, void* stream) {
+  PRL_REQUIRE(P > 0 && P < (int64_t)1 << 30, "prl_flat_adamw: bad size %lld", (long long)P);
+  PRL_REQUIRE(params && exp_avg && exp_avg_sq && step && grad, "prl_flat_adamw: null pointer");
+  PRL_REQUIRE(aligned16(params) && aligned16(exp_avg) && aligned16(exp_avg_sq) && aligned16(grad),
+              "prl_flat_adamw: buffers must be 16-B aligned");
+  hipLaunchKernelGGL(flat_adamw_kernel, dim3(1), dim3(FA_THREADS), 0, as_stream(stream), params,
+                     exp_avg, exp_avg_sq, step, grad, P, lr, beta1, beta2, eps, weight_decay,
+                     max_norm);
+  PRL_LAUNCH_CHECK("flat_adamw");
+  return PRL_OK;
+}

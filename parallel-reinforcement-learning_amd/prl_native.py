@@ -72,13 +72,14 @@ SIGNATURES = {
     "prl_ppo_update_dp": [_P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I32,
                           _I64, _P, _I64] + [_F32] * 9 + [_P, _P, _P, _I64, _P, _P],
     "prl_ppo_update_dpx": [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32,
-                           _I32, _I32, _P] + [_F32] * 9 + [_P, _I32, _I32, _P, _I64, _P, _I64, _P],
+                           _I32, _I32, _P] + [_F32] * 9 + [_P, _I32, _I32, _P, _I64, _I32, _P,
+                                                           _I64, _P],
     "prl_dp_xbuf_bytes": [_I32, _I32, _I32, _I32],
     "prl_dp_set_spin_limit": [ctypes.c_uint32],
     "prl_ppo_update_set_tp": [_I32],
     "prl_ppo_update_last_plan": [_P],
     "prl_source_id": [],
-    "prl_dp_xbuf_alloc": [_I64, _P],
+    "prl_dp_xbuf_alloc": [_I64, _P, _P],
     "prl_dp_xbuf_free": [_P],
     "prl_dp_ipc_handle": [_P, _P, _I64],
     "prl_dp_ipc_open": [_P, _I64, _P],
@@ -91,11 +92,12 @@ SIGNATURES = {
     "prl_ppo_adam_step": [_P, _P, _P, _I32, _I32, _I32, _P, _I64] + [_F32] * 9 + [_P, _P],
     "prl_colsum_partial_floats": [_I64, _I32],
     "prl_colsum_f32": [_P, _I64, _I32, _P, _P, _I64, _P],
+    "prl_flat_adamw": [_P, _P, _P, _P, _P, _I64] + [_F32] * 6 + [_P],
     "prl_ppo_grad_fold_step": [_P] * 7 + [_I64, _F32, _I32, _I32, _I32] + [_P] * 5
                               + [_I64, _I32, _I64] + [_F32] * 10 + [_P, _P, _P, _I64, _P],
 }
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_source_id": ctypes.c_char_p,
-             "prl_ppo_update_last_plan": None,"prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,
+             "prl_ppo_update_last_plan": None, "prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,
              "prl_dp_set_spin_limit": ctypes.c_uint32, "prl_ppo_update_set_tp": _I32,
              "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
 
@@ -649,6 +651,20 @@ def ppo_update_set_tp(mode: int) -> int:
     return int(lib().prl_ppo_update_set_tp(int(mode)))
 
 
+def flat_adamw(params, exp_avg, exp_avg_sq, step, grad, lr, beta1, beta2, eps, weight_decay,
+               max_norm):
+    """clip_grad_norm_(max_norm) + AdamW.step() over flat f32 vectors (one launch)."""
+    P = int(params.numel())
+    for t, n in ((exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq"), (grad, "grad")):
+        if t.numel() != P:
+            raise ValueError(f"{n} has {t.numel()} entries, params {P}")
+    _check(lib().prl_flat_adamw(
+        _dev(params, torch.float32, "params"), _dev(exp_avg, torch.float32, "exp_avg"),
+        _dev(exp_avg_sq, torch.float32, "exp_avg_sq"), _dev(step, torch.float32, "step"),
+        _dev(grad, torch.float32, "grad"), P, float(lr), float(beta1), float(beta2), float(eps),
+        float(weight_decay), float(max_norm), _stream()), "prl_flat_adamw")
+
+
 def ppo_update_last_plan() -> dict:
     """What the last prl_ppo_update / _dpx launch in this process ran: form ("throughput" /
     "latency"), waves per workgroup, workgroups, 16-row tiles per workgroup and step, and
@@ -660,11 +676,18 @@ def ppo_update_last_plan() -> dict:
             "tiles": tiles, "specialised": bool(spec == 1)}
 
 
-def dp_xbuf_alloc(nbytes: int) -> ctypes.c_void_p:
-    """A zeroed device allocation of its own (shareable by IPC handle)."""
+XBUF_KINDS = {"auto": 0, "uncached": 1, "fine": 2}
+
+
+def dp_xbuf_alloc(nbytes: int, kind: str = "auto"):
+    """A zeroed device allocation of its own (shareable by IPC handle): uncached memory, or
+    fine-grained memory as the fallback ("auto"); kind "uncached" / "fine" forces one.  Returns
+    (pointer, "uncached" | "fine")."""
     p = ctypes.c_void_p()
-    _check(lib().prl_dp_xbuf_alloc(int(nbytes), ctypes.byref(p)), "prl_dp_xbuf_alloc")
-    return p
+    k = ctypes.c_int32(XBUF_KINDS[kind])
+    _check(lib().prl_dp_xbuf_alloc(int(nbytes), ctypes.byref(k), ctypes.byref(p)),
+           "prl_dp_xbuf_alloc")
+    return p, {1: "uncached", 2: "fine"}[k.value]
 
 
 def dp_xbuf_free(p):
@@ -695,9 +718,10 @@ def dp_ipc_close(p):
 def ppo_update_dpx(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp,
                    adv, ret, mini_batch, k_epochs, nb_union, inv_count, clip, vf_coef, ent_coef,
                    lr, beta1, beta2, eps, weight_decay, max_norm, loss_out, world, rank, xbufs,
-                   seq0, workspace):
+                   seq0, workspace, fine_grained=False):
     """The persistent engine as one data-parallel rank: the cross-rank gradient sum runs inside
-    the launch over the ranks' IPC-mapped slice buffers `xbufs` (rank order)."""
+    the launch over the ranks' IPC-mapped slice buffers `xbufs` (rank order); fine_grained: any
+    rank's buffer is fine-grained memory (the flags are then fenced)."""
     N = int(S.shape[0])
     arr = (ctypes.c_void_p * len(xbufs))(*[ctypes.c_void_p(getattr(x, "value", x)) for x in xbufs])
     _check(lib().prl_ppo_update_dpx(
@@ -710,7 +734,8 @@ def ppo_update_dpx(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, ac
         float(vf_coef), float(ent_coef), float(lr), float(beta1), float(beta2), float(eps),
         float(weight_decay), float(max_norm), _dev(loss_out, torch.float32, "loss_out"),
         int(world), int(rank), ctypes.cast(arr, ctypes.c_void_p), int(seq0),
-        _dev(workspace, torch.uint8, "workspace"), workspace.numel(), _stream()),
+        int(bool(fine_grained)), _dev(workspace, torch.uint8, "workspace"), workspace.numel(),
+        _stream()),
         "prl_ppo_update_dpx")
 
 

@@ -89,9 +89,10 @@ def test_two_ranks_graphed_equal_one_process_on_the_union(tmp_path, fused):
         np.testing.assert_allclose(outs[0][key], ref[key], rtol=0, atol=2e-5, err_msg=key)
 
 
-def _dpx_worker(rank, world, port, mb, nb, k, out_dir):
+def _dpx_worker(rank, world, port, mb, nb, k, out_dir, xbuf="auto"):
     sys.path[:0] = PATHS
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PRL_DP_PERSISTENT="1")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PRL_DP_PERSISTENT="1",
+                      PRL_DP_XBUF=xbuf)
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
@@ -104,8 +105,9 @@ def _dpx_worker(rank, world, port, mb, nb, k, out_dir):
         p.learn()       # a second launch on the same slice buffers (flags carry global steps)
         torch.cuda.synchronize()
         sd = {kk: v.cpu().numpy() for kk, v in p.policy.state_dict().items()}
-        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **sd, _path=np.array(p.last_update_path),
-                 _loss=np.float32(p.last_loss.item()))
+        np.savez(os.path.join(out_dir, f"{'' if xbuf == 'auto' else xbuf}rank{rank}.npz"), **sd,
+                 _path=np.array(p.last_update_path), _loss=np.float32(p.last_loss.item()),
+                 _kinds=np.array(p._engine.dp_xbuf_kinds))
         p._engine.close()
     finally:
         torch.distributed.destroy_process_group()
@@ -164,6 +166,31 @@ def test_two_ranks_persistent_dp_engine(tmp_path):
     (l1, v1), (l2, v2) = (_outputs(q, torch.from_numpy(S[:256]).cuda(),
                                    torch.from_numpy(A[:256]).cuda()) for q in (q1, q2))
     assert float((l1 - l2).abs().max()) <= 1e-4 and float((v1 - v2).abs().max()) <= 1e-4
+
+
+def test_two_ranks_persistent_dp_engine_fine_grained_buffers(tmp_path):
+    """The data-parallel persistent launch on prl_dp_xbuf_alloc's FALLBACK memory (fine-grained,
+    forced with PRL_DP_XBUF=fine): the flag store then follows a system-scope release and the
+    slice loads a system-scope acquire (args.dp_fine).  Same 2-rank workload as above; the
+    fences change no arithmetic, so both ranks end with exactly the bits of the default
+    (uncached) buffers."""
+    import random
+    mb, nb, k = 64, 5, 3
+    port = 29700 + random.randint(0, 30)
+    mp.spawn(_dpx_worker, args=(2, port, mb, nb, k, str(tmp_path), "auto"), nprocs=2, join=True)
+    mp.spawn(_dpx_worker, args=(2, port + 40, mb, nb, k, str(tmp_path), "fine"), nprocs=2,
+             join=True)
+    auto = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(2)]
+    fine = [np.load(os.path.join(tmp_path, f"finerank{r}.npz")) for r in range(2)]
+    assert [str(x) for x in fine[0]["_kinds"]] == ["fine", "fine"]
+    assert [str(x) for x in auto[0]["_kinds"]] == ["uncached", "uncached"]
+    assert str(fine[0]["_path"]) == "fused-dp-persistent"
+    for key in auto[0].files:
+        if key.startswith("_"):
+            continue
+        for r in range(2):
+            np.testing.assert_array_equal(fine[r][key], auto[0][key], err_msg=key)
+    assert float(fine[0]["_loss"]) == float(auto[0]["_loss"])
 
 
 def _nccl_one_rank_worker(port, out_dir):

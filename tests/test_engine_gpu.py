@@ -405,7 +405,7 @@ def test_dpx_one_rank_equals_engine(cont):
             def upd(S, A_, old, adv, ret, n_ranks, p=p, state=state):
                 eng = p._fused_engine()
                 if state["xb"] is None:
-                    state["xb"] = prl_native.dp_xbuf_alloc(
+                    state["xb"], _ = prl_native.dp_xbuf_alloc(
                         prl_native.dp_xbuf_bytes(eng.D, eng.A, eng.discrete, eng.mini_batch))
                 n, mb = int(S.shape[0]), eng.mini_batch
                 nb = -(-n // mb)

@@ -378,3 +378,81 @@ def test_wide_graphed_rollout_equals_eager_rollout(monkeypatch):
     assert r1 == r0
     for x, y in zip(m1, m0):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("scale", [1e-3, 1e2])
+def test_flat_adamw_matches_torch_clip_and_adamw(scale):
+    """prl_flat_adamw (the wide step's optimizer tail: clip_grad_norm_(2.0) + AdamW.step() in one
+    launch over flat buffers, PPO.py:248-250) against torch's own clip_grad_norm_ + AdamW
+    (capturable) on C5's parameter shapes over four steps.  scale 1e-3: norm < 2, no clipping;
+    1e2: clipping every step.  The two differ only in float32 rounding (norm summed in float64
+    here, the AdamW division as rcp + one Newton step): parameters within 1e-9 absolute (each
+    step moves them ~1e-3), moments within 1e-5 relative, and the clipped gradient within 1e-6
+    relative."""
+    import prl_native
+    pol = _policy(True, 348, 17)
+    shapes = [p.shape for p in pol.parameters()]
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in pol.parameters()]
+    opt = torch.optim.AdamW(ref, lr=1e-3, capturable=True)
+    P = sum(p.numel() for p in ref)
+    flat = torch.cat([p.detach().reshape(-1) for p in ref]).contiguous()
+    m, v = torch.zeros_like(flat), torch.zeros_like(flat)
+    step = torch.zeros(1, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for _ in range(4):
+        grad = torch.randn(P, device="cuda", generator=g) * scale
+        off = 0
+        for p, sh in zip(ref, shapes):
+            p.grad = grad[off:off + p.numel()].view(sh).clone()
+            off += p.numel()
+        torch.nn.utils.clip_grad_norm_(ref, 2.0)
+        opt.step()
+        gbuf = grad.clone()
+        prl_native.flat_adamw(flat, m, v, step, gbuf, 1e-3, 0.9, 0.999, 1e-8, 1e-2, 2.0)
+        torch.cuda.synchronize()
+        want_g = torch.cat([p.grad.reshape(-1) for p in ref])
+        assert float((gbuf - want_g).abs().max()) <= 1e-6 * float(want_g.abs().max())
+    want = torch.cat([p.detach().reshape(-1) for p in ref])
+    assert float((flat - want).abs().max()) <= 1e-9, float((flat - want).abs().max())
+    wm = torch.cat([opt.state[p]["exp_avg"].reshape(-1) for p in ref])
+    wv = torch.cat([opt.state[p]["exp_avg_sq"].reshape(-1) for p in ref])
+    assert float((m - wm).abs().max()) <= 1e-5 * float(wm.abs().max())
+    assert float((v - wv).abs().max()) <= 1e-5 * float(wv.abs().max())
+    assert float(step.item()) == 4.0
+
+
+def test_wide_learn_native_adam_equals_torch_adam(monkeypatch):
+    """learn() on C5's net through the wide step with the native optimizer tail (default) and
+    with torch's clip_grad_norm_ + fused AdamW (PRL_WIDE_ADAM=0): same data, two epochs with a
+    ragged minibatch; the learned function agrees (log-probs / values on probe states, 1e-3 as
+    the wide step's other learn() comparisons: continuous log-probs amplify float32 rounding), the
+    optimizer's step count and state tensors stay consistent across two learn() calls."""
+    from PPO import PPO
+    rng = np.random.default_rng(2)
+    N, D, A = 3 * 512 + 77, 348, 17
+    S = torch.from_numpy((rng.normal(size=(N, D)) * 0.5).astype(np.float32)).cuda()
+    Aa = torch.from_numpy(np.tanh(rng.normal(size=(N, A))).astype(np.float32)).cuda()
+    R = torch.from_numpy(rng.normal(1, 0.5, N).astype(np.float32)).cuda()
+    Dn = torch.from_numpy((rng.random(N) < 0.05).astype(np.float32)).cuda()
+    Dn[-1] = 1
+    outs = []
+    for native in ("1", "0"):
+        monkeypatch.setenv("PRL_WIDE_ADAM", native)
+        torch.manual_seed(0)
+        p = PPO(True, D, A, action_scaling=1.0, k_epochs=2, batch_size=64, mini_batch_size=512)
+        p.show_progress = False
+        for _ in range(2):
+            p.memory.push_device(S, Aa, R, Dn)
+            p.learn()
+        torch.cuda.synchronize()
+        assert p._last_graphed.wide is not None
+        assert (p._last_graphed.fa is not None) == (native == "1")
+        st = p.optimizer.state[next(p.policy.parameters())]
+        assert float(st["step"]) == 2 * 2 * 4
+        with torch.no_grad():
+            lp, V, _ = copy.deepcopy(p.policy).double().get_evaluate(S[:1024].double(),
+                                                                     Aa[:1024].double())
+        outs.append((lp.cpu(), V.cpu()))
+    (l1, v1), (l0, v0) = outs
+    assert float((l1 - l0).abs().max()) <= 1e-3 * (1 + float(l0.abs().max()))
+    assert float((v1 - v0).abs().max()) <= 1e-3 * (1 + float(v0.abs().max()))
