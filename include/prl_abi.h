@@ -118,6 +118,22 @@ int prl_rollout_step_at(int kind, int64_t E, int64_t* step_dev, double* phys,
                         uint8_t* traj_done, int32_t* ep_len, int32_t* active_after,
                         double* reward_sum, void* stream);
 
+/* A WHOLE device rollout of a wide-net policy in ONE persistent launch (AsyncPPO.worker's loop,
+ * AsyncTools/AsyncPPO.py:117-146, with PPO.get_action's forward + sampling, PPO/PPO.py:81-96 /
+ * ActorCritic.get_dist, PPO/ActorCritic.py:85-105, and the env step, AsyncPPO.py:64-102): every
+ * env with terminal[e] == 0 is stepped until its episode ends — the action from the continuous
+ * actor (params: policy_old's flat parameters, torch parameters() order) sampled exactly as
+ * prl_rollout_step samples it, the trajectory rows, t_elapsed / ep_len / terminal and the counters
+ * written as the per-step kernels write them (active_after[t] += envs still active after step t,
+ * reward_sum[0] += rewards).  Each wave owns 16 envs and keeps the actor in LDS.  Supported:
+ * prl_wide_rollout_supported() (the synthetic env with its D = 348 / A = 17 continuous net). */
+int prl_wide_rollout_supported(int kind, int32_t D, int32_t A, int32_t discrete);
+int prl_wide_rollout(int kind, const float* params, int32_t D, int32_t A, int32_t discrete,
+                     int64_t E, double* phys, int32_t* t_elapsed, uint8_t* terminal,
+                     float action_scaling, uint64_t sample_seed, int32_t t_max, float* traj_obs,
+                     float* traj_act, float* traj_rew, uint8_t* traj_done, int32_t* ep_len,
+                     int32_t* active_after, double* reward_sum, void* stream);
+
 /* ---- mask / compaction / flatten (replace AsyncTools/utils.py) ----------------------------- */
 /* utils.indexes_of_active_environments + number_of_active_environments (utils.py:3-7):
  * idx_out[0..count) = ascending e with terminal[e] == 0; count_out[0] = count (int64). */

@@ -239,6 +239,11 @@ class AsyncPPO:  # AsyncPPO.py:104-165
         env.reset_device(tr.obs[0])
         tr.active_after.zero_()
         tr.reward_sum.zero_()
+        k = self._fused_rollout(seed, scaling)
+        if k is not None:
+            self._warm = True
+            self.last_vector_steps = k + 1
+            return k
         stream = torch.cuda.current_stream()
         graph = None
         if (self._warm and not getattr(self, "_graph_failed", False)
@@ -278,6 +283,28 @@ class AsyncPPO:  # AsyncPPO.py:104-165
         self._warm = True
         self.last_vector_steps = k + 1
         return k
+
+    def _fused_rollout(self, seed, scaling):
+        """The whole rollout as ONE persistent launch (prl_wide_rollout: each wave steps 16 envs to
+        the end of their episodes with policy_old's actor in LDS) where it applies — the wide
+        continuous nets on the synthetic env (C5); PRL_WIDE_ROLLOUT=0 keeps the per-step path.
+        Returns the index of the last vector step (max episode length - 1), or None."""
+        if os.environ.get("PRL_WIDE_ROLLOUT", "1") == "0":
+            return None
+        params_fn = getattr(self.ppo, "rollout_params", None)
+        spec, env, tr = self.env.spec, self.env, self._traj
+        if params_fn is None or not prl_native.wide_rollout_supported(
+                spec.kind, spec.obs_dim, spec.act_dim, spec.discrete):
+            return None
+        with torch.no_grad():
+            flat = params_fn(tr.obs[0])
+        if flat is None:
+            return None
+        prl_native.wide_rollout(spec.kind, flat, spec.obs_dim, spec.act_dim, spec.discrete,
+                                env.phys, env.t_elapsed, env.terminal, scaling, seed, tr.T,
+                                tr.obs, tr.act, tr.rew, tr.done, tr.ep_len, tr.active_after,
+                                tr.reward_sum)
+        return max(int(tr.ep_len.max().item()) - 1, 0)
 
     def _vector_step(self, k, obs, seed, scaling, active_after):
         """Policy forward on this step's observations + the fused rollout step kernel."""

@@ -219,6 +219,13 @@ class PPO:
         """Gather policy_old's current parameters into the flat buffer dist_params_at reads."""
         self._dist_flat(obs)
 
+    def rollout_params(self, obs: torch.Tensor):
+        """policy_old's parameters as one flat vector for AsyncPPO's persistent wide-net rollout
+        (prl_wide_rollout), gathered now; None when the native distribution path does not apply
+        (same rule as dist_params_at)."""
+        with torch.no_grad():
+            return self._dist_flat(obs)
+
     def _dist_flat(self, obs, gather: bool = True):
         """policy_old's parameters gathered into one persistent flat buffer for
         prl_ppo_wide_dist, or None when the native distribution path does not apply.  The gather

@@ -34,6 +34,9 @@ SIGNATURES = {
                          _P, _P, _P, _P, _P],
     "prl_rollout_step_at": [_INT, _I64, _P, _P, _P, _P, _P, _I64, _F32, _U64, _I32, _P, _P, _P,
                          _P, _P, _P, _P, _P],
+    "prl_wide_rollout_supported": [_INT, _I32, _I32, _I32],
+    "prl_wide_rollout": [_INT, _P, _I32, _I32, _I32, _I64, _P, _P, _P, _F32, _U64, _I32, _P, _P,
+                         _P, _P, _P, _P, _P, _P],
     "prl_active_indices": [_P, _I64, _P, _P, _P, _P],
     "prl_mask_update": [_P, _I64, _P, _I64, _P, _P],
     "prl_compact_rows": [_P, _I64, _I64, _P, _P, _P, _P, _P],
@@ -284,6 +287,30 @@ def rollout_step_at(kind, step_dev, phys, t_elapsed, terminal, dist, action_scal
                                      _dev(active_after, torch.int32, "active_after"),
                                      _dev(reward_sum, torch.float64, "reward_sum"), _stream()),
            "prl_rollout_step_at")
+
+
+def wide_rollout_supported(kind, D, A, discrete) -> bool:
+    return bool(lib().prl_wide_rollout_supported(int(kind), int(D), int(A), int(bool(discrete))))
+
+
+def wide_rollout(kind, params, D, A, discrete, phys, t_elapsed, terminal, action_scaling, seed,
+                 t_max, traj_obs, traj_act, traj_rew, traj_done, ep_len, active_after, reward_sum):
+    """The whole rollout of the wide continuous actor in one persistent launch (prl_wide_rollout):
+    every non-terminal env stepped to the end of its episode."""
+    E = t_elapsed.numel()
+    _check(lib().prl_wide_rollout(kind, _dev(params, torch.float32, "params"), int(D), int(A),
+                                  int(bool(discrete)), E, _dev(phys, torch.float64, "phys"),
+                                  _dev(t_elapsed, torch.int32, "t"),
+                                  _dev(terminal, torch.uint8, "terminal"), float(action_scaling),
+                                  int(seed) & (2**64 - 1), int(t_max),
+                                  _dev(traj_obs, torch.float32, "traj_obs"),
+                                  _dev(traj_act, torch.float32, "traj_act"),
+                                  _dev(traj_rew, torch.float32, "traj_rew"),
+                                  _dev(traj_done, torch.uint8, "traj_done"),
+                                  _dev(ep_len, torch.int32, "ep_len"),
+                                  _dev(active_after, torch.int32, "active_after"),
+                                  _dev(reward_sum, torch.float64, "reward_sum"), _stream()),
+           "prl_wide_rollout")
 
 
 # ------------------------------------------------------------------------- masks / buffers

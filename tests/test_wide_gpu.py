@@ -456,3 +456,62 @@ def test_wide_learn_native_adam_equals_torch_adam(monkeypatch):
     (l1, v1), (l0, v0) = outs
     assert float((l1 - l0).abs().max()) <= 1e-3 * (1 + float(l0.abs().max()))
     assert float((v1 - v0).abs().max()) <= 1e-3 * (1 + float(v0.abs().max()))
+
+
+def test_persistent_wide_rollout_matches_per_step_rollout(monkeypatch):
+    """prl_wide_rollout (the whole C5 rollout in ONE launch, each wave stepping 16 envs to the end
+    of their episodes) against the per-step path (prl_ppo_wide_dist + prl_rollout_step per vector
+    step, PRL_WIDE_ROLLOUT=0, eager) on the same runner seeds and policy, three rollouts with a
+    new policy_old before the third: observations, done flags and episode lengths bit for bit (the
+    synthetic env's do not depend on the actions); actions to float32 rounding of the two forward
+    orders (<= 2e-5 absolute, actions in [-1, 1]); rewards (1 - 0.01 sum a^2) to 1e-5.  The fused
+    actions are also checked against a float64 forward of policy_old with the same Philox
+    normals (oracle.sample_normal): tanh(mu + std z) to 2e-5."""
+    import oracle as O
+    from AsyncTools.AsyncPPO import AsyncPPO
+    from PPO import PPO
+    E = 300                      # 19 tiles, the last one ragged
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("PRL_WIDE_ROLLOUT", fused)
+        monkeypatch.setenv("PRL_ROLLOUT_GRAPH", "0")
+        torch.manual_seed(0)
+        p = PPO(True, 348, 17, action_scaling=1.0, batch_size=10**9, mini_batch_size=512)
+        a = AsyncPPO("SyntheticHumanoid-v0", p, num_envs=E, seed=5)
+        rec, mems, pols = [], [], []
+        for it in range(3):
+            if it == 2:
+                with torch.no_grad():
+                    for q in p.policy.parameters():
+                        q.add_(0.02 * torch.randn_like(q))
+                p.policy_old.load_state_dict(p.policy.state_dict())
+            seed = (a.sample_seed + a._rollouts * 0xD1B54A32D192ED03) & (2**64 - 1)
+            n = a.worker()
+            rec.append((n, float(a.reward_score)))
+            mems.append([x.cpu().clone() for x in p.memory.device_tensors("cuda")])
+            pols.append((copy.deepcopy(p.policy_old).cpu().double(), seed,
+                         a.env.t_elapsed.cpu().clone()))
+            p.memory.clear()
+        outs.append((rec, mems, pols))
+    (rf, mf, pf), (rs, ms, _) = outs
+    for it in range(3):
+        assert rf[it][0] == rs[it][0]
+        assert abs(rf[it][1] - rs[it][1]) <= 1e-6 * max(1.0, abs(rs[it][1]))
+        (S1, A1, R1, D1), (S0, A0, R0, D0) = mf[it], ms[it]
+        assert torch.equal(S1, S0) and torch.equal(D1, D0)
+        assert float((A1 - A0).abs().max()) <= 2e-5
+        assert float((R1 - R0).abs().max()) <= 1e-5
+        # fused actions vs a float64 forward with the kernel's Philox normals
+        pol, seed, lens = pf[it]
+        lens = lens.numpy().astype(np.int64)
+        e_of = np.repeat(np.arange(E), lens)
+        t_of = np.concatenate([np.arange(L) for L in lens])
+        idx = np.arange(0, len(e_of), 7)           # a sample of the transitions
+        with torch.no_grad():
+            feats = pol.model(S1[idx].double())
+            mu = pol.mu_head(feats)
+            sd = torch.nn.functional.softplus(torch.clamp(pol.log_std_head(feats), -2, 2))
+        z = torch.tensor([[O.sample_normal(seed, int(e_of[i]), int(t_of[i]), k) for k in range(17)]
+                          for i in idx], dtype=torch.float64)
+        want = torch.tanh(mu + sd * z)
+        assert float((A1[idx].double() - want).abs().max()) <= 2e-5
