@@ -236,14 +236,16 @@ __device__ inline unsigned upd_isum8(unsigned v) {
   return v;
 }
 // one whole wave: wait until the shards of counter `base` sum to >= target; false on timeout /
-// abort (same abort / status / sticky words as upd_wait)
+// abort (same abort / status / sticky words as upd_wait).  Lane 8 loads the abort word in the
+// same round as lanes 0-7 load the shards: one memory round trip per poll, not two in series.
 __device__ inline bool upd_wait_sharded(unsigned* ctr, int base, unsigned target) {
   const int l = threadIdx.x & 63;
   for (unsigned spins = 0;; ++spins) {
-    const unsigned v = l < UPD_SHARDS ? ld_sc1u(ctr + base + 32 * l) : 0u;
-    const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)upd_isum8(v), 0);
+    const unsigned v = l < UPD_SHARDS ? ld_sc1u(ctr + base + 32 * l)
+                                      : (l == UPD_SHARDS ? ld_sc1u(ctr + 2) : 0u);
+    const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)upd_isum8(l < UPD_SHARDS ? v : 0u), 0);
     if (tot >= target) return true;
-    if (ld_sc1u(ctr + 2) != 0u) return false;
+    if ((unsigned)__builtin_amdgcn_readlane((int)v, UPD_SHARDS) != 0u) return false;
     if (spins > UPD_SPIN_LIMIT) {
       if (l == 0) {
         __hip_atomic_store(upd_g(ctr + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -256,11 +258,13 @@ __device__ inline bool upd_wait_sharded(unsigned* ctr, int base, unsigned target
   }
 }
 
-// one lane: wait until *c >= target (or abort); false on timeout / abort
+// one lane: wait until *c >= target (or abort); false on timeout / abort (both words loaded in
+// one round)
 __device__ inline bool upd_wait(unsigned* ctr, int which, unsigned target) {
   for (unsigned spins = 0;; ++spins) {
-    if (ld_sc1u(ctr + which) >= target) return true;
-    if (ld_sc1u(ctr + 2) != 0u) return false;
+    const unsigned v = ld_sc1u(ctr + which), ab = ld_sc1u(ctr + 2);
+    if (v >= target) return true;
+    if (ab != 0u) return false;
     if (spins > UPD_SPIN_LIMIT) {
       __hip_atomic_store(upd_g(ctr + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(upd_g(ctr + 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1433,10 +1437,12 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
       if (t == r) fl = args.xflag[r];
     bool ok = true;
     for (unsigned spins = 0;; ++spins) {
+      // lanes < world poll the ranks' flags, lane 63 the abort word, in one round
       const bool ready = t >= args.world ||
                          __hip_atomic_load(upd_g(fl + g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= want;
+      const unsigned ab = t == 63 ? ld_sc1u(args.ctr + 2) : 0u;
       if (__ballot(!ready) == 0ull) break;
-      if (ld_sc1u(args.ctr + 2) != 0u) { ok = false; break; }
+      if ((unsigned)__builtin_amdgcn_readlane((int)ab, 63) != 0u) { ok = false; break; }
       if (spins > args.dp_spin_limit) {
         if (t == 0) {
           __hip_atomic_store(upd_g(args.ctr + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
