@@ -293,9 +293,10 @@ def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
         # shapes outside the persistent engine (C5): the per-step wide kernel, re-timed on the
         # last learn()'s first minibatch (cursor 0, mb rows) — the dominant kernel of that update
         cur0 = torch.zeros(1, dtype=torch.int64, device=gu.cursor.device)
-        wide_args = (gu.pflat, gu.sources[0].shape[1], ppo.action_dim, not ppo.is_continuous,
+        pflat = gu.fa.flat if gu.fa is not None else gu.pflat
+        wide_args = (pflat, gu.sources[0].shape[1], ppo.action_dim, not ppo.is_continuous,
                      *gu.sources, gu.mb, cur0, None, ppo.policy_clip, ppo.value_coef,
-                     ppo.entropy_coef, torch.empty_like(gu.pflat), torch.zeros(1, device=cur0.device),
+                     ppo.entropy_coef, torch.empty_like(pflat), torch.zeros(1, device=cur0.device),
                      gu.part)
         cold_med, _ = time_kernel(lambda: prl_native.ppo_wide_grad(*wide_args), cold=True)
         warm_med, _ = time_kernel(lambda: prl_native.ppo_wide_grad(*wide_args), cold=False)
