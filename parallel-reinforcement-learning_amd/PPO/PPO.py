@@ -420,9 +420,16 @@ class PPO:
         pbar = tqdm(total=sum(n_ranks) * self.k_epochs, leave=False,
                     disable=not self.show_progress or (world > 1 and tdist.get_rank() != 0))
         loss = None
+        # one GPU, wide step: every minibatch is a few native launches whose ~250 us of GPU time
+        # hides their host enqueue, so they run eagerly in order (no warm-up steps, no capture
+        # per learn); the captured graph stays for data-parallel ranks (all-reduce per step)
+        eager_wide = (graphed is not None and graphed.wide is not None and world == 1
+                      and os.environ.get("PRL_WIDE_GRAPH", "0") != "1")
         for _ in range(self.k_epochs):
             j0 = 0
-            if graphed is not None:
+            if eager_wide:
+                pass
+            elif graphed is not None:
                 j0 = graphed.run_epoch(n_graph)
                 loss = graphed.loss_out
                 pbar.update(sum(counts[:j0]))
