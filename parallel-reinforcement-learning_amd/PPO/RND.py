@@ -18,6 +18,32 @@ import prl_native
 from .layers import GroupNormSiLU, Linear
 
 
+class _MSELoss(torch.autograd.Function):
+    """nn.MSELoss()(preds, targets) (mean reduction) for update_pred's [mb, D] batches: the
+    difference is formed once and kept for the backward (2 (p - t) / numel), and the mean of its
+    squares is one rocBLAS dot instead of PyTorch-ROCm's generic reduction (~140 us per
+    65,536 x 348 batch, RND.py:112 at C5's mini_batch).  Float32, same value up to summation
+    order."""
+
+    @staticmethod
+    def forward(ctx, preds, targets):
+        d = (preds - targets).contiguous()
+        ctx.save_for_backward(d)
+        flat = d.view(-1)
+        return torch.dot(flat, flat) / float(flat.numel())
+
+    @staticmethod
+    def backward(ctx, g):
+        (d,) = ctx.saved_tensors
+        return d * (g * (2.0 / float(d.numel()))), None
+
+
+def mse_loss(preds, targets):
+    if preds.is_cuda and preds.dtype == torch.float32 and preds.shape == targets.shape:
+        return _MSELoss.apply(preds, targets)
+    return nn.functional.mse_loss(preds, targets)
+
+
 class RND(nn.Module):
     def __init__(self, in_features: int, out_features: int, beta: float = 0.001, device=None):
         super().__init__()
@@ -90,7 +116,9 @@ class RND(nn.Module):
                 with torch.no_grad():
                     targets = self.target_net(i)
                 preds = self.pred_net(i)
-                loss = self.loss_fn(preds, targets)
+                loss = (mse_loss(preds, targets)
+                        if isinstance(self.loss_fn, nn.MSELoss) and self.loss_fn.reduction == "mean"
+                        else self.loss_fn(preds, targets))
                 if counts is not None:
                     loss = loss * (i.shape[0] / counts[j])
                 loss.backward()
