@@ -432,12 +432,20 @@ uint32_t prl_dp_set_spin_limit(uint32_t polls);
  * Per process (initial value from PRL_UPD_TP); returns the previous mode.  No reference
  * counterpart (performance knob / tests). */
 int32_t prl_ppo_update_set_tp(int32_t mode);
+/* Replicas per tile group of the latency form (single GPU): every 16-row tile of a step runs on
+ * `replicas` workgroups at once, each publishing 1/replicas of the tile's partial gradient; the
+ * grid grows to tiles x replicas, capped at one workgroup per CU.  Same bits at every value.
+ * Per process (initial value from PRL_UPD_REPL); returns the previous value.  No reference
+ * counterpart (performance knob / tests). */
+int32_t prl_ppo_update_set_repl(int32_t replicas);
 /* What the last prl_ppo_update / prl_ppo_update_dpx call in this process launched:
  * out[0] = 1 for the throughput form, 0 for the latency form; out[1] = waves per workgroup;
  * out[2] = workgroups; out[3] = 16-row tiles per workgroup and step (ceil of rows / 16 / G);
- * out[4] = 1 for a compile-time-layout (CartPole / Pendulum) kernel, 0 for the runtime layout.
- * All -1 before the first launch.  No reference counterpart (tests assert which kernel ran). */
-void prl_ppo_update_last_plan(int32_t out[5]);
+ * out[4] = 1 for a compile-time-layout (CartPole / Pendulum) kernel, 0 for the runtime layout;
+ * out[5] = workgroups per tile group (the latency form's replicated tiles, PRL_UPD_REPL; out[2]
+ * counts them all).  All -1 before the first launch.  No reference counterpart (tests assert
+ * which kernel ran). */
+void prl_ppo_update_last_plan(int32_t out[6]);
 /* A zeroed slice buffer of its own (shareable by IPC handle).  *kind in: 0 = uncached, falling
  * back to fine-grained memory, 1 = uncached only, 2 = fine-grained only; out: 1 = uncached,
  * 2 = fine-grained (what the buffer is; prl_ppo_update_dpx's fine_grained follows it). */

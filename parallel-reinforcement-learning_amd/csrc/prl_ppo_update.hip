@@ -132,6 +132,7 @@ struct UpdArgs {
   const float* ret;
   int64_t N;
   int mb, nb, total_steps, G, R;
+  int Gt;           // tile groups (= G, or G / replicas in the latency form's replicated tiles)
   float clip, vf_coef, ent_coef, lr, beta1, beta2, eps, wd, max_norm;
   float* params;
   float* exp_avg;
@@ -1344,13 +1345,16 @@ struct UpdSub {
   }
 };
 
-// Phase B: workgroup g sums its slice [qlo, qhi) of the gradient quads over the G partials in
-// workgroup order (deterministic) with float64 accumulators (the partials of the output biases
-// cancel across workgroups), publishes the slice (sc1) and returns this thread's share of the
-// slice's sum of squares (parameter quads only).  Uses scratch as [spl][nq] double4.
+// Phase B: workgroup g sums its slice [qlo, qhi) of the G slices of the gradient quads over the
+// Gp partials in workgroup order (deterministic) with float64 accumulators (the partials of the
+// output biases cancel across workgroups), publishes the slice (sc1) and returns this thread's
+// share of the slice's sum of squares (parameter quads only).  Uses scratch as [spl][nq] double4.
+// (Gp < G: the latency form's replicated tiles, one partial per tile group; see ppo_update_body.)
 __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_red,
                                          int Qtot, int Qp, int g, int G, float* scratch, int NT,
-                                         int aux = UPD_AUX_SC1, UpdSub sub = UpdSub{nullptr, nullptr}) {
+                                         int aux = UPD_AUX_SC1, UpdSub sub = UpdSub{nullptr, nullptr},
+                                         int Gp = -1) {
+  if (Gp < 0) Gp = G;
   const int t = threadIdx.x;
   const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
   const int nq = qhi - qlo;
@@ -1365,20 +1369,20 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
     // wide slices (few workgroups): each thread owns whole quads, partials summed in order
     for (int qi = t; qi < nq; qi += NT) {
       double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
-      if (NT > 256) upd_sum_partials<8>(rs_part, Qtot, qlo + qi, 0, 1, G, ax, ay, az, aw);
-      else upd_sum_partials<16>(rs_part, Qtot, qlo + qi, 0, 1, G, ax, ay, az, aw);
+      if (NT > 256) upd_sum_partials<8>(rs_part, Qtot, qlo + qi, 0, 1, Gp, ax, ay, az, aw);
+      else upd_sum_partials<16>(rs_part, Qtot, qlo + qi, 0, 1, Gp, ax, ay, az, aw);
       fin(qi, ax, ay, az, aw);
     }
   } else if (nq > 0) {
     // narrow slices: split the G partials of each quad over spl threads, combine in LDS
     int spl = 1;
-    while (spl * 2 * nq <= NT && spl * 2 <= G) spl *= 2;
+    while (spl * 2 * nq <= NT && spl * 2 <= Gp) spl *= 2;
     double* red = reinterpret_cast<double*>(scratch);   // [spl][nq][4]
     if (t < spl * nq) {
       const int qi = t % nq, sub_ = t / nq;
       double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
-      if (NT > 256) upd_sum_partials<8>(rs_part, Qtot, qlo + qi, sub_, spl, G, ax, ay, az, aw);
-      else upd_sum_partials<16>(rs_part, Qtot, qlo + qi, sub_, spl, G, ax, ay, az, aw);
+      if (NT > 256) upd_sum_partials<8>(rs_part, Qtot, qlo + qi, sub_, spl, Gp, ax, ay, az, aw);
+      else upd_sum_partials<16>(rs_part, Qtot, qlo + qi, sub_, spl, Gp, ax, ay, az, aw);
       double* o = red + 4 * (sub_ * nq + qi);
       o[0] = ax; o[1] = ay; o[2] = az; o[3] = aw;
     }
@@ -1499,6 +1503,13 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
   constexpr bool TP = TPM > 0;
   extern __shared__ __align__(16) float upd_lds[];
   const int t = threadIdx.x, g = blockIdx.x, G = args.G;
+  // Replicated tiles (latency form, single GPU, PRL_UPD_REPL): workgroups g, g + Gt, g + 2 Gt, ...
+  // run the SAME rows (tile group gt = g % Gt: same inputs, same code, the same partial gradient
+  // bits) and each publishes only its 1/X share of that partial, so the publish moves 1/X of the
+  // bytes per workgroup and phase B's G slices are X times narrower; every workgroup then takes
+  // the whole reduced gradient in phase C as before.  Gt == G: no replication.
+  const int Gt = (TP || DP) ? G : args.Gt;
+  const int gt = (TP || DP) ? g : g % Gt;
   const int Lp = n.Lp;
   const int Qp = Lp / 4;            // parameter quads
   const int Qtot = Qp + 1;          // + one quad of loss partials
@@ -1571,11 +1582,11 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
   };
   unsigned long long* const tm = reinterpret_cast<unsigned long long*>(hdr + 16);
   // step s's first tile: its rows of minibatch s % nb (0 rows: every slot a dummy load)
-  auto first_row = [&](int s) { return (int64_t)(s % args.nb) * args.mb + (int64_t)g * R; };
+  auto first_row = [&](int s) { return (int64_t)(s % args.nb) * args.mb + (int64_t)gt * R; };
   auto first_rows = [&](int s) {
     const int64_t fmb0 = (int64_t)(s % args.nb) * args.mb;
     const int fB = (int)std::min<int64_t>(args.mb, args.N - fmb0);
-    return args.profile == 2 ? 0 : std::max(0, std::min(R, fB - g * R));
+    return args.profile == 2 ? 0 : std::max(0, std::min(R, fB - gt * R));
   };
   auto load_first = [&](int s) { load_next(first_row(s), first_rows(s)); };
   // Every prefetch is unconditional (clamped arguments instead of branches around it): a load
@@ -1588,8 +1599,8 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     const int B = (int)std::min<int64_t>(args.mb, args.N - mb0);
     const float invB = DP ? args.inv_count[j] : 1.0f / (float)B;
     // profile mode 2 (PRL_UPD_PROFILE=2, diagnostics only): no rows, i.e. the exchange alone
-    const int myrows = args.profile == 2 ? 0 : std::max(0, std::min(R, B - g * R));
-    const int64_t myrow0 = mb0 + (int64_t)g * R;
+    const int myrows = args.profile == 2 ? 0 : std::max(0, std::min(R, B - gt * R));
+    const int64_t myrow0 = mb0 + (int64_t)gt * R;
     // ---- phase A: partial gradient of this workgroup's rows ------------------------------------
     UpdGradOf<KD, KA> gr;
     if constexpr (TP) gr.zero();
@@ -1623,8 +1634,11 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     if constexpr (TP) {
       upd_grad_publish<KD, KA>(n, gr, upd_rsrc(args.part + (size_t)g * Qtot * 4));
     } else {
-      for (int q = t; q < Qtot; q += NT)
-        st4_sc1(rs_part, ((size_t)g * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
+      // replica g / Gt of tile group gt publishes quads [qa, qb) of the group's partial
+      const int rep = g / Gt, X = G / Gt;
+      const int qa = (int)((int64_t)Qtot * rep / X), qb = (int)((int64_t)Qtot * (rep + 1) / X);
+      for (int q = qa + t; q < qb; q += NT)
+        st4_sc1(rs_part, ((size_t)gt * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1656,7 +1670,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       const unsigned long long gstep = args.dp_seq0 + (unsigned long long)s;
       const int par = (int)(gstep & 1ull);
       (void)upd_slice_reduce(rs_part, dp ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
-                             Qtot, Qp, g, G, scratch, NT, dp ? UPD_AUX_SYS : UPD_AUX_SC1, subm);
+                             Qtot, Qp, g, G, scratch, NT, dp ? UPD_AUX_SYS : UPD_AUX_SC1, subm, Gt);
       subm.mark(1);   // slice combined, its stores issued
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -2233,6 +2247,23 @@ const void* upd_eval_kernel_for(const UpdNet& n) {
 }
 
 int upd_grid(int64_t mb) { return (int)std::min<int64_t>(256, cdiv(mb, UPD_RT)); }
+// Replicas per tile group of the latency form (ppo_update_body: workgroups g, g + Gt, ... run the
+// same rows and split the publish): PRL_UPD_REPL (default 1), capped so that all Gt x X
+// workgroups fit one per CU.
+int g_repl = [] {
+  const char* e = getenv("PRL_UPD_REPL");
+  const int v = e ? atoi(e) : 1;
+  return v >= 1 ? v : 1;
+}();
+int upd_repl(int Gt) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 1;
+  int x = g_repl;
+  while (x > 1 && Gt * x > cus) --x;
+  return x;
+}
 
 // The persistent kernels need all G workgroups resident at once (they hand data to each other).
 // A plain launch gives the same residency as a cooperative one (MI355X_MICROARCH.md,
@@ -2321,7 +2352,7 @@ struct UpdDp {
 // the slice buffers [2][Qtot * 4] f32, then the per-workgroup step flags [G] u64
 size_t upd_xbuf_flags_off(const UpdNet& n) { return (((size_t)n.Lp / 4 + 1) * 32 + 255) & ~(size_t)255; }
 unsigned g_dp_spin_limit = UPD_DP_SPIN_LIMIT;
-int32_t g_last_plan[5] = {-1, -1, -1, -1, -1};   // prl_ppo_update_last_plan
+int32_t g_last_plan[6] = {-1, -1, -1, -1, -1, -1};   // prl_ppo_update_last_plan
 
 int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, int32_t D,
             int32_t A, int32_t discrete, const float* S, const float* actions,
@@ -2335,9 +2366,9 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   PRL_REQUIRE(N > 0 && mini_batch > 0 && k_epochs >= 0, "prl_ppo_update: bad sizes");
   PRL_REQUIRE(params && exp_avg && exp_avg_sq && adam_step && S && actions && old_logp && adv && ret &&
                   workspace, "prl_ppo_update: null pointer");
-  const int G = upd_grid(mini_batch);
+  const int Gt = upd_grid(mini_batch);   // tile groups (one partial each)
   UpdWs ws;
-  const size_t need = upd_ws_carve(args.net, G, reinterpret_cast<char*>(workspace), &ws);
+  const size_t need = upd_ws_carve(args.net, Gt, reinterpret_cast<char*>(workspace), &ws);
   PRL_REQUIRE((size_t)workspace_bytes >= need, "prl_ppo_update: workspace %lld < %zu bytes",
               (long long)workspace_bytes, need);
   const int64_t nb = dp ? (int64_t)dp->nb : cdiv(N, (int64_t)mini_batch);
@@ -2353,8 +2384,8 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   args.mb = mini_batch;
   args.nb = (int)nb;
   args.total_steps = (int)(nb * k_epochs);
-  args.G = G;
-  args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RT) * UPD_RT;
+  args.Gt = Gt;
+  args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)Gt), (int64_t)UPD_RT) * UPD_RT;
   args.clip = clip;
   args.vf_coef = vf_coef;
   args.ent_coef = ent_coef;
@@ -2411,6 +2442,9 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     if (p2.kern) plan = p2;
     else tp = false;
   }
+  // replicated tiles: the latency form on one GPU only
+  const int G = (tp || dp) ? Gt : Gt * upd_repl(Gt);
+  args.G = G;
   const size_t lds = upd_lds_bytes_plan(args.net, plan.nw, tp, plan.tiles);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_update: %zu B of LDS needed", lds);
   hipStream_t st = as_stream(stream);
@@ -2422,6 +2456,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   g_last_plan[3] = args.R / UPD_RT;
   g_last_plan[4] = (!upd_force_generic() && (upd_is_cartpole(args.net) ||
                                              (!args.net.discrete && args.net.A == 1 && args.net.D == 3))) ? 1 : 0;
+  g_last_plan[5] = G / Gt;
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr + UPD_CTR_A, 0, 4 * (UPD_CTR_WORDS - UPD_CTR_A), st));
@@ -2475,8 +2510,14 @@ extern "C" int32_t prl_ppo_update_set_tp(int32_t mode) {
   return prev;
 }
 
-extern "C" void prl_ppo_update_last_plan(int32_t out[5]) {
-  for (int i = 0; i < 5; ++i) out[i] = g_last_plan[i];
+extern "C" int32_t prl_ppo_update_set_repl(int32_t replicas) {
+  const int prev = g_repl;
+  g_repl = replicas >= 1 ? replicas : 1;
+  return prev;
+}
+
+extern "C" void prl_ppo_update_last_plan(int32_t out[6]) {
+  for (int i = 0; i < 6; ++i) out[i] = g_last_plan[i];
 }
 
 extern "C" uint32_t prl_dp_set_spin_limit(uint32_t polls) {
@@ -2611,6 +2652,7 @@ extern "C" int prl_ppo_grad_step(const float* img_params, int32_t D, int32_t A, 
   args.N = N;
   args.mb = mini_batch;
   args.G = G;
+  args.Gt = G;
   args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RT) * UPD_RT;
   args.clip = clip;
   args.vf_coef = vf_coef;
@@ -2689,6 +2731,7 @@ extern "C" int prl_ppo_grad_fold_step(const float* in_p, const float* in_m, cons
   args.N = N;
   args.mb = mini_batch;
   args.G = G;
+  args.Gt = G;
   args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RT) * UPD_RT;
   args.clip = clip;
   args.vf_coef = vf_coef;
@@ -2827,6 +2870,7 @@ extern "C" int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, 
   args.N = N;
   args.mb = mini_batch;
   args.G = G;
+  args.Gt = G;
   args.R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)G), (int64_t)UPD_RT) * UPD_RT;
   args.clip = clip;
   args.vf_coef = vf_coef;

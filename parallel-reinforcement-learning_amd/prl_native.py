@@ -80,6 +80,7 @@ SIGNATURES = {
     "prl_dp_xbuf_bytes": [_I32, _I32, _I32, _I32],
     "prl_dp_set_spin_limit": [ctypes.c_uint32],
     "prl_ppo_update_set_tp": [_I32],
+    "prl_ppo_update_set_repl": [_I32],
     "prl_ppo_update_last_plan": [_P],
     "prl_source_id": [],
     "prl_dp_xbuf_alloc": [_I64, _P, _P],
@@ -102,6 +103,7 @@ SIGNATURES = {
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_source_id": ctypes.c_char_p,
              "prl_ppo_update_last_plan": None, "prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,
              "prl_dp_set_spin_limit": ctypes.c_uint32, "prl_ppo_update_set_tp": _I32,
+             "prl_ppo_update_set_repl": _I32,
              "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
 
 _lib = None
@@ -678,6 +680,12 @@ def ppo_update_set_tp(mode: int) -> int:
     return int(lib().prl_ppo_update_set_tp(int(mode)))
 
 
+def ppo_update_set_repl(replicas: int) -> int:
+    """Workgroups per 16-row tile group of the engine's latency form (each publishes its share of
+    the tile's partial gradient); returns the previous value.  Every value gives the same bits."""
+    return int(lib().prl_ppo_update_set_repl(int(replicas)))
+
+
 def flat_adamw(params, exp_avg, exp_avg_sq, step, grad, lr, beta1, beta2, eps, weight_decay,
                max_norm):
     """clip_grad_norm_(max_norm) + AdamW.step() over flat f32 vectors (one launch)."""
@@ -694,13 +702,14 @@ def flat_adamw(params, exp_avg, exp_avg_sq, step, grad, lr, beta1, beta2, eps, w
 
 def ppo_update_last_plan() -> dict:
     """What the last prl_ppo_update / _dpx launch in this process ran: form ("throughput" /
-    "latency"), waves per workgroup, workgroups, 16-row tiles per workgroup and step, and
-    whether the kernel was a compile-time-layout specialisation."""
-    out = (ctypes.c_int32 * 5)()
+    "latency"), waves per workgroup, workgroups, 16-row tiles per workgroup and step, whether
+    the kernel was a compile-time-layout specialisation, and the workgroups per tile group (the
+    latency form's replicated tiles)."""
+    out = (ctypes.c_int32 * 6)()
     lib().prl_ppo_update_last_plan(out)
-    tp, nw, G, tiles, spec = list(out)
+    tp, nw, G, tiles, spec, repl = list(out)
     return {"form": {1: "throughput", 0: "latency"}.get(tp), "waves": nw, "grid": G,
-            "tiles": tiles, "specialised": bool(spec == 1)}
+            "tiles": tiles, "specialised": bool(spec == 1), "replicas": repl}
 
 
 XBUF_KINDS = {"auto": 0, "uncached": 1, "fine": 2}

@@ -644,3 +644,51 @@ def test_throughput_form_equals_latency_form(cont, mb, N):
         a, b = outs[0][k].double(), outs[1][k].double()
         assert float((a - b).abs().max()) <= 1e-3 * float(a.abs().max()) + 1e-12, names[k]
     assert abs(float(outs[0][4]) - float(outs[1][4])) <= 1e-4 * max(1.0, abs(float(outs[0][4])))
+
+
+@pytest.mark.parametrize("cont", [False, True])
+@pytest.mark.parametrize("mb,N", [(512, 512 * 5 + 77), (1000, 1000 * 3 + 1)])
+def test_replicated_tiles_equal_single(cont, mb, N):
+    """The latency form's replicated tiles (prl_ppo_update_set_repl): with X workgroups per
+    16-row tile group, each publishing 1/X of the group's partial gradient and phase B cut into
+    X times more slices, every replica computes the same partial bits and the slice sums run over
+    the same partials in the same order, so parameters, moments, step count and loss are the same
+    BITS as with one workgroup per tile.  mb 1000: 63 tile groups (the grid capped at one
+    workgroup per CU: 4 replicas fit, 8 do not)."""
+    import prl_native
+    from PPO import PPO
+    D, A = (3, 1) if cont else (4, 2)
+    data = _data(N, D, cont, seed=47)
+    torch.manual_seed(0)
+    p = PPO(cont, D, A, action_scaling=2.0 if cont else None, k_epochs=2, batch_size=64,
+            mini_batch_size=mb)
+    p.show_progress = False
+    eng = p._fused_engine()
+    init = [eng.flat.clone(), eng.m.clone(), eng.v.clone(), eng.step.clone()]
+    p.memory.push_device(*data)
+    p.learn()
+    torch.cuda.synchronize()
+    ins = [x.clone() for x in p._last_update_inputs]
+    Gt = -(-mb // 16)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    outs = {}
+    for x in (1, 2, 3, 4, 8):
+        prev = prl_native.ppo_update_set_repl(x)
+        try:
+            for dst, src in zip((eng.flat, eng.m, eng.v, eng.step), init):
+                dst.copy_(src)
+            eng.ws.fill_(0)
+            loss = eng.run(*ins, 2)
+            torch.cuda.synchronize()
+            plan = prl_native.ppo_update_last_plan()
+            want = max(r for r in range(1, x + 1) if Gt * r <= cus)
+            assert plan["form"] == "latency" and plan["replicas"] == want, plan
+            assert plan["grid"] == Gt * want, plan
+            outs[x] = [t.cpu().clone() for t in (eng.flat, eng.m, eng.v, eng.step, loss)]
+        finally:
+            prl_native.ppo_update_set_repl(prev)
+    assert not torch.equal(outs[1][0], init[0].cpu())
+    names = ("params", "exp_avg", "exp_avg_sq", "step", "loss")
+    for x in (2, 3, 4, 8):
+        for a, b, name in zip(outs[1], outs[x], names):
+            assert torch.equal(a, b), (x, name, float((a.double() - b.double()).abs().max()))
