@@ -386,7 +386,27 @@ def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
         if env_scale:
             roofline_env["at_scale"] = env_at_scale(cfg["env"], spec_, scaling, bpe)
 
+    # world > 1: the N = 1 rate of the same per-GPU workload in the same run — rank 0 alone runs
+    # one more iteration as a single-GPU job (learn() with world 1: no collective, the
+    # single-GPU engine) while the other ranks wait at a barrier, so value / n1 reads as the
+    # speedup over one GPU from this one line (north_star's >= 6x at 8 GPUs)
+    n1 = None
+    if world > 1 and getattr(args, "n1_check", True):
+        if eng is not None:
+            eng.events = None
+        if rank == 0:
+            ppo._world = lambda: 1
+            try:
+                n, t_roll, t_learn, _ = iteration()
+            finally:
+                del ppo._world
+            n1 = {"value": round(n / (t_roll + t_learn), 1), "transitions": n,
+                  "rollout_s": round(t_roll, 3), "learn_s": round(t_learn, 3),
+                  "how": "rank 0 alone, one iteration after the timed region, learn() as a "
+                         "single-GPU job (the other ranks idle at a barrier)"}
+        dist.barrier()
     out = {"value": round(total_n / elapsed, 1), "ms_per_step": round(elapsed / steps * 1e3, 2),
+           "n1_same_run": n1,
            "steps": steps, "warmup": warmup, "elapsed_s": elapsed, "total_n": total_n,
            "rollout_env_steps_per_s": round(total_n / max(roll_max, 1e-9), 1),
            "learn_ms_per_1M": round(learn_per_tr * (1 << 20) * 1e3, 1),
@@ -433,6 +453,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm, the measured configuration) or gloo (rehearsal of "
                          "the multi-rank path with several ranks on one GPU)")
+    ap.add_argument("--no-n1-check", dest="n1_check", action="store_false",
+                    help="world > 1: skip rank 0's single-GPU iteration (n1_same_run)")
     ap.add_argument("--dump-gae", default=None,
                     help="save the roofline GAE launch's inputs (torch.save) for PMC passes")
     args = ap.parse_args()
@@ -515,6 +537,9 @@ def main():
                        "mini_batch_size": cfg["mb"], "k_epochs": cfg["k_epochs"],
                        "parallelism": f"dp{world}"},
         }
+        if res["n1_same_run"] is not None:
+            out["n1_same_run"] = res["n1_same_run"]
+            out["speedup_vs_1gpu"] = round(res["value"] / res["n1_same_run"]["value"], 3)
         for k in ("rollout_env_steps_per_s", "learn_ms_per_1M", "transitions_per_step",
                   "vector_steps_per_rollout", "roofline", "roofline_gae", "roofline_env",
                   "roofline_rnd"):
