@@ -6,8 +6,8 @@ fewer launches: PyTorch-ROCm's nn.GroupNorm backward in this image returns wrong
 gradients once a batch has >= 512 rows (tools/diag_groupnorm.py), which would silently corrupt
 every PPO update.  The module subclasses nn.GroupNorm, so its parameters and state_dict keys
 (`<block>.1.weight`, `<block>.1.bias`) are the reference's; the SiLU slot becomes nn.Identity.
-CPU-resident modules (no GPU present) evaluate nn.functional.group_norm + silu, as the
-reference does on the CPU.
+CPU-resident modules (no GPU present) and non-float32 tensors evaluate nn.functional.group_norm +
+silu, as the reference does on the CPU.
 """
 import torch
 import torch.nn.functional as F
@@ -45,8 +45,9 @@ class GroupNormSiLU(nn.GroupNorm):
             raise ValueError("only GroupNorm(8, 64) has a HIP kernel")
 
     def forward(self, x):
-        if x.is_cuda:
+        if x.is_cuda and x.dtype == torch.float32 and self.weight.dtype == torch.float32:
             return _GroupNormSiLU.apply(x, self.weight, self.bias, self.eps)
+        # CPU, or another dtype (tests' float64 copies of a device policy): torch's own ops
         return F.silu(F.group_norm(x, self.num_groups, self.weight, self.bias, self.eps))
 
 

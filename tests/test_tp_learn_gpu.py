@@ -36,9 +36,44 @@ pytestmark = pytest.mark.gpu
 # first steps are ~lr * sign(g), so those differences reach the weights as ~lr * (relative
 # gradient difference) per step plus the sign flips of near-zero gradient entries (GroupNorm's
 # scale-invariant directions), bounded by the steps' size.  CartPole: 2e-6 as at mb 512
-# (test_stack_gpu).  Pendulum: 17-dim-free but |logp| of the narrow Gaussian reaches ~10, whose
-# float32 rounding moves ratios by ~1e-6: 1e-5, <= 0.2 % of the steps' movement.
-WEIGHT_ATOL = {"learn_mb65536": 2e-6, "learn_cont_mb65536": 1e-5}
+# (test_stack_gpu).  Pendulum: |logp| of the narrow Gaussian reaches ~10, whose float32 rounding
+# moves ratios by ~1e-6, and the sign flips above then reach ~2e-5 (2.4e-5
+# measured on MI355X, 0.4 % of the steps' movement).  So for Pendulum the bar is relational: the
+# engine's weights must be no further from a float64 run of the same update loop (_learn_f64)
+# than the reference's own float32 run is, to a factor of F64_FACTOR, plus 2e-6; and within
+# 5e-5 (0.8 % of the movement) of the reference.
+WEIGHT_ATOL = {"learn_mb65536": 2e-6, "learn_cont_mb65536": 5e-5}
+F64_FACTOR = 3.0
+
+
+def _learn_f64(policy, S, A, adv, ret, mb, k_epochs):
+    """The reference's update loop (PPO.py:216-255) in float64 on the CPU from `policy`'s
+    weights: old log-probs from the same weights (ratio 1 on the first minibatch, as in the
+    reference), k_epochs x sequential unshuffled minibatches of the clipped surrogate + 0.5
+    SmoothL1 - 0.01 H (the loss _grad_f64 restates), clip_grad_norm_(2.0), torch AdamW (the
+    reference's defaults, lr 1e-3).  Returns the final state_dict."""
+    import copy
+    from torch import nn
+    pol = copy.deepcopy(policy).cpu().double()
+    S, A = S.cpu().double(), A.cpu().double()
+    adv, ret = adv.cpu().double(), ret.cpu().double()
+    with torch.no_grad():
+        old = pol.get_evaluate(S, A)[0]
+    opt = torch.optim.AdamW(pol.parameters(), lr=1e-3)
+    N = S.shape[0]
+    for _ in range(k_epochs):
+        for lo in range(0, N, mb):
+            sl = slice(lo, min(lo + mb, N))
+            logp, V, H = pol.get_evaluate(S[sl], A[sl])
+            ratio = torch.exp(torch.clamp(logp - old[sl], -20, 20))
+            s1 = ratio * adv[sl]
+            s2 = torch.clamp(ratio, 0.8, 1.2) * adv[sl]
+            loss = -torch.min(s1, s2) + 0.5 * nn.SmoothL1Loss()(V, ret[sl]) - 0.01 * H
+            opt.zero_grad()
+            loss.mean().backward()
+            nn.utils.clip_grad_norm_(pol.parameters(), 2.0)
+            opt.step()
+    return pol.state_dict()
 
 
 def _sub(g, prefix):
@@ -81,6 +116,16 @@ def test_large_minibatch_learn_matches_reference_learn(golden, tag):
     moved = max(float((ref[k].double() - init[k].double()).abs().max()) for k in ref)
     print(f"{tag}: max |w - w_ref| {worst:.3e} (the 6 steps moved weights by up to {moved:.3e})")
     assert worst <= WEIGHT_ATOL[tag], worst
+    if cont:
+        import copy
+        q = copy.deepcopy(p.policy)
+        q.load_state_dict(init)
+        w64 = _learn_f64(q, torch.from_numpy(S), torch.from_numpy(Aa), torch.from_numpy(g["adv"]),
+                         torch.from_numpy(g["returns"]), mb, int(g["k_epochs"]))
+        ours = max(float((sd[k].cpu().double() - w64[k]).abs().max()) for k in ref)
+        theirs = max(float((ref[k].double() - w64[k]).abs().max()) for k in ref)
+        print(f"{tag}: vs float64 update: engine {ours:.3e}, reference float32 {theirs:.3e}")
+        assert ours <= F64_FACTOR * theirs + 2e-6, (ours, theirs)
     old = p.policy_old.state_dict()
     for k, v in sd.items():
         assert torch.equal(old[k], v)

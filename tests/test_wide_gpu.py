@@ -354,10 +354,12 @@ def test_wide_dist_at_reads_the_step_in_place():
 def test_wide_graphed_rollout_equals_eager_rollout(monkeypatch):
     """C5's net on the synthetic env: the graphed rollout (distribution read from traj_obs[k] in
     place, parameters gathered once per rollout) gives the eager rollout's memory and scores
-    bit for bit, including after learn() changed policy_old between rollouts."""
+    bit for bit, including after learn() changed policy_old between rollouts.  (The per-step
+    path: PRL_WIDE_ROLLOUT=0; by default C5 rolls out in one persistent launch, tested below.)"""
     from AsyncTools.AsyncPPO import AsyncPPO
     from PPO import PPO
     outs = []
+    monkeypatch.setenv("PRL_WIDE_ROLLOUT", "0")
     for graphed in ("1", "0"):
         monkeypatch.setenv("PRL_ROLLOUT_GRAPH", graphed)
         torch.manual_seed(0)
@@ -386,9 +388,11 @@ def test_flat_adamw_matches_torch_clip_and_adamw(scale):
     launch over flat buffers, PPO.py:248-250) against torch's own clip_grad_norm_ + AdamW
     (capturable) on C5's parameter shapes over four steps.  scale 1e-3: norm < 2, no clipping;
     1e2: clipping every step.  The two differ only in float32 rounding (norm summed in float64
-    here, the AdamW division as rcp + one Newton step): parameters within 1e-9 absolute (each
-    step moves them ~1e-3), moments within 1e-5 relative, and the clipped gradient within 1e-6
-    relative."""
+    here, the AdamW division as rcp + one Newton step): moments within 1e-5 relative and the
+    clipped gradient within 1e-6 relative.  Parameters: the native tail rounds each step's update with fused multiply-adds
+    (p * decay, then fma(-step_size, m / denom, p)) where torch rounds mul_ and addcdiv_
+    separately: up to ~2 ulps of the parameter per step, so 4 steps stay within 16 ulps of the
+    largest parameter (2.4e-7 measured on MI355X at |p| <= 0.3)."""
     import prl_native
     pol = _policy(True, 348, 17)
     shapes = [p.shape for p in pol.parameters()]
@@ -413,7 +417,8 @@ def test_flat_adamw_matches_torch_clip_and_adamw(scale):
         want_g = torch.cat([p.grad.reshape(-1) for p in ref])
         assert float((gbuf - want_g).abs().max()) <= 1e-6 * float(want_g.abs().max())
     want = torch.cat([p.detach().reshape(-1) for p in ref])
-    assert float((flat - want).abs().max()) <= 1e-9, float((flat - want).abs().max())
+    ulp = float(torch.finfo(torch.float32).eps) * float(want.abs().max())
+    assert float((flat - want).abs().max()) <= 16 * ulp, float((flat - want).abs().max())
     wm = torch.cat([opt.state[p]["exp_avg"].reshape(-1) for p in ref])
     wv = torch.cat([opt.state[p]["exp_avg_sq"].reshape(-1) for p in ref])
     assert float((m - wm).abs().max()) <= 1e-5 * float(wm.abs().max())
