@@ -239,7 +239,9 @@ int prl_ppo_update_info(int32_t D, int32_t A, int32_t discrete, int64_t mini_bat
  * per minibatch j (rows [j*mb, min((j+1)*mb, N)) of S/actions/old_logp/adv/ret, unshuffled):
  * ActorCritic.get_evaluate (ActorCritic.py:118-146), loss = mean(-min(surr1, surr2)) +
  * vf_coef * SmoothL1(V, ret) - ent_coef * H (PPO.py:225-245), its gradient,
- * clip_grad_norm_(max_norm) and AdamW(lr, (beta1, beta2), eps, weight_decay).  params /
+ * clip_grad_norm_(max_norm) and AdamW(lr, (beta1, beta2), eps, weight_decay) — the betas as
+ * doubles everywhere in this ABI (the reference forms 1 - beta and the bias corrections in
+ * Python double precision; from a float32 0.999 they would be 1.3e-5 off).  params /
  * exp_avg / exp_avg_sq: the flat parameter vector and moments in torch parameters() order
  * (updated in place); adam_step: device f32 step count (read, then advanced by the step count);
  * loss_out: device f32, the last step's loss.  Workspace: prl_ppo_update_info's size (its status
@@ -248,7 +250,7 @@ int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, float* adam
                    int32_t A, int32_t discrete, const float* S, const float* actions,
                    const float* old_logp, const float* adv, const float* ret, int64_t N,
                    int32_t mini_batch, int32_t k_epochs, float clip, float vf_coef,
-                   float ent_coef, float lr, float beta1, float beta2, float eps,
+                   float ent_coef, float lr, double beta1, double beta2, float eps,
                    float weight_decay, float max_norm, float* loss_out, void* workspace,
                    int64_t workspace_bytes, void* stream);
 /* ActorCritic.get_evaluate (ActorCritic.py:118-146) over N rows, as PPO.learn evaluates
@@ -279,8 +281,8 @@ int prl_ppo_grad_step(const float* img_params, int32_t D, int32_t A, int32_t dis
 /* clip_grad_norm_(max_norm) + AdamW step number `step` (1-based) on the images from the
  * all-reduced gradient; loss_out (device f32, may be NULL) = that step's loss. */
 int prl_ppo_adam_step(float* img_params, float* img_m, float* img_v, int32_t D, int32_t A,
-                      int32_t discrete, const float* grad, int64_t step, float lr, float beta1,
-                      float beta2, float eps, float weight_decay, float max_norm, float inv_count,
+                      int32_t discrete, const float* grad, int64_t step, float lr, double beta1,
+                      double beta2, float eps, float weight_decay, float max_norm, float inv_count,
                       float vf_coef, float ent_coef, float* loss_out, void* stream);
 /* One launch per optimizer step (what the data-parallel loops use): the PREVIOUS step's
  * clip_grad_norm_(max_norm) + AdamW (step number step_prev, its all-reduced gradient grad_prev,
@@ -296,7 +298,7 @@ int prl_ppo_grad_fold_step(const float* in_p, const float* in_m, const float* in
                            const float* S, const float* actions, const float* old_logp,
                            const float* adv, const float* ret, int64_t N, int32_t mini_batch,
                            int64_t minibatch_index, float inv_count, float clip, float vf_coef,
-                           float ent_coef, float lr, float beta1, float beta2, float eps,
+                           float ent_coef, float lr, double beta1, double beta2, float eps,
                            float weight_decay, float max_norm, float* loss_out, float* grad_out,
                            void* workspace, int64_t workspace_bytes, void* stream);
 /* ---- wide-net optimizer step (shapes outside the persistent engine: D <= 352, <= 48 outputs) -- */
@@ -359,7 +361,7 @@ int prl_colsum_f32(const float* x, int64_t rows, int32_t cols, float* out, float
  * leaves p.grad).  The norm is summed in float64 in a fixed order (deterministic).  One launch,
  * graph-capturable; the wide step's optimizer tail (PPO/update.py).  16-B aligned buffers. */
 int prl_flat_adamw(float* params, float* exp_avg, float* exp_avg_sq, float* step, float* grad,
-                   int64_t P, float lr, float beta1, float beta2, float eps, float weight_decay,
+                   int64_t P, float lr, double beta1, double beta2, float eps, float weight_decay,
                    float max_norm, void* stream);
 /* Host call: device address of the u32 status words inside an engine workspace ([0] last
  * launch, [1] sticky timeout flag). */
@@ -388,7 +390,7 @@ int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, int32_t D, 
                       const float* old_logp, const float* adv, const float* ret, int64_t N,
                       int32_t mini_batch, int32_t k_epochs, int64_t nb, const int64_t* counts,
                       int64_t step0, float clip, float vf_coef, float ent_coef, float lr,
-                      float beta1, float beta2, float eps, float weight_decay, float max_norm,
+                      double beta1, double beta2, float eps, float weight_decay, float max_norm,
                       float* grad, float* loss_out, void* workspace, int64_t workspace_bytes,
                       void* comm, void* stream);
 
@@ -414,7 +416,7 @@ int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_sq, float* 
                        const float* actions, const float* old_logp, const float* adv,
                        const float* ret, int64_t N, int32_t mini_batch, int32_t k_epochs,
                        int32_t nb_union, const float* inv_count, float clip, float vf_coef,
-                       float ent_coef, float lr, float beta1, float beta2, float eps,
+                       float ent_coef, float lr, double beta1, double beta2, float eps,
                        float weight_decay, float max_norm, float* loss_out, int32_t world,
                        int32_t rank, void* const* xbufs, int64_t seq0, int32_t fine_grained,
                        void* workspace, int64_t workspace_bytes, void* stream);

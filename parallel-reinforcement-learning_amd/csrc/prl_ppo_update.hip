@@ -133,7 +133,9 @@ struct UpdArgs {
   int64_t N;
   int mb, nb, total_steps, G, R;
   int Gt;           // tile groups (= G, or G / replicas in the latency form's replicated tiles)
-  float clip, vf_coef, ent_coef, lr, beta1, beta2, eps, wd, max_norm;
+  float clip, vf_coef, ent_coef, lr;
+  double beta1, beta2;   // AdamW betas as the caller's doubles: 1 - beta2 from a float32 beta2 is 1.3e-5 off
+  float eps, wd, max_norm;
   float* params;
   float* exp_avg;
   float* exp_avg_sq;
@@ -1284,7 +1286,7 @@ __device__ inline void upd_sum_partials(__amdgpu_buffer_rsrc_t rs_part, int Qtot
 struct AdamConst {
   float step_size, inv_bc2_sqrt, decay, omb1, omb2, beta2, eps;
 };
-__device__ __forceinline__ AdamConst adam_const(double tstep, float lr, float beta1, float beta2,
+__device__ __forceinline__ AdamConst adam_const(double tstep, float lr, double beta1, double beta2,
                                                 float eps, float wd) {
   const double bc1 = 1.0 - pow((double)beta1, tstep);
   const double bc2 = 1.0 - pow((double)beta2, tstep);
@@ -1294,7 +1296,7 @@ __device__ __forceinline__ AdamConst adam_const(double tstep, float lr, float be
   c.decay = (float)(1.0 - (double)lr * (double)wd);
   c.omb1 = (float)(1.0 - (double)beta1);
   c.omb2 = (float)(1.0 - (double)beta2);
-  c.beta2 = beta2;
+  c.beta2 = (float)beta2;
   c.eps = eps;
   return c;
 }
@@ -1757,7 +1759,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       const float step_size = s_adam[0];
       const float inv_bc2_sqrt = s_adam[1];   // scalar divide -> one multiply
       const float decay = (float)(1.0 - (double)args.lr * (double)args.wd);
-      const float b2 = args.beta2;
+      const float b2 = (float)args.beta2;
       const float omb1 = (float)(1.0 - (double)args.beta1), omb2 = (float)(1.0 - (double)args.beta2);
       constexpr int BATCH = NQ;
 #pragma unroll
@@ -1938,7 +1940,9 @@ struct UpdFold {
   const float *p_in, *m_in, *v_in;    // state before that step's AdamW
   float *p_out, *m_out, *v_out;       // state after it
   double tstep;                       // that step's AdamW step number (1-based)
-  float lr, beta1, beta2, eps, wd, max_norm, inv_count, vf_coef, ent_coef;
+  float lr;
+  double beta1, beta2;
+  float eps, wd, max_norm, inv_count, vf_coef, ent_coef;
   float* loss_out;                    // that step's loss (workgroup 0), may be null
 };
 
@@ -2084,8 +2088,8 @@ __global__ __launch_bounds__((64 * upd_nw<KD, KA>()), 1) void ppo_grad_kernel(Up
 constexpr int ADAM_PF = 24;   // gradient quads per thread held in registers (Qp <= 6144)
 __global__ __launch_bounds__(UPD_THREADS) void ppo_adam_kernel(int Lp, float* img_p, float* img_m,
                                                              float* img_v, const float* grad,
-                                                             double tstep, float lr, float beta1,
-                                                             float beta2, float eps, float wd,
+                                                             double tstep, float lr, double beta1,
+                                                             double beta2, float eps, float wd,
                                                              float max_norm, float inv_count,
                                                              float vf_coef, float ent_coef,
                                                              float* loss_out) {
@@ -2248,11 +2252,12 @@ const void* upd_eval_kernel_for(const UpdNet& n) {
 
 int upd_grid(int64_t mb) { return (int)std::min<int64_t>(256, cdiv(mb, UPD_RT)); }
 // Replicas per tile group of the latency form (ppo_update_body: workgroups g, g + Gt, ... run the
-// same rows and split the publish): PRL_UPD_REPL (default 1), capped so that all Gt x X
+// same rows and split the publish): PRL_UPD_REPL (default 2: mb 512 13.84 vs 14.03 us per step,
+// same-box A/B; 4 and 8 slower, their waits grow), capped so that all Gt x X
 // workgroups fit one per CU.
 int g_repl = [] {
   const char* e = getenv("PRL_UPD_REPL");
-  const int v = e ? atoi(e) : 1;
+  const int v = e ? atoi(e) : 2;
   return v >= 1 ? v : 1;
 }();
 int upd_repl(int Gt) {
@@ -2358,7 +2363,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
             int32_t A, int32_t discrete, const float* S, const float* actions,
             const float* old_logp, const float* adv, const float* ret, int64_t N,
             int32_t mini_batch, int32_t k_epochs, float clip, float vf_coef, float ent_coef,
-            float lr, float beta1, float beta2, float eps, float weight_decay, float max_norm,
+            float lr, double beta1, double beta2, float eps, float weight_decay, float max_norm,
             float* loss_out, void* workspace, int64_t workspace_bytes, void* stream,
             const UpdDp* dp) {
   UpdArgs args{};
@@ -2477,8 +2482,8 @@ extern "C" int prl_ppo_update(float* params, float* exp_avg, float* exp_avg_sq, 
                               int32_t D, int32_t A, int32_t discrete, const float* S,
                               const float* actions, const float* old_logp, const float* adv,
                               const float* ret, int64_t N, int32_t mini_batch, int32_t k_epochs,
-                              float clip, float vf_coef, float ent_coef, float lr, float beta1,
-                              float beta2, float eps, float weight_decay, float max_norm,
+                              float clip, float vf_coef, float ent_coef, float lr, double beta1,
+                              double beta2, float eps, float weight_decay, float max_norm,
                               float* loss_out, void* workspace, int64_t workspace_bytes,
                               void* stream) {
   return upd_run(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp,
@@ -2492,7 +2497,7 @@ extern "C" int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_
                                   const float* adv, const float* ret, int64_t N,
                                   int32_t mini_batch, int32_t k_epochs, int32_t nb_union,
                                   const float* inv_count, float clip, float vf_coef,
-                                  float ent_coef, float lr, float beta1, float beta2, float eps,
+                                  float ent_coef, float lr, double beta1, double beta2, float eps,
                                   float weight_decay, float max_norm, float* loss_out,
                                   int32_t world, int32_t rank, void* const* xbufs, int64_t seq0,
                                   int32_t fine_grained, void* workspace, int64_t workspace_bytes,
@@ -2679,7 +2684,7 @@ extern "C" int prl_ppo_grad_step(const float* img_params, int32_t D, int32_t A, 
 
 extern "C" int prl_ppo_adam_step(float* img_params, float* img_m, float* img_v, int32_t D,
                                  int32_t A, int32_t discrete, const float* grad, int64_t step,
-                                 float lr, float beta1, float beta2, float eps, float weight_decay,
+                                 float lr, double beta1, double beta2, float eps, float weight_decay,
                                  float max_norm, float inv_count, float vf_coef, float ent_coef,
                                  float* loss_out, void* stream) {
   UpdNet n;
@@ -2705,7 +2710,7 @@ extern "C" int prl_ppo_grad_fold_step(const float* in_p, const float* in_m, cons
                                       const float* adv, const float* ret, int64_t N,
                                       int32_t mini_batch, int64_t minibatch_index, float inv_count,
                                       float clip, float vf_coef, float ent_coef, float lr,
-                                      float beta1, float beta2, float eps, float weight_decay,
+                                      double beta1, double beta2, float eps, float weight_decay,
                                       float max_norm, float* loss_out, float* grad_out,
                                       void* workspace, int64_t workspace_bytes, void* stream) {
   UpdArgs args{};
@@ -2847,7 +2852,7 @@ extern "C" int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, 
                                  const float* old_logp, const float* adv, const float* ret, int64_t N,
                                  int32_t mini_batch, int32_t k_epochs, int64_t nb,
                                  const int64_t* counts, int64_t step0, float clip, float vf_coef,
-                                 float ent_coef, float lr, float beta1, float beta2, float eps,
+                                 float ent_coef, float lr, double beta1, double beta2, float eps,
                                  float weight_decay, float max_norm, float* grad, float* loss_out,
                                  void* workspace, int64_t workspace_bytes, void* comm, void* stream) {
   UpdArgs args{};

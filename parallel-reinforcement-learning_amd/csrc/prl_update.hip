@@ -257,7 +257,7 @@ constexpr int FA_THREADS = 1024;
 
 __global__ __launch_bounds__(FA_THREADS) void flat_adamw_kernel(
     float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, float* __restrict__ step,
-    float* __restrict__ grad, int64_t P, float lr, float beta1, float beta2, float eps, float wd,
+    float* __restrict__ grad, int64_t P, float lr, double beta1, double beta2, float eps, float wd,
     float max_norm) {
   __shared__ double s_part[FA_THREADS / 64];
   __shared__ float s_c[3];
@@ -289,12 +289,13 @@ __global__ __launch_bounds__(FA_THREADS) void flat_adamw_kernel(
   __syncthreads();
   const float clipc = s_c[0], step_size = s_c[1], inv_bc2_sqrt = s_c[2];
   const float decay = (float)(1.0 - (double)lr * (double)wd);
-  const float omb1 = (float)(1.0 - (double)beta1), omb2 = (float)(1.0 - (double)beta2);
+  // 1 - beta from the caller's double betas (torch forms them in Python double precision)
+  const float omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2), b2 = (float)beta2;
   auto upd = [&](float g, float& pw, float& mw, float& vw) {
     const float gr = g * clipc;
     pw = pw * decay;
     mw = fmaf(omb1, gr - mw, mw);
-    vw = fmaf(omb2 * gr, gr, vw * beta2);
+    vw = fmaf(omb2 * gr, gr, vw * b2);
     const float denom = fmaf(__builtin_amdgcn_sqrtf(vw), inv_bc2_sqrt, eps);
     float rq = __builtin_amdgcn_rcpf(denom);
     rq = fmaf(rq, fmaf(-denom, rq, 1.0f), rq);   // one Newton step: ~0.5 ulp
@@ -325,7 +326,7 @@ __global__ __launch_bounds__(FA_THREADS) void flat_adamw_kernel(
 }
 
 extern "C" int prl_flat_adamw(float* params, float* exp_avg, float* exp_avg_sq, float* step,
-                              float* grad, int64_t P, float lr, float beta1, float beta2, float eps,
+                              float* grad, int64_t P, float lr, double beta1, double beta2, float eps,
                               float weight_decay, float max_norm, void* stream) {
   PRL_REQUIRE(P > 0 && P < (int64_t)1 << 30, "prl_flat_adamw: bad size %lld", (long long)P);
   PRL_REQUIRE(params && exp_avg && exp_avg_sq && step && grad, "prl_flat_adamw: null pointer");

@@ -22,6 +22,11 @@ _P = ctypes.c_void_p
 _I64, _I32, _U64, _F32, _F64, _INT = (ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64,
                                       ctypes.c_float, ctypes.c_double, ctypes.c_int)
 # symbol -> argtypes (restype int unless listed in _RESTYPES)
+# the update engines' scalars: clip, vf_coef, ent_coef, lr, beta1, beta2, eps, weight_decay,
+# max_norm — the AdamW betas as doubles (1 - beta2 formed from a float32 0.999 is 1.3e-5 off the
+# reference's Python-double 1 - 0.999)
+_UPD_SCALARS = [_F32] * 4 + [_F64] * 2 + [_F32] * 3
+
 SIGNATURES = {
     "prl_abi_version": [],
     "prl_last_error": [],
@@ -65,7 +70,7 @@ SIGNATURES = {
     "prl_categorical_bwd": [_P, _P, _P, _I64, _I32, _P, _P],
     "prl_ppo_update_info": [_I32, _I32, _I32, _I64, _P, _P, _P],
     "prl_ppo_update": [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I32]
-                      + [_F32] * 9 + [_P, _P, _I64, _P],
+                      + _UPD_SCALARS + [_P, _P, _I64, _P],
     "prl_ppo_update_status_ptr": [_P, _P],
     "prl_ppo_update_profile_ptr": [_P, _P],
     "prl_dp_rccl_open": [ctypes.c_char_p],
@@ -73,9 +78,9 @@ SIGNATURES = {
     "prl_dp_comm_init": [_P, _I64, _I32, _I32, _P],
     "prl_dp_comm_destroy": [_P],
     "prl_ppo_update_dp": [_P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I32,
-                          _I64, _P, _I64] + [_F32] * 9 + [_P, _P, _P, _I64, _P, _P],
+                          _I64, _P, _I64] + _UPD_SCALARS + [_P, _P, _P, _I64, _P, _P],
     "prl_ppo_update_dpx": [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32,
-                           _I32, _I32, _P] + [_F32] * 9 + [_P, _I32, _I32, _P, _I64, _I32, _P,
+                           _I32, _I32, _P] + _UPD_SCALARS + [_P, _I32, _I32, _P, _I64, _I32, _P,
                                                            _I64, _P],
     "prl_dp_xbuf_bytes": [_I32, _I32, _I32, _I32],
     "prl_dp_set_spin_limit": [ctypes.c_uint32],
@@ -93,12 +98,14 @@ SIGNATURES = {
     "prl_ppo_image": [_I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _I32, _P],
     "prl_ppo_grad_step": [_P, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64, _I32, _I64, _F32, _F32,
                           _F32, _P, _P, _I64, _P],
-    "prl_ppo_adam_step": [_P, _P, _P, _I32, _I32, _I32, _P, _I64] + [_F32] * 9 + [_P, _P],
+    # lr, beta1, beta2, eps, weight_decay, max_norm, inv_count, vf_coef, ent_coef
+    "prl_ppo_adam_step": [_P, _P, _P, _I32, _I32, _I32, _P, _I64, _F32, _F64, _F64] + [_F32] * 6
+                         + [_P, _P],
     "prl_colsum_partial_floats": [_I64, _I32],
     "prl_colsum_f32": [_P, _I64, _I32, _P, _P, _I64, _P],
-    "prl_flat_adamw": [_P, _P, _P, _P, _P, _I64] + [_F32] * 6 + [_P],
+    "prl_flat_adamw": [_P, _P, _P, _P, _P, _I64, _F32, _F64, _F64, _F32, _F32, _F32, _P],
     "prl_ppo_grad_fold_step": [_P] * 7 + [_I64, _F32, _I32, _I32, _I32] + [_P] * 5
-                              + [_I64, _I32, _I64] + [_F32] * 10 + [_P, _P, _P, _I64, _P],
+                              + [_I64, _I32, _I64, _F32] + _UPD_SCALARS + [_P, _P, _P, _I64, _P],
 }
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_source_id": ctypes.c_char_p,
              "prl_ppo_update_last_plan": None, "prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,

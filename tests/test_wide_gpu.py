@@ -386,7 +386,8 @@ def test_wide_graphed_rollout_equals_eager_rollout(monkeypatch):
 def test_flat_adamw_matches_torch_clip_and_adamw(scale):
     """prl_flat_adamw (the wide step's optimizer tail: clip_grad_norm_(2.0) + AdamW.step() in one
     launch over flat buffers, PPO.py:248-250) against torch's own clip_grad_norm_ + AdamW
-    (capturable) on C5's parameter shapes over four steps.  scale 1e-3: norm < 2, no clipping;
+    (the reference's defaults: bias corrections from Python doubles) on C5's parameter shapes
+    over four steps.  scale 1e-3: norm < 2, no clipping;
     1e2: clipping every step.  The two differ only in float32 rounding (norm summed in float64
     here, the AdamW division as rcp + one Newton step): moments within 1e-5 relative and the
     clipped gradient within 1e-6 relative.  Parameters: the native tail rounds each step's update with fused multiply-adds
@@ -397,7 +398,7 @@ def test_flat_adamw_matches_torch_clip_and_adamw(scale):
     pol = _policy(True, 348, 17)
     shapes = [p.shape for p in pol.parameters()]
     ref = [torch.nn.Parameter(p.detach().clone()) for p in pol.parameters()]
-    opt = torch.optim.AdamW(ref, lr=1e-3, capturable=True)
+    opt = torch.optim.AdamW(ref, lr=1e-3)   # the reference's AdamW (PPO.py:51-54): defaults
     P = sum(p.numel() for p in ref)
     flat = torch.cat([p.detach().reshape(-1) for p in ref]).contiguous()
     m, v = torch.zeros_like(flat), torch.zeros_like(flat)
