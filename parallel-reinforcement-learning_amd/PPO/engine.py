@@ -440,9 +440,12 @@ class FusedUpdate:
         P = ctypes.c_void_p
         lib = prl_native.lib()
         stream = P(torch.cuda.current_stream().cuda_stream)
+        # clip, vf_coef, ent_coef, lr, beta1, beta2, eps, weight_decay, max_norm (the betas as
+        # doubles: prl_native._UPD_SCALARS)
         hyper = tuple(ctypes.c_float(x) for x in (
-            self.ppo.policy_clip, self.ppo.value_coef, self.ppo.entropy_coef, group["lr"], beta1,
-            beta2, group["eps"], group["weight_decay"], 2.0))
+            self.ppo.policy_clip, self.ppo.value_coef, self.ppo.entropy_coef, group["lr"]))
+        hyper += (ctypes.c_double(beta1), ctypes.c_double(beta2))
+        hyper += tuple(ctypes.c_float(x) for x in (group["eps"], group["weight_decay"], 2.0))
         step = int(round(float(self.step.item())))
         n_local = int(S.shape[0])
         if comm is not None and k_epochs > 0:

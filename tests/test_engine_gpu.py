@@ -507,9 +507,10 @@ def _unfolded_stepped(eng, S, A, old, adv, ret, k_epochs, n_ranks):
             step += 1
             assert lib.prl_ppo_adam_step(*(P(x.data_ptr()) for x in img), eng.D, eng.A,
                                          int(eng.discrete), P(grad.data_ptr()), step,
+                                         ctypes.c_float(group["lr"]), ctypes.c_double(beta1),
+                                         ctypes.c_double(beta2),
                                          *(ctypes.c_float(x) for x in (
-                                             group["lr"], beta1, beta2, group["eps"],
-                                             group["weight_decay"], 2.0)), inv,
+                                             group["eps"], group["weight_decay"], 2.0)), inv,
                                          ctypes.c_float(ppo.value_coef),
                                          ctypes.c_float(ppo.entropy_coef),
                                          P(eng.loss.data_ptr()), stream) == 0
