@@ -1,9 +1,6 @@
 #!/bin/bash
-# GPU box: which test function of tests/test_kernels_gpu.py, run before it, makes the C5 graphed
-# rollout's reward score NaN in test_wide_graphed_rollout_equals_eager_rollout (passes alone).
+# GPU box: the full tests/test_kernels_gpu.py, then the C5 graphed-rollout NaN diagnostic
+# (tools/diag_graph_nan_test.py) in the same process.
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-T=tests/test_wide_gpu.py::test_wide_graphed_rollout_equals_eager_rollout
-for f in $(grep -o "^def test_[a-z0-9_]*" tests/test_kernels_gpu.py | cut -c5-); do
-  timeout -k 10 200 python -u -m pytest -q --timeout 100 --timeout-method thread "tests/test_kernels_gpu.py::$f" $T > gpurun_out/bis_$f.log 2>&1
-  echo "$f rc=$? $(tail -1 gpurun_out/bis_$f.log)"
-done
+timeout -k 10 400 python -u -m pytest -q -s --timeout 200 --timeout-method thread tests/test_kernels_gpu.py tools/diag_graph_nan_test.py > gpurun_out/bis_diag.log 2>&1
+echo "rc=$?"; grep -E "^k=|^capture|^replay|^it0|passed|failed" gpurun_out/bis_diag.log | head -70

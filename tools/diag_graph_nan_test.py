@@ -1,0 +1,66 @@
+"""pytest-run diagnostic (run after tests/test_kernels_gpu.py, where the full suite saw it): the
+C5 graphed rollout's first (eager + warm-up capture) rollout, reward sum and live rows' dist
+checked after every vector step, around the capture and after the replay."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "parallel-reinforcement-learning_amd"))
+
+
+def test_diag_graph_nan(monkeypatch):
+    from AsyncTools.AsyncPPO import AsyncPPO
+    from PPO import PPO
+    monkeypatch.setenv("PRL_WIDE_ROLLOUT", "0")
+    monkeypatch.setenv("PRL_ROLLOUT_GRAPH", "1")
+    E = 200
+    torch.manual_seed(0)
+    p = PPO(True, 348, 17, action_scaling=1.0, batch_size=10**9, mini_batch_size=512)
+    a = AsyncPPO("SyntheticHumanoid-v0", p, num_envs=E, seed=5)
+    log = []
+    orig_step = a._step_kernel
+
+    def step(k, dist, seed, scaling, active_after):
+        if not isinstance(k, torch.Tensor):
+            torch.cuda.synchronize()
+            tr = a._traj
+            live = a.env.terminal == 0
+            bad = (~torch.isfinite(dist).all(-1)) & live
+            before = float(tr.reward_sum.item())
+        orig_step(k, dist, seed, scaling, active_after)
+        if not isinstance(k, torch.Tensor):
+            torch.cuda.synchronize()
+            after = float(tr.reward_sum.item())
+            if int(bad.sum()) or after != after:
+                e = int(torch.nonzero(bad)[0]) if int(bad.sum()) else -1
+                log.append(f"k={k}: live rows with non-finite dist {int(bad.sum())} (first e={e}), "
+                           f"reward_sum {before} -> {after}, obs row finite "
+                           f"{bool(torch.isfinite(a._traj.obs[k, e]).all()) if e >= 0 else None}")
+    a._step_kernel = step
+    orig_cap = a._capture_step
+
+    def cap(seed, scaling):
+        tr = a._traj
+        torch.cuda.synchronize()
+        b = float(tr.reward_sum.item())
+        g = orig_cap(seed, scaling)
+        torch.cuda.synchronize()
+        log.append(f"capture: reward_sum {b} -> {float(tr.reward_sum.item())}")
+        if g is not None:
+            orig_replay = g.replay
+
+            def replay():
+                r0 = float(tr.reward_sum.item())
+                orig_replay()
+                torch.cuda.synchronize()
+                r1 = float(tr.reward_sum.item())
+                if r1 != r1 or len(log) < 40:
+                    log.append(f"replay: reward_sum {r0} -> {r1}, k_dev {a._k_dev.tolist()}")
+            g.replay = replay
+        return g
+    a._capture_step = cap
+    n = a.worker()
+    print("\n".join(log[:60]))
+    print(f"it0: N={n} reward_score={float(a.reward_score)}")
