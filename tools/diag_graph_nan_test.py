@@ -39,6 +39,25 @@ def test_diag_graph_nan(monkeypatch):
                            f"reward_sum {before} -> {after}, obs row finite "
                            f"{bool(torch.isfinite(a._traj.obs[k, e]).all()) if e >= 0 else None}")
     a._step_kernel = step
+    orig_dist = p.dist_params
+    seen = {"n": 0}
+
+    def dist_params(obs):
+        tr = a._traj
+        torch.cuda.synchronize()
+        b = float(tr.reward_sum.item())
+        flat_ptr = getattr(p, "_dist_flat_buf", None)
+        out = orig_dist(obs)
+        torch.cuda.synchronize()
+        c = float(tr.reward_sum.item())
+        if (b == b) != (c == c) and seen["n"] < 3:
+            seen["n"] += 1
+            rs = tr.reward_sum
+            log.append(f"dist_params flipped reward_sum {b} -> {c}: reward_sum ptr {rs.data_ptr():#x}, "
+                       f"out ptr {out.data_ptr():#x} bytes {out.numel() * 4}, obs ptr {obs.data_ptr():#x}, "
+                       f"flat ptr {p._dist_flat_buf.data_ptr():#x} bytes {p._dist_flat_buf.numel() * 4}")
+        return out
+    p.dist_params = dist_params
     orig_cap = a._capture_step
 
     def cap(seed, scaling):
