@@ -58,6 +58,23 @@ def test_diag_graph_nan(monkeypatch):
                        f"flat ptr {p._dist_flat_buf.data_ptr():#x} bytes {p._dist_flat_buf.numel() * 4}")
         return out
     p.dist_params = dist_params
+    import AsyncTools.AsyncPPO as AP
+    RealEvent = torch.cuda.Event
+    flips = {"n": 0}
+
+    class Ev(RealEvent):   # recorded right after the loop's pinned copy of active_after[k]
+        def record(self, stream=None):
+            tr = a._traj
+            torch.cuda.synchronize()
+            v = float(tr.reward_sum.item())
+            if v != v and flips["n"] < 2:
+                flips["n"] += 1
+                log.append(f"NaN right after the pinned copy: reward_sum ptr {tr.reward_sum.data_ptr():#x}, "
+                           f"active_after ptr {tr.active_after.data_ptr():#x}, pinned ptr "
+                           f"{tr.pinned.data_ptr():#x} is_pinned {tr.pinned.is_pinned()}, "
+                           f"ep_len ptr {tr.ep_len.data_ptr():#x}, offsets ptr {tr.offsets.data_ptr():#x}")
+            return super().record(stream) if stream is not None else super().record()
+    monkeypatch.setattr(AP.torch.cuda, "Event", Ev)
     orig_cap = a._capture_step
 
     def cap(seed, scaling):
