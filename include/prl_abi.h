@@ -440,6 +440,10 @@ int32_t prl_ppo_update_set_tp(int32_t mode);
  * Per process (initial value from PRL_UPD_REPL); returns the previous value.  No reference
  * counterpart (performance knob / tests). */
 int32_t prl_ppo_update_set_repl(int32_t replicas);
+/* Test utility: fill every CU's LDS with `value` (LDS is not cleared between launches; a kernel
+ * that reads LDS it did not write in its own launch sees the previous launch's contents).  No
+ * reference counterpart. */
+int prl_debug_fill_lds(float value, void* stream);
 /* What the last prl_ppo_update / prl_ppo_update_dpx call in this process launched:
  * out[0] = 1 for the throughput form, 0 for the latency form; out[1] = waves per workgroup;
  * out[2] = workgroups; out[3] = 16-row tiles per workgroup and step (ceil of rows / 16 / G);

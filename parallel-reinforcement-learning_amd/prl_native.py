@@ -86,6 +86,7 @@ SIGNATURES = {
     "prl_dp_set_spin_limit": [ctypes.c_uint32],
     "prl_ppo_update_set_tp": [_I32],
     "prl_ppo_update_set_repl": [_I32],
+    "prl_debug_fill_lds": [_F32, _P],
     "prl_ppo_update_last_plan": [_P],
     "prl_source_id": [],
     "prl_dp_xbuf_alloc": [_I64, _P, _P],
@@ -685,6 +686,12 @@ def ppo_update_set_tp(mode: int) -> int:
     """Form of the fused update engine: 0 latency form, 1 throughput form (launches of >= 2
     steps), 2 auto (default); returns the previous mode.  Both forms give the same bits."""
     return int(lib().prl_ppo_update_set_tp(int(mode)))
+
+
+def debug_fill_lds(value: float) -> None:
+    """Fill every CU's LDS with `value` on the current stream (tests: kernels must not read LDS
+    they did not write in their own launch)."""
+    _check(lib().prl_debug_fill_lds(float(value), _stream()), "prl_debug_fill_lds")
 
 
 def ppo_update_set_repl(replicas: int) -> int:

@@ -521,3 +521,27 @@ def test_persistent_wide_rollout_matches_per_step_rollout(monkeypatch):
                           for i in idx], dtype=torch.float64)
         want = torch.tanh(mu + sd * z)
         assert float((A1[idx].double() - want).abs().max()) <= 2e-5
+
+
+@pytest.mark.parametrize("N", [200, 1000])
+def test_wide_dist_reads_no_stale_lds(N):
+    """prl_ppo_wide_dist after every CU's LDS was filled with NaN and after it was filled with 0
+    (prl_debug_fill_lds): the same bits, and no NaN — the kernel reads no LDS it did not write in
+    its own launch.  (The full GPU suite once saw one row's [mu | std] come out NaN in a C5
+    rollout after earlier tests; the row's observations were finite.)"""
+    import prl_native
+    pol = _policy(True, 348, 17, seed=5)
+    torch.manual_seed(3)
+    S = torch.randn(N, 348, device="cuda")
+    flat = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
+    outs = []
+    for fill in (float("nan"), 0.0, float("inf")):
+        prl_native.debug_fill_lds(fill)
+        out = torch.empty(N, 34, device="cuda")
+        prl_native.ppo_wide_dist(flat, 348, 17, False, S, out)
+        torch.cuda.synchronize()
+        outs.append(out.cpu())
+    assert bool(torch.isfinite(outs[1]).all())
+    for o in (outs[0], outs[2]):
+        bad = ~(o == outs[1]).all(1)
+        assert not bool(bad.any()), f"rows differing after a poisoned LDS: {torch.nonzero(bad)[:8].tolist()}"
