@@ -33,6 +33,18 @@ def test_diag_graph_nan(monkeypatch):
         if not isinstance(k, torch.Tensor):
             torch.cuda.synchronize()
             after = float(tr.reward_sum.item())
+            if int(bad.sum()) and not os.path.exists(os.path.join(ROOT, "gpurun_out", "nan_case.pt")):
+                os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+                obs = a._traj.obs[k].clone()
+                flat = p._dist_flat_buf.clone()
+                again = torch.empty_like(dist)
+                import prl_native
+                prl_native.ppo_wide_dist(flat, 348, 17, False, obs, again)
+                torch.cuda.synchronize()
+                torch.save({"obs": obs.cpu(), "flat": flat.cpu(), "dist": dist.cpu(), "again": again.cpu(),
+                            "live": live.cpu(), "k": k}, os.path.join(ROOT, "gpurun_out", "nan_case.pt"))
+                log.append(f"saved nan_case.pt: recomputed dist finite rows "
+                           f"{int(torch.isfinite(again).all(-1).sum())}/{again.shape[0]}")
             if int(bad.sum()) or after != after or k < 5:
                 e = int(torch.nonzero(bad)[0]) if int(bad.sum()) else -1
                 log.append(f"k={k}: live rows with non-finite dist {int(bad.sum())} (first e={e}), "
