@@ -682,7 +682,17 @@ __device__ __forceinline__ void ppo_wide_grad_body(const WdNet& n, const WdArgs&
             wv.z = d0 + 2 < D ? w0row[d0 + 2] : 0.f;
             wv.w = d0 + 3 < D ? w0row[d0 + 3] : 0.f;
           }
-          const float4 xv = *reinterpret_cast<const float4*>(Xs + x * XS + d0);
+          float4 xv = *reinterpret_cast<const float4*>(Xs + x * XS + d0);
+          if (16 * sg + 16 > D) {
+            // the last, partial column group (D % 16 != 0): with the unpadded row stride
+            // (XS == D) columns >= D are the NEXT row's first columns.  Their weights are 0, but
+            // 0 x NaN is NaN: a non-finite value there (a terminal env's unwritten observation
+            // row in the rollout's distribution pass) leaked into this row's outputs.  Zero them.
+            xv.x = d0 < D ? xv.x : 0.f;
+            xv.y = d0 + 1 < D ? xv.y : 0.f;
+            xv.z = d0 + 2 < D ? xv.z : 0.f;
+            xv.w = d0 + 3 < D ? xv.w : 0.f;
+          }
           acc[0] = wd_mma(wv.x, xv.x, acc[0]);
           acc[1] = wd_mma(wv.y, xv.y, acc[1]);
           acc[2] = wd_mma(wv.z, xv.z, acc[2]);

@@ -545,3 +545,34 @@ def test_wide_dist_reads_no_stale_lds(N):
     for o in (outs[0], outs[2]):
         bad = ~(o == outs[1]).all(1)
         assert not bool(bad.any()), f"rows differing after a poisoned LDS: {torch.nonzero(bad)[:8].tolist()}"
+
+
+def test_wide_dist_rows_independent_of_nonfinite_neighbours():
+    """A non-finite observation row (a terminal env's never-written row of traj_obs[k], which the
+    rollout's distribution pass covers too) leaves every other row's [mu | std] bit for bit
+    unchanged.  D = 348 = 16 x 21 + 12: the trunk's last column group reads 4 columns past the
+    row end (the next row's first columns under the unpadded row stride); they are zeroed, since
+    their zero weights would still turn a NaN there into a NaN output (found in the full GPU suite:
+    row 101 of a C5 rollout went NaN through row 102's column 0)."""
+    import prl_native
+    pol = _policy(True, 348, 17, seed=5)
+    torch.manual_seed(4)
+    N = 200
+    S = torch.randn(N, 348, device="cuda")
+    flat = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
+
+    def dist(x):
+        out = torch.empty(N, 34, device="cuda")
+        prl_native.ppo_wide_dist(flat, 348, 17, False, x, out)
+        torch.cuda.synchronize()
+        return out.cpu()
+
+    clean = dist(S)
+    P = S.clone()
+    P[102, :4] = float("nan")
+    P[18] = float("nan")
+    P[111, 0] = float("inf")
+    out = dist(P)
+    keep = torch.ones(N, dtype=torch.bool)
+    keep[[18, 102, 111]] = False
+    assert torch.equal(out[keep], clean[keep])
