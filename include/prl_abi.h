@@ -440,19 +440,12 @@ int32_t prl_ppo_update_set_tp(int32_t mode);
  * Per process (initial value from PRL_UPD_REPL); returns the previous value.  No reference
  * counterpart (performance knob / tests). */
 int32_t prl_ppo_update_set_repl(int32_t replicas);
-/* The throughput form's kernel on the specialised shapes (CartPole, Pendulum): 1 = the
- * wave-per-tile form (each of a workgroup's four waves runs whole 16-row tiles, the four waves'
- * gradients summed in LDS once per step; last_plan out[0] = 2), 0 = the 8-wave head-split
- * kernels.  Per process (initial value from PRL_UPD_WT); returns the previous mode.  No reference
- * counterpart (performance knob / tests). */
-int32_t prl_ppo_update_set_wt(int32_t mode);
 /* Test utility: fill every CU's LDS with `value` (LDS is not cleared between launches; a kernel
  * that reads LDS it did not write in its own launch sees the previous launch's contents).  No
  * reference counterpart. */
 int prl_debug_fill_lds(float value, void* stream);
 /* What the last prl_ppo_update / prl_ppo_update_dpx call in this process launched:
- * out[0] = 1 for the throughput form, 2 for its wave-per-tile kernel, 0 for the latency form;
- * out[1] = waves per workgroup;
+ * out[0] = 1 for the throughput form, 0 for the latency form; out[1] = waves per workgroup;
  * out[2] = workgroups; out[3] = 16-row tiles per workgroup and step (ceil of rows / 16 / G);
  * out[4] = 1 for a compile-time-layout (CartPole / Pendulum) kernel, 0 for the runtime layout;
  * out[5] = workgroups per tile group (the latency form's replicated tiles, PRL_UPD_REPL; out[2]

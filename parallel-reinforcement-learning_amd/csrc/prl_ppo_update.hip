@@ -1491,8 +1491,6 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
   return true;
 }
 
-#include "prl_wt_tile.h"
-
 // NQ = parameter quads per thread (ceil(Lp / 4 / 256)): AdamW's moments live in registers.
 // DP: the data-parallel form (prl_ppo_update_dpx): union-minibatch row weights and the
 // cross-rank slice sum; a separate instantiation, so the single-GPU kernel carries none of it.
@@ -1505,8 +1503,6 @@ template <int NQ, int KD, int KA, bool DP, int TPM = 0>
 __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& args) {
   constexpr int NW = upd_nw<KD, KA>(), NT = 64 * NW;
   constexpr bool TP = TPM > 0;
-  constexpr bool WT = TPM == 2;   // the wave-per-tile throughput form (prl_wt_tile.h)
-  static_assert(!WT || (NW == 4 && KD >= 0 && KD <= 1 && !DP), "WT: the 4-wave specialised kernels");
   extern __shared__ __align__(16) float upd_lds[];
   const int t = threadIdx.x, g = blockIdx.x, G = args.G;
   // Replicated tiles (latency form, single GPU, PRL_UPD_REPL): workgroups g, g + Gt, g + 2 Gt, ...
@@ -1524,9 +1520,9 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
   // sits below 64 KB so every scratch address folds into the ds instructions' 16-bit offset field
   // (no base registers kept live across the step loop)
   float* scratch = upd_lds + UPD_HDR;                                   // tile activations
-  const int scr_floats = WT ? upd_wt_scratch_floats(n) : (upd_scratch_floats(n.D, NW, upd_ts(n)) + 3) & ~3;
+  const int scr_floats = (upd_scratch_floats(n.D, NW, upd_ts(n)) + 3) & ~3;
   float* W = scratch + scr_floats;                                       // [Lp]
-  float* Ga = WT ? scratch : W + Lp;   // [Lp + 4] (WT: the step's image aliases the wave scratch)
+  float* Ga = W + Lp;                                                    // [Lp + 4]
   const UpdScr sc = upd_scr(scratch, n.D, NW);
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
   float* s_adam = hdr + 10;         // [2] this step's AdamW step size, 1 / sqrt(bc2)
@@ -1598,15 +1594,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
   // Every prefetch is unconditional (clamped arguments instead of branches around it): a load
   // under a branch made the compiler join nin's paths with copies that waited for the loads on
   // the spot.
-  if constexpr (!WT) load_first(0);
-  // WT: each wave's own next tile (tile w of the step's rows first)
-  UpdIn<upd_ksm<KA>()> win[1];
-  auto wt_load_first = [&](int s) {
-    const int wv = t >> 6;
-    upd_wt_load(n, args, first_row(s) + (int64_t)wv * UPD_RT,
-                std::max(0, std::min(UPD_RT, first_rows(s) - wv * UPD_RT)), win[0]);
-  };
-  if constexpr (WT) wt_load_first(0);
+  load_first(0);
   for (int s = 0; s < args.total_steps; ++s) {
     const int j = s % args.nb;
     const int64_t mb0 = (int64_t)j * args.mb;
@@ -1617,38 +1605,11 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     const int64_t myrow0 = mb0 + (int64_t)gt * R;
     // ---- phase A: partial gradient of this workgroup's rows ------------------------------------
     UpdGradOf<KD, KA> gr;
-    if constexpr (TP && !WT) gr.zero();
+    if constexpr (TP) gr.zero();
     if (!TP && myrows == 0) {   // no rows this step: publish zeros
       for (int k = t; k < Lp + 4; k += NT) Ga[k] = 0.0f;
     }
-    if constexpr (WT) {
-      constexpr int NHW = upd_kd_discrete(KD) ? 2 : 3;
-      const int wv = t >> 6;
-      UpdWtGrad<NHW> wg;
-      wg.zero();
-      float* wsc = scratch + wv * upd_wt_wave_floats(NHW);
-      const int ntile = (myrows + UPD_RT - 1) / UPD_RT;
-      for (int c = wv; c < ntile; c += 4) {
-        const UpdIn<upd_ksm<KA>()> cur = win[0];
-        // prefetch the wave's next tile: this step's c + 4, else the next step's tile wv
-        if (c + 4 < ntile)
-          upd_wt_load(n, args, myrow0 + (int64_t)(c + 4) * UPD_RT, std::min(UPD_RT, myrows - (c + 4) * UPD_RT), win[0]);
-        else
-          wt_load_first(s + 1);
-        upd_wt_tile<KD, KA>(n, args, W, wsc, cur, std::min(UPD_RT, myrows - c * UPD_RT), invB, wg);
-      }
-      if (wv >= ntile) wt_load_first(s + 1);   // no tile this step
-      __syncthreads();   // every wave's tiles done: the scratch becomes the step's image
-      for (int q4 = t; q4 < (Lp + 4) / 4; q4 += NT)
-        *reinterpret_cast<float4*>(Ga + 4 * q4) = float4{0.f, 0.f, 0.f, 0.f};
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {   // wave order: deterministic
-        if (wv == r) upd_wt_grad_add<KD>(n, wg, Ga);
-        __syncthreads();
-      }
-    }
-    for (int c0 = 0; !WT && c0 < myrows; c0 += UPD_RT) {
+    for (int c0 = 0; c0 < myrows; c0 += UPD_RT) {
       const UpdIn<upd_ksm<KA>()> cur = upd_in_real(nin[0]);
       // prefetch the next tile to run: this step's next one, else the next step's first (runs
       // under this tile and the step's hand-offs)
@@ -1670,9 +1631,9 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
                                 tm, gr);
     }
     if constexpr (!TP) __syncthreads();
-    mark(0);   // phase A compute (WT: tiles + the four waves' image)
+    mark(0);   // phase A compute
     const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_red = upd_rsrc(args.red);
-    if constexpr (TP && !WT) {
+    if constexpr (TP) {
       upd_grad_publish<KD, KA>(n, gr, upd_rsrc(args.part + (size_t)g * Qtot * 4));
     } else {
       // replica g / Gt of tile group gt publishes quads [qa, qb) of the group's partial
@@ -1687,7 +1648,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
     // the latency form prefetched the next step's first tile at its tile's start (no tile ran:
     // here); the throughput form here, under the waits (at the last tile's start its loads
     // were still in flight at the publish drain: +0.7-0.9 us per step at mb 65,536)
-    if (!WT && (TP || myrows == 0)) load_first(s + 1);
+    if (TP || myrows == 0) load_first(s + 1);
     if (t < 64) {
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_A, g);
       const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));
@@ -2256,37 +2217,23 @@ const void* upd_kernel_for(const UpdNet& n, bool dp = false) {
 struct UpdPlan {
   const void* kern;
   int nw, tiles;
-  bool wt;   // the wave-per-tile form (TPM = 2)
 };
-// PRL_UPD_WT / prl_ppo_update_set_wt: 1 = the wave-per-tile form wherever the throughput form
-// runs on a specialised shape, 0 = the 8-wave head-split throughput kernels
-int g_wt_mode = [] {
-  const char* e = getenv("PRL_UPD_WT");
-  return (e && e[0] == '1') ? 1 : 0;
-}();
 UpdPlan upd_tp_plan(const UpdNet& n) {
   const int qp = n.Lp / 4;
-  if (!upd_force_generic() && g_wt_mode == 1) {
-    if (upd_is_cartpole(n) && cdiv(qp, 256) <= 10)
-      return {reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4, false, 2>), 4, 1, true};
-    if (!n.discrete && n.A == 1 && n.D == 3 && cdiv(qp, 256) <= 14)
-      return {reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3, false, 2>), 4, 1, true};
-  }
   if (!upd_force_generic()) {
     if (upd_is_cartpole(n) && upd_waves8_enabled() && cdiv(qp, 512) <= 5)
-      return {reinterpret_cast<const void*>(ppo_update_kernel<5, 2, 2, 4, false, 1>), 8, 1, false};
+      return {reinterpret_cast<const void*>(ppo_update_kernel<5, 2, 2, 4, false, 1>), 8, 1};
     if (upd_is_cartpole(n) && cdiv(qp, 256) <= 10)
-      return {reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4, false, 1>), 4, 1, false};
+      return {reinterpret_cast<const void*>(ppo_update_kernel<10, 1, 2, 4, false, 1>), 4, 1};
     const bool pend = !n.discrete && n.A == 1 && n.D == 3;
     if (pend && upd_waves8_enabled() && cdiv(qp, 512) <= 7)
-      return {reinterpret_cast<const void*>(ppo_update_kernel<7, 3, 1, 3, false, 1>), 8, 1, false};
+      return {reinterpret_cast<const void*>(ppo_update_kernel<7, 3, 1, 3, false, 1>), 8, 1};
     if (pend && cdiv(qp, 256) <= 14)
-      return {reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3, false, 1>), 4, 1, false};
+      return {reinterpret_cast<const void*>(ppo_update_kernel<14, 0, 1, 3, false, 1>), 4, 1};
   }
-  return {nullptr, 4, 1, false};   // (the runtime-layout kernel spills more in this form: latency form)
+  return {nullptr, 4, 1};   // (the runtime-layout kernel spills more in this form: latency form)
 }
-size_t upd_lds_bytes_plan(const UpdNet& n, int nw, bool tp, int tiles, bool wt = false) {
-  if (wt) return sizeof(float) * (size_t)(UPD_HDR + upd_wt_scratch_floats(n) + n.Lp);
+size_t upd_lds_bytes_plan(const UpdNet& n, int nw, bool tp, int tiles) {
   return sizeof(float) * (size_t)(UPD_HDR + (tp ? n.Lp : 2 * n.Lp + 4) +
                                   tiles * ((upd_scratch_floats(n.D, nw, upd_ts(n)) + 3) & ~3));
 }
@@ -2494,7 +2441,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   args.tp_m1 = ws.mv + 2 * L4;
   args.tp_v1 = ws.mv + 3 * L4;
   bool tp = upd_tp_host(args.R, args.total_steps, dp != nullptr);
-  UpdPlan plan{upd_kernel_for(args.net, dp != nullptr), upd_nw_host(args.net, true), 1, false};
+  UpdPlan plan{upd_kernel_for(args.net, dp != nullptr), upd_nw_host(args.net, true), 1};
   if (tp) {
     const UpdPlan p2 = upd_tp_plan(args.net);
     if (p2.kern) plan = p2;
@@ -2503,12 +2450,12 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   // replicated tiles: the latency form on one GPU only
   const int G = (tp || dp) ? Gt : Gt * upd_repl(Gt);
   args.G = G;
-  const size_t lds = upd_lds_bytes_plan(args.net, plan.nw, tp, plan.tiles, plan.wt);
+  const size_t lds = upd_lds_bytes_plan(args.net, plan.nw, tp, plan.tiles);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_update: %zu B of LDS needed", lds);
   hipStream_t st = as_stream(stream);
   const void* kern = plan.kern;
   PRL_REQUIRE(kern, "prl_ppo_update: %d parameter quads per thread not built", upd_nq(args.net));
-  g_last_plan[0] = plan.wt ? 2 : (tp ? 1 : 0);
+  g_last_plan[0] = tp ? 1 : 0;
   g_last_plan[1] = plan.nw;
   g_last_plan[2] = G;
   g_last_plan[3] = args.R / UPD_RT;
@@ -2565,12 +2512,6 @@ extern "C" int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_
 extern "C" int32_t prl_ppo_update_set_tp(int32_t mode) {
   const int prev = g_tp_mode;
   g_tp_mode = (mode >= 0 && mode <= 2) ? mode : 2;
-  return prev;
-}
-
-extern "C" int32_t prl_ppo_update_set_wt(int32_t mode) {
-  const int prev = g_wt_mode;
-  g_wt_mode = mode == 1 ? 1 : 0;
   return prev;
 }
 

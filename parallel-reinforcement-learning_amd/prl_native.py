@@ -86,7 +86,6 @@ SIGNATURES = {
     "prl_dp_set_spin_limit": [ctypes.c_uint32],
     "prl_ppo_update_set_tp": [_I32],
     "prl_ppo_update_set_repl": [_I32],
-    "prl_ppo_update_set_wt": [_I32],
     "prl_debug_fill_lds": [_F32, _P],
     "prl_ppo_update_last_plan": [_P],
     "prl_source_id": [],
@@ -112,7 +111,7 @@ SIGNATURES = {
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_source_id": ctypes.c_char_p,
              "prl_ppo_update_last_plan": None, "prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,
              "prl_dp_set_spin_limit": ctypes.c_uint32, "prl_ppo_update_set_tp": _I32,
-             "prl_ppo_update_set_repl": _I32, "prl_ppo_update_set_wt": _I32,
+             "prl_ppo_update_set_repl": _I32,
              "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
 
 _lib = None
@@ -695,12 +694,6 @@ def debug_fill_lds(value: float) -> None:
     _check(lib().prl_debug_fill_lds(float(value), _stream()), "prl_debug_fill_lds")
 
 
-def ppo_update_set_wt(mode: int) -> int:
-    """The throughput form's kernel on CartPole / Pendulum: 1 the wave-per-tile form, 0 the 8-wave
-    head-split kernels; returns the previous mode."""
-    return int(lib().prl_ppo_update_set_wt(int(mode)))
-
-
 def ppo_update_set_repl(replicas: int) -> int:
     """Workgroups per 16-row tile group of the engine's latency form (each publishes its share of
     the tile's partial gradient); returns the previous value.  Every value gives the same bits."""
@@ -729,7 +722,7 @@ def ppo_update_last_plan() -> dict:
     out = (ctypes.c_int32 * 6)()
     lib().prl_ppo_update_last_plan(out)
     tp, nw, G, tiles, spec, repl = list(out)
-    return {"form": {2: "wave-tile", 1: "throughput", 0: "latency"}.get(tp), "waves": nw, "grid": G,
+    return {"form": {1: "throughput", 0: "latency"}.get(tp), "waves": nw, "grid": G,
             "tiles": tiles, "specialised": bool(spec == 1), "replicas": repl}
 
 

@@ -80,24 +80,8 @@ def _sub(g, prefix):
     return {k[len(prefix):]: torch.from_numpy(np.array(g[k])) for k in g.files if k.startswith(prefix)}
 
 
-@pytest.fixture(params=[0, 1], ids=["tp8", "wavetile"])
-def tp_kernel(request):
-    """The throughput form's kernel: 0 the 8-wave head-split kernels, 1 the wave-per-tile form
-    (prl_ppo_update_set_wt)."""
-    import prl_native
-    prev = prl_native.ppo_update_set_wt(request.param)
-    yield request.param
-    prl_native.ppo_update_set_wt(prev)
-
-
-def _tp_plan_ok(plan, wt, grid=256, tiles=None):
-    want = {"form": "wave-tile", "waves": 4} if wt else {"form": "throughput", "waves": 8}
-    ok = all(plan[k] == v for k, v in want.items()) and plan["specialised"] and plan["grid"] == grid
-    return ok and plan["replicas"] == 1 and (tiles is None or plan["tiles"] == tiles)
-
-
 @pytest.mark.parametrize("tag", ["learn_mb65536", "learn_cont_mb65536"])
-def test_large_minibatch_learn_matches_reference_learn(golden, tag, tp_kernel):
+def test_large_minibatch_learn_matches_reference_learn(golden, tag):
     import prl_native
     from PPO import PPO
     g = golden(tag)
@@ -119,7 +103,8 @@ def test_large_minibatch_learn_matches_reference_learn(golden, tag, tp_kernel):
     torch.cuda.synchronize()
     assert p.last_update_path == "fused"
     plan = prl_native.ppo_update_last_plan()
-    assert _tp_plan_ok(plan, tp_kernel, tiles=16), plan
+    assert plan == {"form": "throughput", "waves": 8, "grid": 256, "tiles": 16,
+                    "specialised": True, "replicas": 1}, plan
     _, _, _, adv, returns = p._last_update_inputs
     ret_ref, adv_ref = g["returns"].astype(np.float64), g["adv"].astype(np.float64)
     # GAE is bit-exact against the reference (test_kernels_gpu); here it runs on our old values
@@ -154,7 +139,7 @@ def _eng_logp(eng, policy, S, A):
 @pytest.mark.parametrize("cont", [False, True])
 @pytest.mark.parametrize("mb", [8192, 65536])
 @pytest.mark.parametrize("spread", [0.3, 3.0])
-def test_throughput_form_gradient_matches_autograd(cont, mb, spread, tp_kernel):
+def test_throughput_form_gradient_matches_autograd(cont, mb, spread):
     """Two optimizer steps at lr = 0 — minibatch 0 full (mb rows: 2 or 16 tiles per workgroup),
     minibatch 1 ragged — in one throughput-form launch; old_logp = logp + noise(spread) puts
     ratios on both sides of the clip range (spread 3 also beyond the +-20 clamp's neighbourhood
@@ -163,8 +148,7 @@ def test_throughput_form_gradient_matches_autograd(cont, mb, spread, tp_kernel):
     autograd of the reference loss on that minibatch at the engine's own float32 log-prob values
     (continuous log-probs' float32 rounding is amplified by the mu gradients' cancelling sums,
     DESIGN.md §4; the forward itself is checked against float64 separately).  Tolerance 1e-4 of
-    each tensor's largest entry, as the latency form's test_fused_gradient_off_policy.  Both
-    throughput kernels: the 8-wave head-split and the wave-per-tile form."""
+    each tensor's largest entry, as the latency form's test_fused_gradient_off_policy."""
     import prl_native
     D = 3 if cont else 4
     ragged = mb // 4 + 3
@@ -187,7 +171,8 @@ def test_throughput_form_gradient_matches_autograd(cont, mb, spread, tp_kernel):
     eng.run(S_, A_, old2, adv, ret, 1)
     torch.cuda.synchronize()
     plan = prl_native.ppo_update_last_plan()
-    assert _tp_plan_ok(plan, tp_kernel, tiles=mb // 256 // 16), plan
+    assert plan["form"] == "throughput" and plan["waves"] == 8 and plan["specialised"], plan
+    assert plan["tiles"] == mb // 256 // 16, plan
     assert float(eng.step.item()) == 2.0
     parts = []
     for lo, hi in ((0, mb), (mb, N)):
