@@ -143,7 +143,7 @@ struct UpdArgs {
   float* loss_out;
   float* part;      // [G][Qtot * 4]
   float* red;       // [Qtot * 4]
-  float* sq;        // [G][32]: slice g's float64 squared-norm piece on its own 128-B line
+  float* sq;        // [NW G] per-wave squared-norm pieces of the slices
   unsigned* ctr;    // [0] arrivals A, [1] arrivals B, [2] abort, [3] status (zeroed per launch),
                     // [4] sticky timeout flag (never zeroed by a launch)
   unsigned long long* prof;  // [8] workgroup 0's time per phase (100 MHz ticks, summed over steps)
@@ -1352,7 +1352,7 @@ struct UpdSub {
 // output biases cancel across workgroups), publishes the slice (sc1) and returns this thread's
 // share of the slice's sum of squares (parameter quads only).  Uses scratch as [spl][nq] double4.
 // (Gp < G: the latency form's replicated tiles, one partial per tile group; see ppo_update_body.)
-__device__ inline double upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_red,
+__device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_red,
                                          int Qtot, int Qp, int g, int G, float* scratch, int NT,
                                          int aux = UPD_AUX_SC1, UpdSub sub = UpdSub{nullptr, nullptr},
                                          int Gp = -1) {
@@ -1360,13 +1360,12 @@ __device__ inline double upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdg
   const int t = threadIdx.x;
   const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
   const int nq = qhi - qlo;
-  double ssq = 0.0;   // the slice's sum of squares of the rounded (float) gradient, in float64
+  float ssq = 0.f;
   auto fin = [&](int qi, double ax, double ay, double az, double aw) {
     const float4 r = float4{(float)ax, (float)ay, (float)az, (float)aw};
     if (aux == UPD_AUX_SYS) st4_aux<UPD_AUX_SYS>(rs_red, (size_t)(qlo + qi) * 4, r);
     else st4_aux<UPD_AUX_SC1>(rs_red, (size_t)(qlo + qi) * 4, r);
-    if (qlo + qi < Qp)
-      ssq += ((double)r.x * r.x + (double)r.y * r.y) + ((double)r.z * r.z + (double)r.w * r.w);
+    if (qlo + qi < Qp) ssq += r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w;
   };
   if (nq > NT / 2) {
     // wide slices (few workgroups): each thread owns whole quads, partials summed in order
@@ -1424,8 +1423,7 @@ __device__ inline double upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdg
 // acquire.
 
 __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t rs_red, int Qtot,
-                                   int g, int G, unsigned long long gstep, int par, int* s_abort,
-                                   double& ssq) {
+                                   int g, int G, unsigned long long gstep, int par, int* s_abort) {
   const int t = threadIdx.x, NT = blockDim.x;
   const unsigned long long want = gstep + 1ull;
   if (t == 0) {
@@ -1474,7 +1472,6 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
   if (*s_abort) return false;
   const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
   const size_t base = (size_t)par * Qtot * 4;
-  ssq = 0.0;   // this thread's share of the union slice's squared norm (parameter quads)
   for (int q = qlo + t; q < qhi; q += NT) {
     float4 acc = ld4_aux<UPD_AUX_SYS>(upd_rsrc(args.xbuf[0] + base), (size_t)q * 4);
 #pragma unroll
@@ -1488,8 +1485,6 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
       }
     }
     st4_sc1(rs_red, (size_t)q * 4, acc);
-    if (q < Qtot - 1)
-      ssq += ((double)acc.x * acc.x + (double)acc.y * acc.y) + ((double)acc.z * acc.z + (double)acc.w * acc.w);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1676,35 +1671,12 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
       constexpr bool dp = DP;
       const unsigned long long gstep = args.dp_seq0 + (unsigned long long)s;
       const int par = (int)(gstep & 1ull);
-      double ssq = upd_slice_reduce(rs_part, dp ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
-                                    Qtot, Qp, g, G, scratch, NT, dp ? UPD_AUX_SYS : UPD_AUX_SC1, subm, Gt);
+      (void)upd_slice_reduce(rs_part, dp ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
+                             Qtot, Qp, g, G, scratch, NT, dp ? UPD_AUX_SYS : UPD_AUX_SC1, subm, Gt);
       subm.mark(1);   // slice combined, its stores issued
-      // the slice's float64 sum of squares (clip_grad_norm_'s piece) travels with the slice —
-      // stored sc1 by thread 0 on this workgroup's own 128-B line of `sq` and drained before
-      // thread 0's arrival at counter B, like the slice itself (Guideline 16, R1).  Data-parallel
-      // ranks: the piece of the union slice (every rank forms the same one)
-      double* s_sqw = reinterpret_cast<double*>(hdr + 112);   // [NW <= 8]
-      if constexpr (!dp) {
-        const double wsum = wave_sum_f64_to63(ssq);
-        if ((t & 63) == 63) s_sqw[t >> 6] = wsum;
-      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if constexpr (dp) {
-        if (!upd_dp_union_slice(args, rs_red, Qtot, g, G, gstep, par, s_abort, ssq)) return;
-        const double wsum = wave_sum_f64_to63(ssq);
-        if ((t & 63) == 63) s_sqw[t >> 6] = wsum;
-        __syncthreads();
-      }
-      if (t == 0) {
-        double tot = 0.0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) tot += s_sqw[w];
-        const unsigned long long bits = __builtin_bit_cast(unsigned long long, tot);
-        st4_sc1(upd_rsrc(args.sq), (size_t)g * 32,
-                float4{__uint_as_float((unsigned)bits), __uint_as_float((unsigned)(bits >> 32)), 0.f, 0.f});
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (dp && !upd_dp_union_slice(args, rs_red, Qtot, g, G, gstep, par, s_abort)) return;
       mark(3);   // slice reduce
       if (t < 64) {
         if (t == 0) upd_arrive(args.ctr, UPD_CTR_B, g);
@@ -1745,31 +1717,37 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
         }
       }
     }
+    // 8 waves (two per SIMD, 256 registers each): park the quads in the gradient image, free
+    // since the publish, so they do not stay live across the norm into AdamW
+    constexpr bool PARK = NW == 8 && !TP;
+    float* const park = Ga;
     float clipc;
     {
-      // clip_grad_norm_'s norm from the G slice owners' float64 pieces: every wave sums them in
-      // one fixed order (lane k: pieces k, k + 64, ...; then a fixed DPP tree), so every wave of
-      // every workgroup forms the same coefficient — and AdamW below waits only for its own
-      // gradient quads, not for the whole gradient's norm.  (Round 1 summed float32 pieces
-      // published as 4-B words, eight workgroups' to a 128-B line, which were read stale on some
-      // runs; each piece is now a 16-B sc1 store on its workgroup's own line, drained before the
-      // arrival that signals it — the protocol the slices themselves use.  Rounds 2-3 re-squared
-      // the whole reduced gradient in every workgroup instead.)
-      const __amdgpu_buffer_rsrc_t rs_sq = upd_rsrc(args.sq);
-      double part = 0.0;
-      for (int k = t & 63; k < G; k += 64) {
-        const float4 v = ld4_sc1(rs_sq, (size_t)k * 32);
-        part += __builtin_bit_cast(double, ((unsigned long long)__float_as_uint(v.y) << 32) |
-                                               (unsigned long long)__float_as_uint(v.x));
+      // clip_grad_norm_'s norm from the reduced gradient this workgroup just loaded: per thread
+      // its quads in order, a fixed DPP tree per wave, the NW wave sums in wave order (LDS) — the
+      // same data, order and code in every workgroup, so every copy forms the same coefficient.
+      // (Round 1 summed per-slice pieces published by the slice owners instead: those 4-B words,
+      // eight workgroups' to a 128-B line, were read stale on some runs — a wrong clip
+      // coefficient, run-to-run differences; tools/exp/engine_determinism4.py.)
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        if (i * NT < Qp && t + i * NT < Qp) {
+          acc += (gq[i].x * gq[i].x + gq[i].y * gq[i].y) + (gq[i].z * gq[i].z + gq[i].w * gq[i].w);
+          if (PARK) *reinterpret_cast<float4*>(park + 4 * (t + i * NT)) = gq[i];
+        }
       }
-      const double tot_d = wave_sum_f64_to63(part);
-      const unsigned long long tb = __builtin_bit_cast(unsigned long long, tot_d);
-      const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)tb, 63);
-      const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(tb >> 32), 63);
-      const float tot = (float)__builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-      subm.mark(2);   // the norm pieces landed
+      subm.mark(2);   // thread 0's gradient quads landed
+      acc = wave_sum_f32_to63(acc);
+      float* s_nrm = hdr + 96;  // [NW <= 16] (hdr + 8 / + 10 hold s_abort / s_adam)
+      if ((t & 63) == 63) s_nrm[t >> 6] = acc;
+      __syncthreads();
+      float tot = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) tot += s_nrm[w];
       const float coef = args.max_norm / (sqrtf(tot) + 1e-6f);
       clipc = coef < 1.0f ? coef : 1.0f;
+      // profile: steps whose clip_grad_norm_ scaled the gradient (prof[28])
       if (args.profile && g == 0 && t == 0 && coef < 1.0f) tm[20] += 1ull;
       if (g == 0 && t == 0 && s + 1 == args.total_steps) {
         const float4 lp = ld4_sc1(rs_red, (size_t)Qp * 4);
@@ -1800,7 +1778,7 @@ __device__ __forceinline__ void ppo_update_body(const UpdNet& n, const UpdArgs& 
               m4 = mreg[i];
               v4 = vreg[i];
             }
-            const float4 g4 = gq[i];
+            const float4 g4 = PARK ? *reinterpret_cast<const float4*>(park + 4 * q) : gq[i];
             // torch AdamW (decoupled decay; lerp for m; addcmul for v) with fused multiply-adds.
             // 8 waves: two elements per packed-f32 instruction (v_pk_mul / v_pk_fma: the same
             // operations per element, so the same bits as the scalar form; sqrt / rcp scalar):
@@ -2325,14 +2303,14 @@ struct UpdWs {
 };
 
 // workspace: ctr[UPD_CTR_WORDS] (words 0-3 and the shards zeroed per launch, word 4 sticky) |
-// prof[32] | sq[256][32] (slice norm pieces, one 128-B line each) | red[Qtot*4] | part[G][Qtot*4] | img[3][Qtot*4] | mv[4][Qtot*4] | slack
+// prof[32] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4] | img[3][Qtot*4] | mv[4][Qtot*4] | slack
 // (phase C's sweeps read up to one thread block of quads past an image: the slack keeps the
 // last one inside the allocation)
 size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
   const size_t Qtot = (size_t)n.Lp / 4 + 1;
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-  const size_t o_ctr = take(4 * UPD_CTR_WORDS), o_prof = take(256), o_sq = take(256 * 128), o_red = take(Qtot * 16),
+  const size_t o_ctr = take(4 * UPD_CTR_WORDS), o_prof = take(256), o_sq = take(2048 * 4), o_red = take(Qtot * 16),
                o_part = take((size_t)G * Qtot * 16), o_img = take((size_t)3 * Qtot * 16),
                o_mv = take((size_t)4 * Qtot * 16);
   (void)take(512 * 16);
