@@ -356,13 +356,15 @@ int64_t prl_colsum_partial_floats(int64_t rows, int32_t cols);
 int prl_colsum_f32(const float* x, int64_t rows, int32_t cols, float* out, float* partial,
                    int64_t partial_floats, void* stream);
 /* nn.utils.clip_grad_norm_(params, max_norm) followed by AdamW.step() (PPO/PPO.py:248-250; torch
- * defaults, capturable: step[0] f32 on the device is incremented first) over FLAT f32 vectors of
- * P entries in parameters() order: params, exp_avg, exp_avg_sq and grad (left clipped, as torch
- * leaves p.grad).  The norm is summed in float64 in a fixed order (deterministic).  One launch,
- * graph-capturable; the wide step's optimizer tail (PPO/update.py).  16-B aligned buffers. */
+ * defaults, capturable: the update uses step[0] + 1, and step[0] f32 on the device is advanced)
+ * over FLAT f32 vectors of P entries in parameters() order: params, exp_avg, exp_avg_sq and grad
+ * (left clipped, as torch leaves p.grad).  The norm is summed in float64 in a fixed order
+ * (deterministic) and stored to total_norm[0] (f32, what clip_grad_norm_ returns).  Two launches
+ * (update; clip of grad + step count), graph-capturable; the wide step's optimizer tail
+ * (PPO/update.py).  16-B aligned buffers. */
 int prl_flat_adamw(float* params, float* exp_avg, float* exp_avg_sq, float* step, float* grad,
                    int64_t P, float lr, double beta1, double beta2, float eps, float weight_decay,
-                   float max_norm, void* stream);
+                   float max_norm, float* total_norm, void* stream);
 /* Host call: device address of the u32 status words inside an engine workspace ([0] last
  * launch, [1] sticky timeout flag). */
 int prl_ppo_update_status_ptr(void* workspace, uint32_t** status);

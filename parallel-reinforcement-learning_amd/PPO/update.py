@@ -39,7 +39,7 @@ def wide_info(ppo, D: int):
 
 class FlatAdamState:
     """The policy's parameters, gradients and AdamW state as flat f32 vectors in parameters()
-    order, for prl_flat_adamw (clip_grad_norm_(2.0) + AdamW.step() in one launch, PPO.py:248-250):
+    order, for prl_flat_adamw (clip_grad_norm_(2.0) + AdamW.step() in two launches, PPO.py:248-250):
     every Parameter's .data, every .grad (PPO._ensure_flat_grads) and the optimizer's exp_avg /
     exp_avg_sq state tensors are VIEWS of these buffers, so torch's own optimizer, state_dict()
     and save_weights see the same copy (as engine.FusedUpdate does for the persistent engine).
@@ -55,6 +55,7 @@ class FlatAdamState:
         self.m = torch.zeros(n, dtype=torch.float32, device=dev)
         self.v = torch.zeros(n, dtype=torch.float32, device=dev)
         self.step = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.total_norm = torch.zeros(1, dtype=torch.float32, device=dev)   # clip_grad_norm_'s value
         self._bind()
 
     def _views(self, buf):
@@ -106,7 +107,7 @@ class FlatAdamState:
         group = self.ppo.optimizer.param_groups[0]
         beta1, beta2 = group["betas"]
         prl_native.flat_adamw(self.flat, self.m, self.v, self.step, grad, group["lr"], beta1,
-                              beta2, group["eps"], group["weight_decay"], max_norm)
+                              beta2, group["eps"], group["weight_decay"], max_norm, self.total_norm)
 
     def sync(self):
         """The optimizer's state = this one's: moments as views, step counts = ours."""

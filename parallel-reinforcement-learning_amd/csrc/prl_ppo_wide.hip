@@ -1162,30 +1162,28 @@ __device__ __forceinline__ void ppo_wide_dw0_body(const WdNet& n, const WdArgs& 
     }
   }
 }
-template <int KSM, bool KSPEC = false>
-__global__ __launch_bounds__(WD_THREADS, 2) void ppo_wide_dw0_kernel(WdArgs a, float* part2, int G2) {
-  if constexpr (KSPEC) {
-    constexpr WdNet N = wd_make(WD_C5_D, WD_C5_A, 0);
-    ppo_wide_dw0_body<KSM>(N, a, part2, G2);
-  } else {
-    ppo_wide_dw0_body<KSM>(a.net, a, part2, G2);
-  }
-}
 
 // grad[k] = sum_g part[g][k] in workgroup order (f64), k < P; loss = (L0 + vf L1 - ent L2) / B.
 // Block = 64 quads x 4 workgroup slots; slot s sums workgroups s, s + 4, ... and the 4 slot
 // sums are added in slot order.
 constexpr int WR_QUADS = 64;
-__global__ __launch_bounds__(256) void ppo_wide_reduce_kernel(const float* __restrict__ part, int G,
-                                                              int P, int Pq, float* __restrict__ grad,
-                                                              float* __restrict__ loss_out,
-                                                              const int64_t* cursor,
-                                                              const float* scales, int64_t N,
-                                                              int64_t mb, float vf_coef,
-                                                              float ent_coef) {
+struct WrArgs {
+  const float* part;
+  int G, P, Pq;
+  float* grad;
+  float* loss_out;
+  const int64_t* cursor;
+  const float* scales;
+  int64_t N, mb;
+  float vf_coef, ent_coef;
+};
+__device__ __forceinline__ void ppo_wide_reduce_body(const WrArgs& r, int blk) {
+  const float* __restrict__ part = r.part;
+  const int G = r.G, P = r.P, Pq = r.Pq;
+  float* __restrict__ grad = r.grad;
   __shared__ double4 acc_s[4][WR_QUADS];
   const int t = threadIdx.x, slot = t >> 6, qi = t & 63;
-  const int quad = blockIdx.x * WR_QUADS + qi;
+  const int quad = blk * WR_QUADS + qi;
   const int stride = Pq + 4;
   const int nq = stride / 4;
   double4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -1230,13 +1228,34 @@ __global__ __launch_bounds__(256) void ppo_wide_reduce_kernel(const float* __res
       if (k0 + 1 < P) grad[k0 + 1] = (float)s.y;
       if (k0 + 2 < P) grad[k0 + 2] = (float)s.z;
       if (k0 + 3 < P) grad[k0 + 3] = (float)s.w;
-    } else if (k0 == Pq && loss_out) {
-      const int64_t j = *cursor;
-      const int64_t lo = j * mb;
-      const int64_t rows = lo < N ? (N - lo < mb ? N - lo : mb) : 0;
-      const float inv = rows > 0 ? (scales ? scales[j] : 1.0f) / (float)rows : 0.f;
-      loss_out[0] = (float)s.x * inv + vf_coef * ((float)s.y * inv) - ent_coef * ((float)s.z * inv);
+    } else if (k0 == Pq && r.loss_out) {
+      const int64_t j = *r.cursor;
+      const int64_t lo = j * r.mb;
+      const int64_t rows = lo < r.N ? (r.N - lo < r.mb ? r.N - lo : r.mb) : 0;
+      const float inv = rows > 0 ? (r.scales ? r.scales[j] : 1.0f) / (float)rows : 0.f;
+      r.loss_out[0] = (float)s.x * inv + r.vf_coef * ((float)s.y * inv) - r.ent_coef * ((float)s.z * inv);
     }
+  }
+}
+__global__ __launch_bounds__(256) void ppo_wide_reduce_kernel(WrArgs r) { ppo_wide_reduce_body(r, blockIdx.x); }
+
+// dW0 (workgroups 0 .. G2-1) and, in the same launch, the fold of the tile kernel's partials
+// into every other gradient (workgroups G2 ..: ppo_wide_reduce_body): the two read disjoint
+// buffers, and the fold's ~38 MB stream at C5's minibatch ran alone behind the tile kernel
+// before (9 us per step), while dW0 streams X at ~35 % of HBM.
+template <int KSM, bool KSPEC = false>
+__global__ __launch_bounds__(WD_THREADS, 2) void ppo_wide_dw0_kernel(WdArgs a, float* part2, int G2,
+                                                                    WrArgs r) {
+  static_assert(WD_THREADS == 256, "the fold body runs 256-thread workgroups");
+  if ((int)blockIdx.x >= G2) {
+    ppo_wide_reduce_body(r, (int)blockIdx.x - G2);
+    return;
+  }
+  if constexpr (KSPEC) {
+    constexpr WdNet N = wd_make(WD_C5_D, WD_C5_A, 0);
+    ppo_wide_dw0_body<KSM>(N, a, part2, G2);
+  } else {
+    ppo_wide_dw0_body<KSM>(a.net, a, part2, G2);
   }
 }
 
@@ -1484,24 +1503,26 @@ extern "C" int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A,
 #undef WD_LAUNCH
   PRL_LAUNCH_CHECK("ppo_wide_grad");
   const int nq = (n.Pq + 4) / 4;
-  hipLaunchKernelGGL(ppo_wide_reduce_kernel, dim3((unsigned)cdiv(nq, WR_QUADS)), dim3(256), 0, st,
-                     part, G, n.P, n.Pq, grad, loss_out, cursor, scales, N, mini_batch, vf_coef,
-                     ent_coef);
-  PRL_LAUNCH_CHECK("ppo_wide_reduce");
-  if (split) {   // dW0 = dH0^T X, then its fold over the G2 partials into grad's W0 block
+  const int GR = (int)cdiv(nq, WR_QUADS);
+  const WrArgs fold{part, G, n.P, n.Pq, grad, loss_out, cursor, scales, N, mini_batch, vf_coef, ent_coef};
+  if (split) {   // dW0 = dH0^T X beside the partials' fold, then dW0's fold into grad's W0 block
+    const dim3 grid2((unsigned)(G2 + GR));
     if (KSM == 32)
-      hipLaunchKernelGGL(ppo_wide_dw0_kernel<32>, dim3(G2), dim3(WD_THREADS), 0, st, a, part2, G2);
+      hipLaunchKernelGGL(ppo_wide_dw0_kernel<32>, grid2, dim3(WD_THREADS), 0, st, a, part2, G2, fold);
     else
       if (wd_spec(n))
-        hipLaunchKernelGGL((ppo_wide_dw0_kernel<88, true>), dim3(G2), dim3(WD_THREADS), 0, st, a, part2, G2);
+        hipLaunchKernelGGL((ppo_wide_dw0_kernel<88, true>), grid2, dim3(WD_THREADS), 0, st, a, part2, G2, fold);
       else
-        hipLaunchKernelGGL((ppo_wide_dw0_kernel<88, false>), dim3(G2), dim3(WD_THREADS), 0, st, a, part2, G2);
+        hipLaunchKernelGGL((ppo_wide_dw0_kernel<88, false>), grid2, dim3(WD_THREADS), 0, st, a, part2, G2, fold);
     PRL_LAUNCH_CHECK("ppo_wide_dw0");
     const int P2 = WD_H * n.D;   // 64 D: a multiple of 4
+    const WrArgs fold2{part2, G2, P2, P2, grad + n.w0, nullptr, cursor, scales, N, mini_batch, vf_coef, ent_coef};
     hipLaunchKernelGGL(ppo_wide_reduce_kernel, dim3((unsigned)cdiv((P2 + 4) / 4, WR_QUADS)), dim3(256),
-                       0, st, part2, G2, P2, P2, grad + n.w0, nullptr, cursor, scales, N,
-                       mini_batch, vf_coef, ent_coef);
+                       0, st, fold2);
     PRL_LAUNCH_CHECK("ppo_wide_reduce_dw0");
+  } else {
+    hipLaunchKernelGGL(ppo_wide_reduce_kernel, dim3((unsigned)GR), dim3(256), 0, st, fold);
+    PRL_LAUNCH_CHECK("ppo_wide_reduce");
   }
   return PRL_OK;
 }

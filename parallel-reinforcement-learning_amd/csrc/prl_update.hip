@@ -247,44 +247,74 @@ extern "C" int prl_colsum_f32(const float* x, int64_t rows, int32_t cols, float*
 // (torch defaults: decoupled weight decay, lerp for exp_avg, addcmul for exp_avg_sq, bias
 // corrections from the incremented step count).  Parameters, gradient and both moments are flat
 // vectors in parameters() order (the policy's Parameters and the optimizer's state are views of
-// them, PPO/update.py FlatAdamState).  One workgroup of 1024 threads: the squared norm with float64
-// accumulators in a fixed thread -> wave -> workgroup order (deterministic), the clip coefficient
-// max_norm / (norm + 1e-6) clamped to 1 (the gradient is left clipped, as torch leaves p.grad),
-// then the elementwise update with the persistent engine's arithmetic (prl_ppo_update.hip
-// phase C).  ~37 K parameters (C5's net): a few microseconds, one launch instead of torch's
-// foreach-norm / stack / norm / coefficient / foreach-mul / fused-AdamW chain.
+// them, PPO/update.py FlatAdamState).  Two launches: flat_adamw_kernel (below) forms the squared
+// norm in float64 in a fixed order in EVERY workgroup, the clip coefficient max_norm / (norm +
+// 1e-6) clamped to 1, and updates its own 1,024 quads of params / exp_avg / exp_avg_sq with the
+// persistent engine's arithmetic (prl_ppo_update.hip phase C); workgroup 0 stores the norm.
+// flat_adam_clip_kernel then leaves the gradient clipped (as torch leaves p.grad) and advances
+// the step count — the gradient cannot be rewritten in the first launch, whose workgroups are
+// still reading all of it for their norms.  One launch of torch's foreach-norm / stack / norm /
+// coefficient / foreach-mul / fused-AdamW chain each.
 constexpr int FA_THREADS = 1024;
+constexpr int FA_BATCH = 8;   // gradient quads per thread in flight during the norm pass
 
+// Every workgroup forms the whole squared norm itself, in the same fixed order (thread t: quads
+// t, t + 1024, ... ascending, float64 fma; the 16 waves' sums in wave order), so all of them get
+// the same clip coefficient with no exchange; workgroup b then updates quads b*1024 + t (and the
+// last one the P % 4 tail).  (Until round 4 one 1024-thread workgroup did the norm AND the whole
+// update: ~19 us per C5 step, most of it one CU streaming ~600 KB in and out.)
 __global__ __launch_bounds__(FA_THREADS) void flat_adamw_kernel(
-    float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, float* __restrict__ step,
-    float* __restrict__ grad, int64_t P, float lr, double beta1, double beta2, float eps, float wd,
-    float max_norm) {
+    float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, const float* __restrict__ step,
+    const float* __restrict__ grad, int64_t P, float lr, double beta1, double beta2, float eps,
+    float wd, float max_norm, float* __restrict__ total_norm) {
   __shared__ double s_part[FA_THREADS / 64];
   __shared__ float s_c[3];
   const int t = threadIdx.x;
   const int64_t Q = P / 4;
+  const float4* g4p = reinterpret_cast<const float4*>(grad);
   double acc = 0.0;
-  for (int64_t q = t; q < Q; q += FA_THREADS) {
-    const float4 x = reinterpret_cast<const float4*>(grad)[q];
-    acc = fma((double)x.x, (double)x.x, acc);
-    acc = fma((double)x.y, (double)x.y, acc);
-    acc = fma((double)x.z, (double)x.z, acc);
-    acc = fma((double)x.w, (double)x.w, acc);
+  for (int64_t q0 = t; q0 < Q; q0 += (int64_t)FA_BATCH * FA_THREADS) {
+    float4 x[FA_BATCH];
+#pragma unroll
+    for (int i = 0; i < FA_BATCH; ++i) {
+      const int64_t q = q0 + (int64_t)i * FA_THREADS;
+      x[i] = q < Q ? g4p[q] : float4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < FA_BATCH; ++i) {
+      if (q0 + (int64_t)i * FA_THREADS < Q) {
+        acc = fma((double)x[i].x, (double)x[i].x, acc);
+        acc = fma((double)x[i].y, (double)x[i].y, acc);
+        acc = fma((double)x[i].z, (double)x[i].z, acc);
+        acc = fma((double)x[i].w, (double)x[i].w, acc);
+      }
+    }
   }
   for (int64_t k = 4 * Q + t; k < P; k += FA_THREADS) acc = fma((double)grad[k], (double)grad[k], acc);
   acc = wave_sum(acc);
   if ((t & 63) == 0) s_part[t >> 6] = acc;
   const float step0 = step[0];
+  // this workgroup's quad and its operands, loaded under the norm's reduction
+  const int64_t qm = (int64_t)blockIdx.x * FA_THREADS + t;
+  const bool mine = qm < Q;
+  float4 g4 = {0.f, 0.f, 0.f, 0.f}, p4 = g4, m4 = g4, v4 = g4;
+  if (mine) {
+    g4 = g4p[qm];
+    p4 = reinterpret_cast<const float4*>(p)[qm];
+    m4 = reinterpret_cast<const float4*>(m)[qm];
+    v4 = reinterpret_cast<const float4*>(v)[qm];
+  }
   __syncthreads();
   if (t == 0) {
     double tot = 0.0;
     for (int w = 0; w < FA_THREADS / 64; ++w) tot += s_part[w];
-    const float coef = max_norm / ((float)sqrt(tot) + 1e-6f);
+    const float norm = (float)sqrt(tot);
+    const float coef = max_norm / (norm + 1e-6f);
     s_c[0] = coef < 1.0f ? coef : 1.0f;
+    if (blockIdx.x == 0) total_norm[0] = norm;
     const double tstep = (double)step0 + 1.0;
     s_c[1] = (float)((double)lr / (1.0 - pow((double)beta1, tstep)));    // step size
     s_c[2] = (float)(1.0 / sqrt(1.0 - pow((double)beta2, tstep)));       // 1 / sqrt(bc2)
-    step[0] = step0 + 1.0f;
   }
   __syncthreads();
   const float clipc = s_c[0], step_size = s_c[1], inv_bc2_sqrt = s_c[2];
@@ -300,41 +330,63 @@ __global__ __launch_bounds__(FA_THREADS) void flat_adamw_kernel(
     float rq = __builtin_amdgcn_rcpf(denom);
     rq = fmaf(rq, fmaf(-denom, rq, 1.0f), rq);   // one Newton step: ~0.5 ulp
     pw = fmaf(-step_size, mw * rq, pw);
-    return gr;
   };
-  for (int64_t q = t; q < Q; q += FA_THREADS) {
-    float4 g4 = reinterpret_cast<const float4*>(grad)[q];
-    float4 p4 = reinterpret_cast<const float4*>(p)[q];
-    float4 m4 = reinterpret_cast<const float4*>(m)[q];
-    float4 v4 = reinterpret_cast<const float4*>(v)[q];
-    g4.x = upd(g4.x, p4.x, m4.x, v4.x);
-    g4.y = upd(g4.y, p4.y, m4.y, v4.y);
-    g4.z = upd(g4.z, p4.z, m4.z, v4.z);
-    g4.w = upd(g4.w, p4.w, m4.w, v4.w);
-    reinterpret_cast<float4*>(grad)[q] = g4;
-    reinterpret_cast<float4*>(p)[q] = p4;
-    reinterpret_cast<float4*>(m)[q] = m4;
-    reinterpret_cast<float4*>(v)[q] = v4;
+  if (mine) {
+    upd(g4.x, p4.x, m4.x, v4.x);
+    upd(g4.y, p4.y, m4.y, v4.y);
+    upd(g4.z, p4.z, m4.z, v4.z);
+    upd(g4.w, p4.w, m4.w, v4.w);
+    reinterpret_cast<float4*>(p)[qm] = p4;
+    reinterpret_cast<float4*>(m)[qm] = m4;
+    reinterpret_cast<float4*>(v)[qm] = v4;
   }
-  for (int64_t k = 4 * Q + t; k < P; k += FA_THREADS) {
-    float pw = p[k], mw = m[k], vw = v[k];
-    grad[k] = upd(grad[k], pw, mw, vw);
-    p[k] = pw;
-    m[k] = mw;
-    v[k] = vw;
+  if (blockIdx.x + 1 == gridDim.x) {   // the P % 4 tail
+    for (int64_t k = 4 * Q + t; k < P; k += FA_THREADS) {
+      float pw = p[k], mw = m[k], vw = v[k];
+      upd(grad[k], pw, mw, vw);
+      p[k] = pw;
+      m[k] = mw;
+      v[k] = vw;
+    }
+  }
+}
+// grad *= the clip coefficient (from the stored norm, formed as flat_adamw_kernel formed it:
+// the same bits); thread 0 of workgroup 0 advances the step count
+__global__ __launch_bounds__(256) void flat_adam_clip_kernel(float* __restrict__ grad, int64_t P,
+                                                             float max_norm,
+                                                             const float* __restrict__ total_norm,
+                                                             float* __restrict__ step) {
+  const float coef = max_norm / (total_norm[0] + 1e-6f);
+  const float clipc = coef < 1.0f ? coef : 1.0f;
+  const int64_t Q = P / 4, q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q < Q) {
+    float4 g = reinterpret_cast<const float4*>(grad)[q];
+    g.x *= clipc;
+    g.y *= clipc;
+    g.z *= clipc;
+    g.w *= clipc;
+    reinterpret_cast<float4*>(grad)[q] = g;
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t k = 4 * Q + threadIdx.x; k < P; k += 256) grad[k] *= clipc;
+    if (threadIdx.x == 0) step[0] = step[0] + 1.0f;
   }
 }
 
 extern "C" int prl_flat_adamw(float* params, float* exp_avg, float* exp_avg_sq, float* step,
                               float* grad, int64_t P, float lr, double beta1, double beta2, float eps,
-                              float weight_decay, float max_norm, void* stream) {
+                              float weight_decay, float max_norm, float* total_norm, void* stream) {
   PRL_REQUIRE(P > 0 && P < (int64_t)1 << 30, "prl_flat_adamw: bad size %lld", (long long)P);
-  PRL_REQUIRE(params && exp_avg && exp_avg_sq && step && grad, "prl_flat_adamw: null pointer");
+  PRL_REQUIRE(params && exp_avg && exp_avg_sq && step && grad && total_norm, "prl_flat_adamw: null pointer");
   PRL_REQUIRE(aligned16(params) && aligned16(exp_avg) && aligned16(exp_avg_sq) && aligned16(grad),
               "prl_flat_adamw: buffers must be 16-B aligned");
-  hipLaunchKernelGGL(flat_adamw_kernel, dim3(1), dim3(FA_THREADS), 0, as_stream(stream), params,
+  const unsigned nblk = (unsigned)std::max<int64_t>(1, cdiv(P / 4, FA_THREADS));
+  hipLaunchKernelGGL(flat_adamw_kernel, dim3(nblk), dim3(FA_THREADS), 0, as_stream(stream), params,
                      exp_avg, exp_avg_sq, step, grad, P, lr, beta1, beta2, eps, weight_decay,
-                     max_norm);
+                     max_norm, total_norm);
   PRL_LAUNCH_CHECK("flat_adamw");
+  hipLaunchKernelGGL(flat_adam_clip_kernel, dim3((unsigned)std::max<int64_t>(1, cdiv(P / 4, 256))),
+                     dim3(256), 0, as_stream(stream), grad, P, max_norm, total_norm, step);
+  PRL_LAUNCH_CHECK("flat_adam_clip");
   return PRL_OK;
 }

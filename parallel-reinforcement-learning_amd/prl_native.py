@@ -104,7 +104,7 @@ SIGNATURES = {
                          + [_P, _P],
     "prl_colsum_partial_floats": [_I64, _I32],
     "prl_colsum_f32": [_P, _I64, _I32, _P, _P, _I64, _P],
-    "prl_flat_adamw": [_P, _P, _P, _P, _P, _I64, _F32, _F64, _F64, _F32, _F32, _F32, _P],
+    "prl_flat_adamw": [_P, _P, _P, _P, _P, _I64, _F32, _F64, _F64, _F32, _F32, _F32, _P, _P],
     "prl_ppo_grad_fold_step": [_P] * 7 + [_I64, _F32, _I32, _I32, _I32] + [_P] * 5
                               + [_I64, _I32, _I64, _F32] + _UPD_SCALARS + [_P, _P, _P, _I64, _P],
 }
@@ -701,17 +701,23 @@ def ppo_update_set_repl(replicas: int) -> int:
 
 
 def flat_adamw(params, exp_avg, exp_avg_sq, step, grad, lr, beta1, beta2, eps, weight_decay,
-               max_norm):
-    """clip_grad_norm_(max_norm) + AdamW.step() over flat f32 vectors (one launch)."""
+               max_norm, total_norm=None):
+    """clip_grad_norm_(max_norm) + AdamW.step() over flat f32 vectors (two launches).  Returns
+    total_norm: a one-entry f32 device tensor holding the gradient's norm (clip_grad_norm_'s
+    return value; a new one unless passed)."""
     P = int(params.numel())
     for t, n in ((exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq"), (grad, "grad")):
         if t.numel() != P:
             raise ValueError(f"{n} has {t.numel()} entries, params {P}")
+    if total_norm is None:
+        total_norm = torch.empty(1, dtype=torch.float32, device=params.device)
     _check(lib().prl_flat_adamw(
         _dev(params, torch.float32, "params"), _dev(exp_avg, torch.float32, "exp_avg"),
         _dev(exp_avg_sq, torch.float32, "exp_avg_sq"), _dev(step, torch.float32, "step"),
         _dev(grad, torch.float32, "grad"), P, float(lr), float(beta1), float(beta2), float(eps),
-        float(weight_decay), float(max_norm), _stream()), "prl_flat_adamw")
+        float(weight_decay), float(max_norm), _dev(total_norm, torch.float32, "total_norm"),
+        _stream()), "prl_flat_adamw")
+    return total_norm
 
 
 def ppo_update_last_plan() -> dict:

@@ -384,8 +384,8 @@ def test_wide_graphed_rollout_equals_eager_rollout(monkeypatch):
 
 @pytest.mark.parametrize("scale", [1e-3, 1e2])
 def test_flat_adamw_matches_torch_clip_and_adamw(scale):
-    """prl_flat_adamw (the wide step's optimizer tail: clip_grad_norm_(2.0) + AdamW.step() in one
-    launch over flat buffers, PPO.py:248-250) against torch's own clip_grad_norm_ + AdamW
+    """prl_flat_adamw (the wide step's optimizer tail: clip_grad_norm_(2.0) + AdamW.step() in two
+    launches over flat buffers, PPO.py:248-250; ~37 K parameters = 10 workgroups of the first) against torch's own clip_grad_norm_ + AdamW
     (the reference's defaults: bias corrections from Python doubles) on C5's parameter shapes
     over four steps.  scale 1e-3: norm < 2, no clipping;
     1e2: clipping every step.  The two differ only in float32 rounding (norm summed in float64
@@ -410,13 +410,14 @@ def test_flat_adamw_matches_torch_clip_and_adamw(scale):
         for p, sh in zip(ref, shapes):
             p.grad = grad[off:off + p.numel()].view(sh).clone()
             off += p.numel()
-        torch.nn.utils.clip_grad_norm_(ref, 2.0)
+        tn = torch.nn.utils.clip_grad_norm_(ref, 2.0)
         opt.step()
         gbuf = grad.clone()
-        prl_native.flat_adamw(flat, m, v, step, gbuf, 1e-3, 0.9, 0.999, 1e-8, 1e-2, 2.0)
+        got_n = prl_native.flat_adamw(flat, m, v, step, gbuf, 1e-3, 0.9, 0.999, 1e-8, 1e-2, 2.0)
         torch.cuda.synchronize()
         want_g = torch.cat([p.grad.reshape(-1) for p in ref])
         assert float((gbuf - want_g).abs().max()) <= 1e-6 * float(want_g.abs().max())
+        assert abs(float(got_n) - float(tn)) <= 1e-6 * float(tn)   # clip_grad_norm_'s return value
     want = torch.cat([p.detach().reshape(-1) for p in ref])
     ulp = float(torch.finfo(torch.float32).eps) * float(want.abs().max())
     assert float((flat - want).abs().max()) <= 16 * ulp, float((flat - want).abs().max())
