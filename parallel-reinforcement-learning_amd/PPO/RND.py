@@ -4,11 +4,15 @@ Same modules, parameter names, initialisation and optimiser as the reference (ta
 pred_net are independent re-initialisations of Linear(D,64) -> GroupNorm(8,64) -> SiLU ->
 Linear(64,D); target frozen; AdamW lr 1e-3 + MSE for the predictor).  The intrinsic-reward
 forward (the hot part: every learn() call runs it over all N transitions) is one fused HIP
-kernel on fp32 MFMA (prl_rnd_forward); the predictor update stays in PyTorch (north star).
+kernel on fp32 MFMA (prl_rnd_forward); the predictor update's forward / backward stay PyTorch
+(north star), replayed as one HIP graph per minibatch on one GPU with the native AdamW
+(prl_flat_adamw) stepping flat views of the predictor's state.
 """
 from __future__ import annotations
 
+import os
 from copy import deepcopy
+from types import SimpleNamespace
 
 import torch
 from torch import nn, optim
@@ -97,6 +101,87 @@ class RND(nn.Module):
         prl_native.rnd_forward(x, tp, pp, float(self.beta), out)
         return out
 
+    # ------------------------------------------------------------------ graphed update (one GPU)
+    def _flat_state(self):
+        """The predictor's parameters, gradients and AdamW state as flat vectors (views, as the
+        policy's: update.FlatAdamState), so one native AdamW launch pair steps them."""
+        from .update import FlatAdamState
+        params = list(self.pred_net.parameters())
+        fa = getattr(self, "_fa", None)
+        if fa is None or len(fa.params) != len(params) or any(a is not b for a, b in zip(fa.params, params)):
+            fa = self._fa = FlatAdamState(SimpleNamespace(policy=self.pred_net, optimizer=self.optimizer))
+            self._fgrad = torch.zeros_like(fa.flat)
+            self._graph = None
+        else:
+            fa.prepare()
+        off = 0
+        base = self._fgrad.data_ptr()
+        for p in params:   # every .grad a view of the flat gradient (re-attached if replaced)
+            if p.grad is None or p.grad.data_ptr() != base + 4 * off:
+                p.grad = self._fgrad[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        return fa
+
+    def _step_body(self, x, fa):
+        """One update_pred step on rows x: MSE(pred(x), target(x)) backward into the flat
+        gradient, then AdamW (no clipping: max_norm = inf gives the coefficient 1)."""
+        self._fgrad.zero_()
+        with torch.no_grad():
+            targets = self.target_net(x)
+        preds = self.pred_net(x)
+        loss = (mse_loss(preds, targets)
+                if isinstance(self.loss_fn, nn.MSELoss) and self.loss_fn.reduction == "mean"
+                else self.loss_fn(preds, targets))
+        loss.backward()
+        group = self.optimizer.param_groups[0]
+        beta1, beta2 = group["betas"]
+        prl_native.flat_adamw(fa.flat, fa.m, fa.v, fa.step, self._fgrad, group["lr"], beta1, beta2,
+                              group["eps"], group["weight_decay"], float("inf"), fa.total_norm)
+
+    def _graphed_ok(self, values, all_reduce, counts) -> bool:
+        if all_reduce is not None or counts is not None or os.environ.get("PRL_RND_GRAPH", "1") == "0":
+            return False
+        if not values or not torch.cuda.is_available():
+            return False
+        w = self.pred_net[0].weight
+        if not (w.is_cuda and w.dtype == torch.float32) or type(self.optimizer) is not optim.AdamW:
+            return False
+        if len(self.optimizer.param_groups) != 1 or self.optimizer.param_groups[0].get("amsgrad"):
+            return False
+        return all(v.is_cuda and v.dtype == torch.float32 and v.dim() == 2 for v in values)
+
+    def _update_graphed(self, values) -> None:
+        """update_pred on one GPU: every full-size minibatch replays ONE captured HIP graph of
+        the step (forward of both nets, MSE, backward, native AdamW) on a static input buffer the
+        minibatch is copied into; the first full one runs eagerly (PyTorch's warm-up before a
+        capture, a real step) and a ragged last one eagerly.  Same steps in the same order as the
+        loop below; AdamW's arithmetic is prl_flat_adamw's (torch's up to fused multiply-adds)."""
+        fa = self._flat_state()
+        mb = max(v.shape[0] for v in values)
+        for v in values:
+            v = v.contiguous()
+            if v.shape[0] != mb:
+                self._step_body(v, fa)
+                continue
+            g = self._graph
+            if g is None or self._graph_x.shape != v.shape:
+                # warm-up (a real step) and capture on a side stream, as PyTorch requires
+                self._graph_x = torch.empty_like(v)
+                g = torch.cuda.CUDAGraph()
+                cur = torch.cuda.current_stream()
+                s = torch.cuda.Stream()
+                s.wait_stream(cur)
+                with torch.cuda.stream(s):
+                    self._step_body(v, fa)
+                    with torch.cuda.graph(g, stream=s):
+                        self._step_body(self._graph_x, fa)
+                cur.wait_stream(s)
+                self._graph = g
+                continue
+            self._graph_x.copy_(v)
+            g.replay()
+        fa.sync()
+
     def update_pred(self, values, all_reduce=None, counts=None) -> None:
         """RND.py:96-115: one MSE/AdamW pass of the predictor over the minibatches (PyTorch).
 
@@ -107,6 +192,10 @@ class RND(nn.Module):
         rank, ranks past their last minibatch contribute zero gradients (lockstep)."""
         self.pred_net.train()
         values = list(values)
+        if self._graphed_ok(values, all_reduce, counts):
+            self._update_graphed(values)
+            self.pred_net.eval()
+            return
         steps = len(values) if counts is None else len(counts)
         params = list(self.pred_net.parameters())
         for j in range(steps):

@@ -1273,7 +1273,13 @@ bool wd_spec(const WdNet& n) {
 int wd_grid(int64_t mb);
 int wd_grid2(int64_t mb) {
   const int64_t tiles = (mb + WD2_RT - 1) / WD2_RT;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, WD2_GRID_MAX));
+  // PRL_WIDE_G2 (A/B): cap on dW0's workgroups (its partials, 89 KB each at C5, are folded after it)
+  static const int cap = [] {
+    const char* e = getenv("PRL_WIDE_G2");
+    const int v = e ? atoi(e) : WD2_GRID_MAX;
+    return v >= 1 && v <= WD2_GRID_MAX ? v : WD2_GRID_MAX;
+  }();
+  return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cap));
 }
 bool wd_split() {
   static const int v = [] {

@@ -180,3 +180,43 @@ def test_load_reference_checkpoint_then_learn(golden, tag):
         sd = torch.load(os.path.join(tmp, "Policy_weights.pth"), weights_only=True)
         for k, v in p.policy.state_dict().items():
             assert torch.equal(sd[k].to(v.device), v)
+
+
+def test_update_pred_graphed_equals_eager(monkeypatch):
+    """update_pred on one GPU (the default): every full minibatch after the first replays one
+    captured graph of the step (forward, MSE, backward, native AdamW on flat views) — against the
+    PyTorch loop (PRL_RND_GRAPH=0: torch AdamW) on the same 16,384-row minibatches (the split-K
+    backward, as at C5's 65,536) plus a ragged last one, over two update_pred calls (the second
+    replays the graph captured by the first).  The gradients are the same kernels in the same
+    order; only AdamW's arithmetic differs (prl_flat_adamw fuses p * decay and the step into
+    fused multiply-adds: <= 2 ulps of a weight per step, test_flat_adamw_matches_torch_clip_and_adamw),
+    so 12 steps stay within 1e-6 of weights |w| <= 0.3; the moments within 1e-5 relative."""
+    import copy
+    from PPO import RND
+    torch.manual_seed(3)
+    D = 348
+    a = RND(D, D)
+    b = copy.deepcopy(a)
+    b.optimizer = torch.optim.AdamW(params=b.pred_net.parameters(), lr=0.001)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for _ in range(2):
+        X = torch.randn(5 * 16384 + 1000, D, device="cuda", generator=g)
+        values = list(X.split(16384))
+        monkeypatch.delenv("PRL_RND_GRAPH", raising=False)
+        a.update_pred(values)
+        monkeypatch.setenv("PRL_RND_GRAPH", "0")
+        b.update_pred(values)
+    torch.cuda.synchronize()
+    assert a._graph is not None
+    for (k, va), vb in zip(a.pred_net.state_dict().items(), b.pred_net.state_dict().values()):
+        assert float((va - vb).abs().max()) <= 1e-6, (k, float((va - vb).abs().max()))
+    sa, sb = a.optimizer.state_dict()["state"], b.optimizer.state_dict()["state"]
+    for i in sb:
+        assert float(sa[i]["step"]) == float(sb[i]["step"]) == 12.0
+        for key in ("exp_avg", "exp_avg_sq"):
+            ref = sb[i][key]
+            assert float((sa[i][key] - ref).abs().max()) <= 1e-5 * float(ref.abs().max()) + 1e-12, key
+    # the intrinsic reward reads the (flat-view) predictor like any other
+    r_a = a.compute_intrinsic_reward(X[:4096])
+    r_b = b.compute_intrinsic_reward(X[:4096])
+    assert float((r_a - r_b).abs().max()) <= 1e-4 * float(r_b.abs().max())
