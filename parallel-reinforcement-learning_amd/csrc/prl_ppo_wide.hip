@@ -1163,10 +1163,12 @@ __device__ __forceinline__ void ppo_wide_dw0_body(const WdNet& n, const WdArgs& 
   }
 }
 
-// grad[k] = sum_g part[g][k] in workgroup order (f64), k < P; loss = (L0 + vf L1 - ent L2) / B.
-// Block = 64 quads x 4 workgroup slots; slot s sums workgroups s, s + 4, ... and the 4 slot
-// sums are added in slot order.
-constexpr int WR_QUADS = 64;
+// grad[k] = sum_g part[g][k] (f64), k < P; loss = (L0 + vf L1 - ent L2) / B.  Block = 256 / S
+// quads x S workgroup slots; slot s sums workgroups s, s + S, s + 2S, ... in that order, and the S
+// slot sums are added in slot order (deterministic).  The standalone fold (dW0's 256 partials)
+// runs S = 16: 4x the blocks of S = 4, 6.6 vs 8.4 us at C5; inside the dW0 launch the tile
+// partials' fold keeps S = 4 (with S = 16 its extra blocks slowed dW0 by 1.1 us;
+// profiles/r04_wide_fold_ab.md).
 struct WrArgs {
   const float* part;
   int G, P, Pq;
@@ -1177,23 +1179,25 @@ struct WrArgs {
   int64_t N, mb;
   float vf_coef, ent_coef;
 };
+template <int S>
 __device__ __forceinline__ void ppo_wide_reduce_body(const WrArgs& r, int blk) {
+  constexpr int QU = 256 / S;
   const float* __restrict__ part = r.part;
   const int G = r.G, P = r.P, Pq = r.Pq;
   float* __restrict__ grad = r.grad;
-  __shared__ double4 acc_s[4][WR_QUADS];
-  const int t = threadIdx.x, slot = t >> 6, qi = t & 63;
-  const int quad = blk * WR_QUADS + qi;
+  __shared__ double4 acc_s[S][QU];
+  const int t = threadIdx.x, slot = t / QU, qi = t % QU;
+  const int quad = blk * QU + qi;
   const int stride = Pq + 4;
   const int nq = stride / 4;
   double4 acc = {0.0, 0.0, 0.0, 0.0};
   if (quad < nq) {
     const float4* src = reinterpret_cast<const float4*>(part) + quad;
     int g = slot;
-    for (; g + 12 < G; g += 16) {
+    for (; g + 3 * S < G; g += 4 * S) {
       float4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = src[(int64_t)(g + 4 * u) * nq];
+      for (int u = 0; u < 4; ++u) v[u] = src[(int64_t)(g + S * u) * nq];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         acc.x += v[u].x;
@@ -1202,7 +1206,7 @@ __device__ __forceinline__ void ppo_wide_reduce_body(const WrArgs& r, int blk) {
         acc.w += v[u].w;
       }
     }
-    for (; g < G; g += 4) {
+    for (; g < G; g += S) {
       const float4 v = src[(int64_t)g * nq];
       acc.x += v.x;
       acc.y += v.y;
@@ -1215,7 +1219,7 @@ __device__ __forceinline__ void ppo_wide_reduce_body(const WrArgs& r, int blk) {
   if (slot == 0 && quad < nq) {
     double4 s = acc_s[0][qi];
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
+    for (int k = 1; k < S; ++k) {
       const double4 o = acc_s[k][qi];
       s.x += o.x;
       s.y += o.y;
@@ -1237,18 +1241,21 @@ __device__ __forceinline__ void ppo_wide_reduce_body(const WrArgs& r, int blk) {
     }
   }
 }
-__global__ __launch_bounds__(256) void ppo_wide_reduce_kernel(WrArgs r) { ppo_wide_reduce_body(r, blockIdx.x); }
+template <int S>
+int wr_blocks(int nq) { return (int)cdiv(nq, 256 / S); }
+template <int S>
+__global__ __launch_bounds__(256) void ppo_wide_reduce_kernel(WrArgs r) { ppo_wide_reduce_body<S>(r, blockIdx.x); }
 
 // dW0 (workgroups 0 .. G2-1) and, in the same launch, the fold of the tile kernel's partials
 // into every other gradient (workgroups G2 ..: ppo_wide_reduce_body): the two read disjoint
 // buffers, and the fold's ~38 MB stream at C5's minibatch ran alone behind the tile kernel
 // before (9 us per step), while dW0 streams X at ~35 % of HBM.
-template <int KSM, bool KSPEC = false>
+template <int KSM, bool KSPEC = false, int S = 4>
 __global__ __launch_bounds__(WD_THREADS, 2) void ppo_wide_dw0_kernel(WdArgs a, float* part2, int G2,
                                                                     WrArgs r) {
   static_assert(WD_THREADS == 256, "the fold body runs 256-thread workgroups");
   if ((int)blockIdx.x >= G2) {
-    ppo_wide_reduce_body(r, (int)blockIdx.x - G2);
+    ppo_wide_reduce_body<S>(r, (int)blockIdx.x - G2);
     return;
   }
   if constexpr (KSPEC) {
@@ -1509,25 +1516,23 @@ extern "C" int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A,
 #undef WD_LAUNCH
   PRL_LAUNCH_CHECK("ppo_wide_grad");
   const int nq = (n.Pq + 4) / 4;
-  const int GR = (int)cdiv(nq, WR_QUADS);
   const WrArgs fold{part, G, n.P, n.Pq, grad, loss_out, cursor, scales, N, mini_batch, vf_coef, ent_coef};
   if (split) {   // dW0 = dH0^T X beside the partials' fold, then dW0's fold into grad's W0 block
-    const dim3 grid2((unsigned)(G2 + GR));
+    const dim3 grid2((unsigned)(G2 + wr_blocks<4>(nq)));
     if (KSM == 32)
       hipLaunchKernelGGL(ppo_wide_dw0_kernel<32>, grid2, dim3(WD_THREADS), 0, st, a, part2, G2, fold);
+    else if (wd_spec(n))
+      hipLaunchKernelGGL((ppo_wide_dw0_kernel<88, true>), grid2, dim3(WD_THREADS), 0, st, a, part2, G2, fold);
     else
-      if (wd_spec(n))
-        hipLaunchKernelGGL((ppo_wide_dw0_kernel<88, true>), grid2, dim3(WD_THREADS), 0, st, a, part2, G2, fold);
-      else
-        hipLaunchKernelGGL((ppo_wide_dw0_kernel<88, false>), grid2, dim3(WD_THREADS), 0, st, a, part2, G2, fold);
+      hipLaunchKernelGGL((ppo_wide_dw0_kernel<88, false>), grid2, dim3(WD_THREADS), 0, st, a, part2, G2, fold);
     PRL_LAUNCH_CHECK("ppo_wide_dw0");
     const int P2 = WD_H * n.D;   // 64 D: a multiple of 4
     const WrArgs fold2{part2, G2, P2, P2, grad + n.w0, nullptr, cursor, scales, N, mini_batch, vf_coef, ent_coef};
-    hipLaunchKernelGGL(ppo_wide_reduce_kernel, dim3((unsigned)cdiv((P2 + 4) / 4, WR_QUADS)), dim3(256),
-                       0, st, fold2);
+    hipLaunchKernelGGL(ppo_wide_reduce_kernel<16>, dim3((unsigned)wr_blocks<16>((P2 + 4) / 4)), dim3(256), 0,
+                       st, fold2);
     PRL_LAUNCH_CHECK("ppo_wide_reduce_dw0");
   } else {
-    hipLaunchKernelGGL(ppo_wide_reduce_kernel, dim3((unsigned)GR), dim3(256), 0, st, fold);
+    hipLaunchKernelGGL(ppo_wide_reduce_kernel<16>, dim3((unsigned)wr_blocks<16>(nq)), dim3(256), 0, st, fold);
     PRL_LAUNCH_CHECK("ppo_wide_reduce");
   }
   return PRL_OK;
