@@ -465,7 +465,8 @@ def test_wide_learn_native_adam_equals_torch_adam(monkeypatch):
     assert float((v1 - v0).abs().max()) <= 1e-3 * (1 + float(v0.abs().max()))
 
 
-def test_persistent_wide_rollout_matches_per_step_rollout(monkeypatch):
+@pytest.mark.parametrize("E,stride", [(300, 7), (5000, 211)])
+def test_persistent_wide_rollout_matches_per_step_rollout(monkeypatch, E, stride):
     """prl_wide_rollout (the whole C5 rollout in ONE launch, each wave stepping 16 envs to the end
     of their episodes) against the per-step path (prl_ppo_wide_dist + prl_rollout_step per vector
     step, PRL_WIDE_ROLLOUT=0, eager) on the same runner seeds and policy, three rollouts with a
@@ -473,11 +474,12 @@ def test_persistent_wide_rollout_matches_per_step_rollout(monkeypatch):
     synthetic env's do not depend on the actions); actions to float32 rounding of the two forward
     orders (<= 2e-5 absolute, actions in [-1, 1]); rewards (1 - 0.01 sum a^2) to 1e-5.  The fused
     actions are also checked against a float64 forward of policy_old with the same Philox
-    normals (oracle.sample_normal): tanh(mu + std z) to 2e-5."""
+    normals (oracle.sample_normal): tanh(mu + std z) to 2e-5.  E = 300: 19 workgroups of 16 envs,
+    the last one ragged; E = 5000: 256 workgroups of 20 envs each, so every workgroup refills
+    its lanes from its queue as episodes end (the team form's env queue)."""
     import oracle as O
     from AsyncTools.AsyncPPO import AsyncPPO
     from PPO import PPO
-    E = 300                      # 19 tiles, the last one ragged
     outs = []
     for fused in ("1", "0"):
         monkeypatch.setenv("PRL_WIDE_ROLLOUT", fused)
@@ -513,7 +515,7 @@ def test_persistent_wide_rollout_matches_per_step_rollout(monkeypatch):
         lens = lens.numpy().astype(np.int64)
         e_of = np.repeat(np.arange(E), lens)
         t_of = np.concatenate([np.arange(L) for L in lens])
-        idx = np.arange(0, len(e_of), 7)           # a sample of the transitions
+        idx = np.arange(0, len(e_of), stride)      # a sample of the transitions
         with torch.no_grad():
             feats = pol.model(S1[idx].double())
             mu = pol.mu_head(feats)
