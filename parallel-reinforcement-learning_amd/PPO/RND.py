@@ -42,6 +42,25 @@ class _MSELoss(torch.autograd.Function):
         return d * (g * (2.0 / float(d.numel()))), None
 
 
+class _MaskedMSELoss(torch.autograd.Function):
+    """The graphed update's MSE: the rows past the minibatch's (mask 0: a ragged minibatch padded
+    to the graph's static shape) contribute nothing, and inv = 1 / (rows x D) is a device scalar,
+    so one captured graph serves every minibatch size.  With mask = 1 it is _MSELoss: the same
+    gradient bits (2 * inv is exact), the loss up to multiplying by 1/numel instead of dividing."""
+
+    @staticmethod
+    def forward(ctx, preds, targets, mask, inv):
+        d = (preds - targets).mul_(mask)
+        ctx.save_for_backward(d, inv)
+        flat = d.view(-1)
+        return torch.dot(flat, flat) * inv
+
+    @staticmethod
+    def backward(ctx, g):
+        d, inv = ctx.saved_tensors
+        return d * (g * 2.0 * inv), None, None, None
+
+
 def mse_loss(preds, targets):
     if preds.is_cuda and preds.dtype == torch.float32 and preds.shape == targets.shape:
         return _MSELoss.apply(preds, targets)
@@ -122,16 +141,20 @@ class RND(nn.Module):
             off += p.numel()
         return fa
 
-    def _step_body(self, x, fa):
+    def _step_body(self, x, fa, mask=None, inv=None):
         """One update_pred step on rows x: MSE(pred(x), target(x)) backward into the flat
-        gradient, then AdamW (no clipping: max_norm = inf gives the coefficient 1)."""
+        gradient, then AdamW (no clipping: max_norm = inf gives the coefficient 1).  mask / inv:
+        the graphed step's row mask and 1 / (rows x D) (rows past the minibatch are padding)."""
         self._fgrad.zero_()
         with torch.no_grad():
             targets = self.target_net(x)
         preds = self.pred_net(x)
-        loss = (mse_loss(preds, targets)
-                if isinstance(self.loss_fn, nn.MSELoss) and self.loss_fn.reduction == "mean"
-                else self.loss_fn(preds, targets))
+        if mask is not None:
+            loss = _MaskedMSELoss.apply(preds, targets, mask, inv)
+        else:
+            loss = (mse_loss(preds, targets)
+                    if isinstance(self.loss_fn, nn.MSELoss) and self.loss_fn.reduction == "mean"
+                    else self.loss_fn(preds, targets))
         loss.backward()
         group = self.optimizer.param_groups[0]
         beta1, beta2 = group["betas"]
@@ -151,22 +174,28 @@ class RND(nn.Module):
         return all(v.is_cuda and v.dtype == torch.float32 and v.dim() == 2 for v in values)
 
     def _update_graphed(self, values) -> None:
-        """update_pred on one GPU: every full-size minibatch replays ONE captured HIP graph of
-        the step (forward of both nets, MSE, backward, native AdamW) on a static input buffer the
-        minibatch is copied into; the first full one runs eagerly (PyTorch's warm-up before a
-        capture, a real step) and a ragged last one eagerly.  Same steps in the same order as the
-        loop below; AdamW's arithmetic is prl_flat_adamw's (torch's up to fused multiply-adds)."""
+        """update_pred on one GPU: every minibatch replays ONE captured HIP graph of the step
+        (forward of both nets, masked MSE, backward, native AdamW) on a static input buffer the
+        minibatch is copied into; a ragged last minibatch fills the buffer's first rows and a
+        row mask zeroes the rest's contribution (the padding rows hold the previous minibatch's
+        finite values, so 0 x them is 0).  The first minibatch of a new shape runs eagerly on a
+        side stream (PyTorch's warm-up before a capture, a real step) and is then captured.  Same
+        steps in the same order as the loop below; the ragged step sums the same products with
+        zero rows added (float32 rounding only); AdamW's arithmetic is prl_flat_adamw's (torch's
+        up to fused multiply-adds)."""
         fa = self._flat_state()
         mb = max(v.shape[0] for v in values)
+        D = values[0].shape[1]
         for v in values:
             v = v.contiguous()
-            if v.shape[0] != mb:
-                self._step_body(v, fa)
-                continue
+            rows = v.shape[0]
             g = self._graph
-            if g is None or self._graph_x.shape != v.shape:
-                # warm-up (a real step) and capture on a side stream, as PyTorch requires
-                self._graph_x = torch.empty_like(v)
+            if g is None or self._graph_x.shape != (mb, D):
+                # warm-up (a real step, unpadded) and capture on a side stream, as PyTorch requires
+                self._graph_x = torch.zeros(mb, D, dtype=torch.float32, device=v.device)
+                self._graph_mask = torch.ones(mb, 1, dtype=torch.float32, device=v.device)
+                self._graph_inv = torch.full((), 1.0 / (mb * D), dtype=torch.float32, device=v.device)
+                self._graph_rows = mb
                 g = torch.cuda.CUDAGraph()
                 cur = torch.cuda.current_stream()
                 s = torch.cuda.Stream()
@@ -174,11 +203,16 @@ class RND(nn.Module):
                 with torch.cuda.stream(s):
                     self._step_body(v, fa)
                     with torch.cuda.graph(g, stream=s):
-                        self._step_body(self._graph_x, fa)
+                        self._step_body(self._graph_x, fa, self._graph_mask, self._graph_inv)
                 cur.wait_stream(s)
                 self._graph = g
                 continue
-            self._graph_x.copy_(v)
+            if rows != self._graph_rows:
+                self._graph_mask[:rows].fill_(1.0)
+                self._graph_mask[rows:].fill_(0.0)
+                self._graph_inv.fill_(1.0 / (rows * D))
+                self._graph_rows = rows
+            self._graph_x[:rows].copy_(v)
             g.replay()
         fa.sync()
 
