@@ -571,7 +571,7 @@ def test_scan_and_flatten_vs_reference_worker(golden):
     np.testing.assert_array_equal(Dn.cpu().numpy(), g["D"])
 
 
-@pytest.mark.parametrize("E,D", [(65_536, 4), (3, 3), (1000, 348)])
+@pytest.mark.parametrize("E,D", [(65_536, 4), (3, 3), (1000, 348), (500, 350)])
 def test_flatten_large_vs_numpy(E, D):
     N = native()
     rng = np.random.default_rng(E)
