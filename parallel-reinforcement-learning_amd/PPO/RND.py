@@ -161,6 +161,16 @@ class RND(nn.Module):
         prl_native.flat_adamw(fa.flat, fa.m, fa.v, fa.step, self._fgrad, group["lr"], beta1, beta2,
                               group["eps"], group["weight_decay"], float("inf"), fa.total_norm)
 
+    def _flat_dp_ok(self, values) -> bool:
+        w = self.pred_net[0].weight
+        if not (w.is_cuda and w.dtype == torch.float32) or type(self.optimizer) is not optim.AdamW:
+            return False
+        if len(self.optimizer.param_groups) != 1 or self.optimizer.param_groups[0].get("amsgrad"):
+            return False
+        if not (isinstance(self.loss_fn, nn.MSELoss) and self.loss_fn.reduction == "mean"):
+            return False
+        return all(v.is_cuda and v.dtype == torch.float32 and v.dim() == 2 for v in values)
+
     def _graphed_ok(self, values, all_reduce, counts) -> bool:
         if all_reduce is not None or counts is not None or os.environ.get("PRL_RND_GRAPH", "1") == "0":
             return False
@@ -231,6 +241,31 @@ class RND(nn.Module):
             self.pred_net.eval()
             return
         steps = len(values) if counts is None else len(counts)
+        if all_reduce is not None and self._flat_dp_ok(values):
+            # data-parallel ranks on the GPU: the gradient is ONE flat buffer (the parameters'
+            # .grad are views of it), so each step is one all-reduce instead of one per parameter
+            # tensor, and AdamW is the native flat launch pair (max_norm = inf: no clipping)
+            fa = self._flat_state()
+            group = self.optimizer.param_groups[0]
+            beta1, beta2 = group["betas"]
+            for j in range(steps):
+                self._fgrad.zero_()
+                if j < len(values):
+                    i = values[j]
+                    with torch.no_grad():
+                        targets = self.target_net(i)
+                    preds = self.pred_net(i)
+                    loss = mse_loss(preds, targets)
+                    if counts is not None:
+                        loss = loss * (i.shape[0] / counts[j])
+                    loss.backward()
+                all_reduce(self._fgrad)
+                prl_native.flat_adamw(fa.flat, fa.m, fa.v, fa.step, self._fgrad, group["lr"], beta1,
+                                      beta2, group["eps"], group["weight_decay"], float("inf"),
+                                      fa.total_norm)
+            fa.sync()
+            self.pred_net.eval()
+            return
         params = list(self.pred_net.parameters())
         for j in range(steps):
             self.optimizer.zero_grad()
