@@ -196,6 +196,14 @@ class RND(nn.Module):
         fa = self._flat_state()
         mb = max(v.shape[0] for v in values)
         D = values[0].shape[1]
+        # the captured AdamW launch holds the hyper-parameters as constants: a changed lr / betas /
+        # eps / weight decay (a scheduler, a user edit of param_groups) re-captures
+        group = self.optimizer.param_groups[0]
+        hyper = (float(group["lr"]), tuple(float(b) for b in group["betas"]), float(group["eps"]),
+                 float(group["weight_decay"]))
+        if getattr(self, "_graph_hyper", None) != hyper:
+            self._graph = None
+            self._graph_hyper = hyper
         for v in values:
             v = v.contiguous()
             rows = v.shape[0]

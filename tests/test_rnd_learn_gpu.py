@@ -220,3 +220,29 @@ def test_update_pred_graphed_equals_eager(monkeypatch):
     r_a = a.compute_intrinsic_reward(X[:4096])
     r_b = b.compute_intrinsic_reward(X[:4096])
     assert float((r_a - r_b).abs().max()) <= 1e-4 * float(r_b.abs().max())
+
+
+def test_update_pred_graph_follows_lr_change():
+    """The graphed update captures AdamW's hyper-parameters as launch constants; a changed lr
+    between update_pred calls must re-capture (against the PyTorch loop with the same change)."""
+    import copy
+    from PPO import RND
+    torch.manual_seed(4)
+    D = 64
+    a = RND(D, D)
+    b = copy.deepcopy(a)
+    b.optimizer = torch.optim.AdamW(params=b.pred_net.parameters(), lr=0.001)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    for lr in (1e-3, 5e-3):
+        for r in (a, b):
+            r.optimizer.param_groups[0]["lr"] = lr
+        X = torch.randn(3 * 2048, D, device="cuda", generator=g)
+        a.update_pred(list(X.split(2048)))
+        os.environ["PRL_RND_GRAPH"] = "0"
+        try:
+            b.update_pred(list(X.split(2048)))
+        finally:
+            del os.environ["PRL_RND_GRAPH"]
+    torch.cuda.synchronize()
+    for (k, va), vb in zip(a.pred_net.state_dict().items(), b.pred_net.state_dict().values()):
+        assert float((va - vb).abs().max()) <= 1e-6, (k, float((va - vb).abs().max()))
