@@ -307,8 +307,9 @@ def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
         fpr = 2 * (trunk + heads + outs) * 2 + 2 * (heads + outs)
         rows = min(gu.mb, int(gu.sources[0].shape[0]))
         ach = fpr * rows / (cold_med * 1e-3) / 1e12
-        roofline = {"kernel": "prl_ppo_wide_grad: ppo_wide_grad_kernel + ppo_wide_reduce_kernel "
-                              "(one optimizer step's forward + loss + backward, wide nets)",
+        roofline = {"kernel": "prl_ppo_wide_grad: ppo_wide_grad_kernel + ppo_wide_dw0_kernel (dW0 "
+                              "beside the partials' fold) + ppo_wide_reduce_kernel (dW0's fold): one "
+                              "optimizer step's forward + loss + backward, wide nets",
                     "bound": "mfma", "achieved": round(ach, 3), "peak": F32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(ach / F32_PEAK_TFLOPS, 5), "traffic": None,
                     "limiter": "one wave per SIMD (256 + 256 registers, no spills) and the LDS "
