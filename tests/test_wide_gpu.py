@@ -465,8 +465,8 @@ def test_wide_learn_native_adam_equals_torch_adam(monkeypatch):
     assert float((v1 - v0).abs().max()) <= 1e-3 * (1 + float(v0.abs().max()))
 
 
-@pytest.mark.parametrize("E,stride", [(300, 7), (5000, 211)])
-def test_persistent_wide_rollout_matches_per_step_rollout(monkeypatch, E, stride):
+@pytest.mark.parametrize("E,stride,team", [(300, 7, "1"), (5000, 211, "1"), (300, 7, "8"), (300, 7, "0")])
+def test_persistent_wide_rollout_matches_per_step_rollout(monkeypatch, E, stride, team):
     """prl_wide_rollout (the whole C5 rollout in ONE launch, each wave stepping 16 envs to the end
     of their episodes) against the per-step path (prl_ppo_wide_dist + prl_rollout_step per vector
     step, PRL_WIDE_ROLLOUT=0, eager) on the same runner seeds and policy, three rollouts with a
@@ -476,7 +476,9 @@ def test_persistent_wide_rollout_matches_per_step_rollout(monkeypatch, E, stride
     actions are also checked against a float64 forward of policy_old with the same Philox
     normals (oracle.sample_normal): tanh(mu + std z) to 2e-5.  E = 300: 19 workgroups of 16 envs,
     the last one ragged; E = 5000: 256 workgroups of 20 envs each, so every workgroup refills
-    its lanes from its queue as episodes end (the team form's env queue)."""
+    its lanes from its queue as episodes end (the team form's env queue).  team: the launch's
+    form (PRL_WIDE_ROLLOUT_TEAM: 1 four waves per tile, the default; 8 eight; 0 one wave per tile)."""
+    monkeypatch.setenv("PRL_WIDE_ROLLOUT_TEAM", team)
     import oracle as O
     from AsyncTools.AsyncPPO import AsyncPPO
     from PPO import PPO
