@@ -435,7 +435,9 @@ __device__ inline void upd_row_dist(const UpdNet& n, const OT& O, const float* a
 // Per-row loss (surrogate, prl_loss.hip semantics) and the gradient w.r.t. the head outputs
 // dO[0 .. nout) (dO[nout .. 16) = 0).  lp = {-min(s1, s2), SmoothL1, H}.  O / dO: LDS rows (the
 // runtime-layout kernel) or register arrays (the specialised kernels: indices fold to constants).
-template <int KD, int KA, class OT, class DT>
+// PART 1: the critic's dO and lp[1] only; 2: the actor's dO, lp[0] and lp[2] only (the same
+// arithmetic for what is computed; the rest stays 0).
+template <int KD, int KA, int PART = 0, class OT, class DT>
 __device__ inline void upd_row_loss(const UpdNet& n, const OT& O, const float* rin, float invB,
                                     float clip, float vf_coef, DT& dO, float (&lp)[3]) {
   const int A = KA > 0 ? KA : n.A;
@@ -443,12 +445,21 @@ __device__ inline void upd_row_loss(const UpdNet& n, const OT& O, const float* r
   const int vcol = discrete ? A : 2 * A;      // critic output column
 #pragma unroll
   for (int j = 0; j < UPD_MAXO; ++j) dO[j] = 0.f;
+  if constexpr (PART != 2) {
+    const float V = O[vcol];
+    const float x = V - rin[10];
+    const float ax = fabsf(x);
+    const float sl = ax < 1.0f ? 0.5f * ax * ax : ax - 0.5f;
+    const float gx = ax < 1.0f ? x : (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f));
+    dO[vcol] = vf_coef * invB * gx;
+    lp[1] = sl;
+  }
+  if constexpr (PART == 1) return;
   UpdDist dist;
   upd_row_dist<KD, KA, OT>(n, O, rin, dist);
   const float logp = dist.logp, H = dist.H, S2 = dist.S2, qa = dist.qa;
   const int ai = dist.ai;
   const float* p = dist.p;
-  const float V = O[vcol];
   // surrogate
   const float diff = logp - rin[8];
   const float cl = diff < -20.0f ? -20.0f : (diff > 20.0f ? 20.0f : diff);
@@ -466,13 +477,7 @@ __device__ inline void upd_row_loss(const UpdNet& n, const OT& O, const float* r
   const float in_clip = (ratio >= lo && ratio <= hi) ? 1.0f : 0.0f;
   const float in_20 = (diff >= -20.0f && diff <= 20.0f) ? 1.0f : 0.0f;
   const float dlogp = -invB * (w1 * adv + w2 * adv * in_clip) * ratio * in_20;
-  const float x = V - rin[10];
-  const float ax = fabsf(x);
-  const float sl = ax < 1.0f ? 0.5f * ax * ax : ax - 0.5f;
-  const float gx = ax < 1.0f ? x : (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f));
-  dO[vcol] = vf_coef * invB * gx;
   lp[0] = -m;
-  lp[1] = sl;
   lp[2] = H;
   // d logp / d head outputs
   if (discrete) {
@@ -847,17 +852,30 @@ __device__ inline void upd_tile_outputs_reg(const UpdNet& n, const float* W, con
 }
 // The row's loss into its dO row of LDS (only the first nout entries are ever read: dW2, dG and
 // the output biases index outputs < nout), 16-B stores; rows past rc get zeros.
+// The 8-wave two-head kernels (CartPole; upd_loss_split) compute per head group only what the
+// group's head reads: group 0 the actor's dO (the ratio / clip / entropy chain), group 1 the
+// critic's — the two waves of a SIMD no longer both issue the whole chain.  Group 0 also leaves
+// its lp[0], lp[2] at columns 12, 13 of its dO rows for wave NW - 1's loss sums.
+template <int NW, int KD, int KA>
+constexpr bool upd_loss_split() { return NW == 8 && KA > 0 && KD >= 0 && upd_kd_discrete(KD); }
 template <int NW, int KD, int KA>
 __device__ inline void upd_tile_loss(const UpdNet& n, const float* W, const UpdScr& sc, int rc,
                                      float invB, const UpdArgs& args, float (&lp)[3]) {
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   float* dOrow = sc.dOs + (w * 16 + x) * 16;
   if constexpr (KA > 0) {
+    constexpr bool SPLIT = upd_loss_split<NW, KD, KA>();
+    static_assert(!SPLIT || KA + 1 <= 12, "the split loss keeps columns 12, 13 of a dO row free");
     float O[UPD_MAXO], dO[UPD_MAXO];
     upd_tile_outputs_reg<NW>(n, W, sc, O);
     if (q == 0) {
       if (x < rc) {
-        upd_row_loss<KD, KA>(n, O, sc.Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dO, lp);
+        if (SPLIT && (w >> 2) == 1)
+          upd_row_loss<KD, KA, 1>(n, O, sc.Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dO, lp);
+        else if (SPLIT)
+          upd_row_loss<KD, KA, 2>(n, O, sc.Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dO, lp);
+        else
+          upd_row_loss<KD, KA>(n, O, sc.Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dO, lp);
       } else {
 #pragma unroll
         for (int j = 0; j < UPD_MAXO; ++j) dO[j] = 0.f;
@@ -865,6 +883,7 @@ __device__ inline void upd_tile_loss(const UpdNet& n, const float* W, const UpdS
 #pragma unroll
       for (int j4 = 0; j4 < 4; ++j4)
         if (4 * j4 < n.nout) upd_st4(dOrow + 4 * j4, upd_v4{dO[4 * j4], dO[4 * j4 + 1], dO[4 * j4 + 2], dO[4 * j4 + 3]});
+      if (SPLIT && (w >> 2) == 0) upd_st4(dOrow + 12, upd_v4{lp[0], lp[2], 0.f, 0.f});
     }
   } else {
     const float* Orow = upd_tile_outputs<NW>(n, W, sc);
@@ -1161,15 +1180,24 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
       }
     }
   }
-  // ---- output biases and loss partials (one wave: the last one)
+  // ---- output biases and loss partials (one wave: the last one).  Split loss: the actor's
+  //      columns and lp[0], lp[2] come from wave 3's dO rows (written before barrier #2; wave 3
+  //      rewrites them only after the next tile's barrier #1)
   if (w == NW - 1) {
+    constexpr bool SPLIT = upd_loss_split<NW, KD, KA>();
     const int tl_ = l;
     if (tl_ < n.nout) {   // f64 sum: the softmax outputs' dO cancel across rows
+      const float* dOb = (SPLIT && tl_ < n.out[0]) ? sc.dOs + 3 * 16 * 16 : dOw;
       double acc = 0.0;
 #pragma unroll
-      for (int r = 0; r < UPD_RT; ++r) acc += (double)dOw[r * 16 + tl_];
+      for (int r = 0; r < UPD_RT; ++r) acc += (double)dOb[r * 16 + tl_];
       if constexpr (RG) gr.bias += (float)acc;
       else upd_gadd(Ga + upd_bias_of(n, tl_), (float)acc, first);
+    }
+    if constexpr (SPLIT) {
+      const float* a = sc.dOs + (3 * 16 + x) * 16 + 12;
+      lp[0] = q == 0 ? a[0] : 0.f;
+      lp[2] = q == 0 ? a[1] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
