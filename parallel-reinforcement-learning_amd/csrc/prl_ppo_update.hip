@@ -858,6 +858,12 @@ __device__ inline void upd_tile_outputs_reg(const UpdNet& n, const float* W, con
 // its lp[0], lp[2] at columns 12, 13 of its dO rows for wave NW - 1's loss sums.
 template <int NW, int KD, int KA>
 constexpr bool upd_loss_split() { return NW == 8 && KA > 0 && KD >= 0 && upd_kd_discrete(KD); }
+// The 8-wave three-head kernels (Pendulum): both groups need the dlogp chain (group 1 runs the
+// log-std head), so group 0 alone runs the whole loss and group 1 reads group 0's dO rows
+// (wave w & 3's) behind one workgroup barrier instead of issuing the same chain beside it;
+// lp[0..2] ride in columns 12-14 of those rows for wave NW - 1's loss sums.
+template <int NW, int KD, int KA>
+constexpr bool upd_loss_handoff() { return NW == 8 && KA > 0 && KD >= 0 && !upd_kd_discrete(KD); }
 template <int NW, int KD, int KA>
 __device__ inline void upd_tile_loss(const UpdNet& n, const float* W, const UpdScr& sc, int rc,
                                      float invB, const UpdArgs& args, float (&lp)[3]) {
@@ -865,7 +871,10 @@ __device__ inline void upd_tile_loss(const UpdNet& n, const float* W, const UpdS
   float* dOrow = sc.dOs + (w * 16 + x) * 16;
   if constexpr (KA > 0) {
     constexpr bool SPLIT = upd_loss_split<NW, KD, KA>();
+    constexpr bool HANDOFF = upd_loss_handoff<NW, KD, KA>();
     static_assert(!SPLIT || KA + 1 <= 12, "the split loss keeps columns 12, 13 of a dO row free");
+    static_assert(!HANDOFF || 2 * KA + 1 <= 12, "the loss hand-off keeps columns 12-14 of a dO row free");
+    if (HANDOFF && (w >> 2) == 1) return;
     float O[UPD_MAXO], dO[UPD_MAXO];
     upd_tile_outputs_reg<NW>(n, W, sc, O);
     if (q == 0) {
@@ -884,6 +893,7 @@ __device__ inline void upd_tile_loss(const UpdNet& n, const float* W, const UpdS
       for (int j4 = 0; j4 < 4; ++j4)
         if (4 * j4 < n.nout) upd_st4(dOrow + 4 * j4, upd_v4{dO[4 * j4], dO[4 * j4 + 1], dO[4 * j4 + 2], dO[4 * j4 + 3]});
       if (SPLIT && (w >> 2) == 0) upd_st4(dOrow + 12, upd_v4{lp[0], lp[2], 0.f, 0.f});
+      if (HANDOFF) upd_st4(dOrow + 12, upd_v4{lp[0], lp[1], lp[2], 0.f});
     }
   } else {
     const float* Orow = upd_tile_outputs<NW>(n, W, sc);
@@ -999,10 +1009,12 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
   __syncthreads();   // #1: Op, Rin
   UPD_CMARK(1)
   // ---- loss of row x (lanes q == 0 of every wave, redundantly: each wave needs dO)
-  const float* dOw = sc.dOs + w * 16 * 16;   // [row][j] of this wave
+  constexpr bool HANDOFF = upd_loss_handoff<NW, KD, KA>();
+  const float* dOw = sc.dOs + (HANDOFF ? (w & 3) : w) * 16 * 16;   // [row][j] of this wave (hand-off: its group-0 partner's)
   float lp[3] = {0.f, 0.f, 0.f};
   upd_tile_loss<NW, KD, KA>(n, W, sc, rc, invB, args, lp);
-  upd_wave_sync();
+  if constexpr (HANDOFF) __syncthreads();
+  else upd_wave_sync();
   UPD_CMARK(2)
   // this wave's [16 rows][16 ch] transpose slots (upd_ts): with one per head, every head stores
   // its G first, then ONE wave sync, so the heads' backward chains below are independent and
@@ -1198,6 +1210,12 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
       const float* a = sc.dOs + (3 * 16 + x) * 16 + 12;
       lp[0] = q == 0 ? a[0] : 0.f;
       lp[2] = q == 0 ? a[1] : 0.f;
+    }
+    if constexpr (HANDOFF) {
+      const float* a = sc.dOs + (3 * 16 + x) * 16 + 12;
+      lp[0] = q == 0 ? a[0] : 0.f;
+      lp[1] = q == 0 ? a[1] : 0.f;
+      lp[2] = q == 0 ? a[2] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
