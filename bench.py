@@ -535,7 +535,10 @@ def main():
             "config": {"workload": workload(args.config, cfg),
                        "env": cfg["env"], "num_envs_per_gpu": cfg["num_envs"],
                        "global_num_envs": cfg["num_envs"] * world,
-                       "mini_batch_size": cfg["mb"], "k_epochs": cfg["k_epochs"],
+                       "mini_batch_size": cfg["mb"],
+                       # union-minibatch rule: optimizer step j uses every rank's
+                       # j-th mini_batch_size rows, so the global minibatch is world x that
+                       "global_mini_batch": cfg["mb"] * world, "k_epochs": cfg["k_epochs"],
                        "parallelism": f"dp{world}"},
         }
         if res["n1_same_run"] is not None:

@@ -127,7 +127,10 @@ class RND(nn.Module):
         from .update import FlatAdamState
         params = list(self.pred_net.parameters())
         fa = getattr(self, "_fa", None)
-        if fa is None or len(fa.params) != len(params) or any(a is not b for a, b in zip(fa.params, params)):
+        # rebuilt when the parameters OR the optimizer object were replaced: the flat state holds
+        # the optimizer it was built for, and a new one must get its moments / step count
+        if (fa is None or fa.ppo.optimizer is not self.optimizer or len(fa.params) != len(params)
+                or any(a is not b for a, b in zip(fa.params, params))):
             fa = self._fa = FlatAdamState(SimpleNamespace(policy=self.pred_net, optimizer=self.optimizer))
             self._fgrad = torch.zeros_like(fa.flat)
             self._graph = None
@@ -161,25 +164,32 @@ class RND(nn.Module):
         prl_native.flat_adamw(fa.flat, fa.m, fa.v, fa.step, self._fgrad, group["lr"], beta1, beta2,
                               group["eps"], group["weight_decay"], float("inf"), fa.total_norm)
 
-    def _flat_dp_ok(self, values) -> bool:
+    def _flat_optimizer_ok(self) -> bool:
+        """The native flat AdamW stands in for self.optimizer / self.loss_fn only when they are
+        exactly what it computes: one-group torch AdamW (no amsgrad / maximize), f32 parameters
+        on the GPU, and the reference's nn.MSELoss(reduction='mean') (RND.py:45)."""
         w = self.pred_net[0].weight
         if not (w.is_cuda and w.dtype == torch.float32) or type(self.optimizer) is not optim.AdamW:
             return False
-        if len(self.optimizer.param_groups) != 1 or self.optimizer.param_groups[0].get("amsgrad"):
+        if len(self.optimizer.param_groups) != 1:
             return False
-        if not (isinstance(self.loss_fn, nn.MSELoss) and self.loss_fn.reduction == "mean"):
+        group = self.optimizer.param_groups[0]
+        if group.get("amsgrad") or group.get("maximize"):
             return False
-        return all(v.is_cuda and v.dtype == torch.float32 and v.dim() == 2 for v in values)
+        return isinstance(self.loss_fn, nn.MSELoss) and self.loss_fn.reduction == "mean"
+
+    def _flat_dp_ok(self) -> bool:
+        # rank-invariant inputs only (optimizer, loss_fn, parameter device / dtype): the flat and
+        # the per-parameter loops issue different numbers of collectives per step, so every rank
+        # must take the same one whatever its own minibatches look like
+        return self._flat_optimizer_ok()
 
     def _graphed_ok(self, values, all_reduce, counts) -> bool:
         if all_reduce is not None or counts is not None or os.environ.get("PRL_RND_GRAPH", "1") == "0":
             return False
         if not values or not torch.cuda.is_available():
             return False
-        w = self.pred_net[0].weight
-        if not (w.is_cuda and w.dtype == torch.float32) or type(self.optimizer) is not optim.AdamW:
-            return False
-        if len(self.optimizer.param_groups) != 1 or self.optimizer.param_groups[0].get("amsgrad"):
+        if not self._flat_optimizer_ok():
             return False
         return all(v.is_cuda and v.dtype == torch.float32 and v.dim() == 2 for v in values)
 
@@ -249,7 +259,7 @@ class RND(nn.Module):
             self.pred_net.eval()
             return
         steps = len(values) if counts is None else len(counts)
-        if all_reduce is not None and self._flat_dp_ok(values):
+        if all_reduce is not None and self._flat_dp_ok():
             # data-parallel ranks on the GPU: the gradient is ONE flat buffer (the parameters'
             # .grad are views of it), so each step is one all-reduce instead of one per parameter
             # tensor, and AdamW is the native flat launch pair (max_norm = inf: no clipping)

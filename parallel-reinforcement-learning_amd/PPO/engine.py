@@ -56,7 +56,9 @@ class FusedUpdate:
     def _bind(self):
         """Alias parameters and optimizer state onto the flat buffers (copies current values)."""
         opt = self.ppo.optimizer
+        self._opt = opt   # the optimizer these moments belong to (a replaced one re-binds)
         with torch.no_grad():
+            self.step.zero_()
             for p, fv, mv, vv in zip(self.params, self._views(self.flat), self._views(self.m),
                                      self._views(self.v)):
                 fv.copy_(p.data)
@@ -67,10 +69,16 @@ class FusedUpdate:
                     vv.copy_(st["exp_avg_sq"])
                     self.step.copy_(torch.as_tensor(st["step"], dtype=torch.float32).reshape(1))
                     st["exp_avg"], st["exp_avg_sq"] = mv, vv
+                else:   # torch's AdamW starts a parameter without state from zero moments
+                    mv.zero_()
+                    vv.zero_()
         self._opt_views = (self._views(self.m), self._views(self.v))
 
     def bound(self) -> bool:
-        """True while the policy parameters still live in the flat buffer."""
+        """True while the policy parameters still live in the flat buffer and the optimizer is
+        the one the moments were taken from."""
+        if self.ppo.optimizer is not self._opt:
+            return False
         return all(p.data.data_ptr() == fv.data_ptr()
                    for p, fv in zip(self.params, self._views(self.flat)))
 

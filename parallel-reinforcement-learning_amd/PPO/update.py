@@ -67,6 +67,7 @@ class FlatAdamState:
 
     def _bind(self):
         opt = self.ppo.optimizer
+        self._opt = opt   # the optimizer these moments belong to (a replaced one re-binds)
         self.step.zero_()
         with torch.no_grad():
             for p, fv, mv, vv in zip(self.params, self._views(self.flat), self._views(self.m),
@@ -85,6 +86,8 @@ class FlatAdamState:
 
     def bound(self) -> bool:
         opt = self.ppo.optimizer
+        if opt is not self._opt:
+            return False
         for p, fv, mv in zip(self.params, self._views(self.flat), self._views(self.m)):
             if p.data.data_ptr() != fv.data_ptr():
                 return False
@@ -124,8 +127,17 @@ class FlatAdamState:
                               else torch.tensor(float(self.step.item())))
 
 
+def flat_adam_ok(optimizer) -> bool:
+    """prl_flat_adamw computes one-group torch AdamW without amsgrad / maximize: anything else
+    (another optimizer type, extra groups) keeps torch's clip_grad_norm_ + optimizer.step()."""
+    if type(optimizer) is not torch.optim.AdamW or len(optimizer.param_groups) != 1:
+        return False
+    group = optimizer.param_groups[0]
+    return not (group.get("amsgrad") or group.get("maximize"))
+
+
 def flat_adam_state(ppo):
-    """ppo's FlatAdamState (built once per policy), re-armed for this learn()."""
+    """ppo's FlatAdamState (built once per policy and optimizer), re-armed for this learn()."""
     fa = getattr(ppo, "_flat_adam", None)
     params = list(ppo.policy.parameters())
     if fa is None or len(fa.params) != len(params) or any(a is not b for a, b in zip(fa.params, params)):
@@ -182,7 +194,7 @@ class GraphedUpdate:
             # parameters / gradient / AdamW state as flat vectors: the kernel reads the
             # parameters in place and clip_grad_norm_ + AdamW are one launch (prl_flat_adamw);
             # PRL_WIDE_ADAM=0 keeps torch's clip_grad_norm_ + fused AdamW
-            if os.environ.get("PRL_WIDE_ADAM", "1") != "0":
+            if os.environ.get("PRL_WIDE_ADAM", "1") != "0" and flat_adam_ok(ppo.optimizer):
                 self.fa = flat_adam_state(ppo)
             else:
                 self.pflat = torch.empty(info[0], dtype=torch.float32, device=dev)

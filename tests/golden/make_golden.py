@@ -433,6 +433,11 @@ def main():
                                                  tag="learn_cont_mb65536", N=2 * 65536 + 9000,
                                                  mb=65536, k_epochs=2, store_inputs=False,
                                                  light=True),
+        # C1 at its own hyper-parameters (README.md:35-49: batch 1,024, mini_batch 512,
+        # k_epochs 11): a CartPole memory of N = 1,500 (two full minibatches and a ragged third),
+        # 33 optimizer steps through the latency form of the engine
+        "learn_c1": lambda: make_learn(torch, ppo_pkg, continuous=False, tag="learn_c1", N=1500,
+                                       mb=512, k_epochs=11, light=True),
         "rnd": lambda: make_rnd(torch, ppo_pkg),
         "worker": lambda: make_worker(apo, utils, ppo_pkg),
         "envs": lambda: make_envs(apo),

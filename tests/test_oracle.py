@@ -27,7 +27,8 @@ def test_gae_python_restatement_matches_c(golden):
 
 
 # ---------------------------------------------------------------------------------- learn
-@pytest.mark.parametrize("tag", ["learn", "learn_cont", "learn_rnd", "learn_rnd_c5", "learn_rnd_big"])
+@pytest.mark.parametrize("tag", ["learn", "learn_cont", "learn_rnd", "learn_rnd_c5", "learn_rnd_big",
+                                 "learn_c1"])
 def test_learn_gae_and_advantages(golden, tag):
     """GAE returns and ret - V bit-exact (with use_RND the rewards are R + r_int, PPO.py:171);
     normalised advantages within north_star's 1e-5 relative, with a 1e-6 absolute guard (in

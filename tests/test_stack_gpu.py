@@ -216,6 +216,42 @@ def test_learn_on_gpu_matches_reference_learn(golden, path):
                                        err_msg=f"{tag}:{k}")
 
 
+def test_learn_c1_hyperparameters_match_reference_learn(golden):
+    """C1 at its own hyper-parameters (README.md:35-49; BASELINE configs[0]): batch 1,024,
+    mini_batch 512, k_epochs 11 — 33 sequential optimizer steps over a 1,500-row CartPole memory
+    (two full minibatches and a ragged third) through the fused engine's latency form, against
+    the reference's own learn() (tests/golden/learn_c1.npz, make_golden.py), at the CartPole
+    2e-6 bound of test_learn_on_gpu_matches_reference_learn."""
+    import prl_native
+    from PPO import PPO
+    g = golden("learn_c1")
+    assert (int(g["mb"]), int(g["k_epochs"]), int(g["N"])) == (512, 11, 1500)
+    torch.manual_seed(0)
+    p = PPO(is_continuous=False, observ_dim=4, action_dim=2, lr=1e-3, k_epochs=11,
+            policy_clip=0.2, GAE_lambda=0.95, gamma=0.995, batch_size=1024, mini_batch_size=512)
+    p.show_progress = False
+    init = {k[len("init/"):]: torch.from_numpy(g[k]) for k in g.files if k.startswith("init/")}
+    for k, v in p.policy.state_dict().items():
+        np.testing.assert_array_equal(v.cpu().numpy(), init[k].numpy(), err_msg=k)
+    for i in range(int(g["N"])):
+        p.memory.push(g["S"][i], np.asarray(g["A"][i]), g["R"][i], g["Dn"][i])
+    p.learn()
+    torch.cuda.synchronize()
+    assert p.last_update_path == "fused"
+    plan = prl_native.ppo_update_last_plan()
+    assert plan["form"] == "latency" and plan["specialised"], plan
+    _, _, _, adv, returns = p._last_update_inputs
+    ret_ref = g["returns"].astype(np.float64)
+    assert np.all(np.abs(returns.cpu().double().numpy() - ret_ref) <= 1e-5 * np.abs(ret_ref) + 1e-5)
+    sd = p.policy.state_dict()
+    worst = max(float(np.abs(sd[k].cpu().numpy() - g["final/" + k]).max()) for k in sd)
+    moved = max(float(np.abs(g["final/" + k] - init[k].numpy()).max()) for k in sd)
+    print(f"learn_c1: max |w - w_ref| {worst:.3e} (33 steps moved weights by up to {moved:.3e})")
+    for k in sd:
+        np.testing.assert_allclose(sd[k].cpu().numpy(), g["final/" + k], rtol=0, atol=2e-6,
+                                   err_msg=f"learn_c1:{k}")
+
+
 def test_compute_gae_api_returns_reference_list(golden):
     from PPO import PPO
     g = golden("gae")
