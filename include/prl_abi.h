@@ -126,8 +126,22 @@ int prl_rollout_step_at(int kind, int64_t E, int64_t* step_dev, double* phys,
  * prl_rollout_step samples it, the trajectory rows, t_elapsed / ep_len / terminal and the counters
  * written as the per-step kernels write them (active_after[t] += envs still active after step t,
  * reward_sum[0] += rewards).  Each wave owns 16 envs and keeps the actor in LDS.  Supported:
- * prl_wide_rollout_supported() (the synthetic env with its D = 348 / A = 17 continuous net). */
+ * prl_wide_rollout_supported() (the synthetic env with its D = 348 / A = 17 continuous net;
+ * CartPole with the D = 4 / A = 2 discrete net, run by prl_cartpole_rollout below). */
 int prl_wide_rollout_supported(int kind, int32_t D, int32_t A, int32_t discrete);
+/* The whole CartPole rollout of the discrete actor (ActorCritic, D 4, A 2: policy_old's flat
+ * parameters in torch parameters() order, the actor's 4,738 used) as ONE launch, one thread
+ * per env: forward, Categorical sampling (the fused step kernel's Philox stream), the float64
+ * step, trajectory push and mask, every non-terminal env to the end of its episode.  Replaces
+ * AsyncPPO.worker's loop (AsyncTools/AsyncPPO.py:117-146) with PPO.get_action (PPO/PPO.py:81-96)
+ * and EnvVectorizer.step (AsyncPPO.py:64-102).  probs_out: null, or [t_max][E][2] f32 receiving
+ * the probabilities each step sampled from (tests).  prl_wide_rollout dispatches here for
+ * PRL_ENV_CARTPOLE. */
+int prl_cartpole_rollout(const float* params, int64_t E, double* phys, int32_t* t_elapsed,
+                         uint8_t* terminal, uint64_t sample_seed, int32_t t_max, float* traj_obs,
+                         float* traj_act, float* traj_rew, uint8_t* traj_done, int32_t* ep_len,
+                         int32_t* active_after, double* reward_sum, float* probs_out,
+                         void* stream);
 int prl_wide_rollout(int kind, const float* params, int32_t D, int32_t A, int32_t discrete,
                      int64_t E, double* phys, int32_t* t_elapsed, uint8_t* terminal,
                      float action_scaling, uint64_t sample_seed, int32_t t_max, float* traj_obs,
@@ -442,6 +456,11 @@ int32_t prl_ppo_update_set_tp(int32_t mode);
  * Per process (initial value from PRL_UPD_REPL); returns the previous value.  No reference
  * counterpart (performance knob / tests). */
 int32_t prl_ppo_update_set_repl(int32_t replicas);
+/* The head-split latency form (csrc/prl_ppo_split.h: the actor and the critic head of a 16-row
+ * tile on two workgroups) for the two-head CartPole shape: 1 = on (default, PRL_UPD_SPLIT), 0 =
+ * the 8-wave kernel.  Per process; returns the previous value.  No reference counterpart
+ * (performance knob / tests). */
+int32_t prl_ppo_update_set_split(int32_t mode);
 /* Test utility: fill every CU's LDS with `value` (LDS is not cleared between launches; a kernel
  * that reads LDS it did not write in its own launch sees the previous launch's contents).  No
  * reference counterpart. */
@@ -451,9 +470,10 @@ int prl_debug_fill_lds(float value, void* stream);
  * out[2] = workgroups; out[3] = 16-row tiles per workgroup and step (ceil of rows / 16 / G);
  * out[4] = 1 for a compile-time-layout (CartPole / Pendulum) kernel, 0 for the runtime layout;
  * out[5] = workgroups per tile group (the latency form's replicated tiles, PRL_UPD_REPL; out[2]
- * counts them all).  All -1 before the first launch.  No reference counterpart (tests assert
- * which kernel ran). */
-void prl_ppo_update_last_plan(int32_t out[6]);
+ * counts them all; the split form: its two head roles); out[6] = 1 for the head-split latency
+ * form.  All -1 before the first launch.  No reference counterpart (tests assert which kernel
+ * ran). */
+void prl_ppo_update_last_plan(int32_t out[7]);
 /* A zeroed slice buffer of its own (shareable by IPC handle).  *kind in: 0 = uncached, falling
  * back to fine-grained memory, 1 = uncached only, 2 = fine-grained only; out: 1 = uncached,
  * 2 = fine-grained (what the buffer is; prl_ppo_update_dpx's fine_grained follows it). */

@@ -220,10 +220,22 @@ class PPO:
         self._dist_flat(obs)
 
     def rollout_params(self, obs: torch.Tensor):
-        """policy_old's parameters as one flat vector for AsyncPPO's persistent wide-net rollout
-        (prl_wide_rollout), gathered now; None when the native distribution path does not apply
-        (same rule as dist_params_at)."""
+        """policy_old's parameters as one flat vector for AsyncPPO's persistent rollouts
+        (prl_wide_rollout: the wide continuous nets, same rule as dist_params_at; and the CartPole
+        net, prl_cartpole_rollout), gathered now; None when neither applies (PRL_CP_ROLLOUT=0
+        keeps CartPole on the per-step path)."""
         with torch.no_grad():
+            if (not self.is_continuous and self.observ_dim == 4 and self.action_dim == 2
+                    and obs.is_cuda and os.environ.get("PRL_CP_ROLLOUT", "1") != "0"
+                    and type(self.policy_old).dist_params is ActorCritic.dist_params):
+                params = [p.detach().reshape(-1) for p in self.policy_old.parameters()]
+                if sum(p.numel() for p in params) != 9027 or params[0].dtype != torch.float32:
+                    return None
+                flat = getattr(self, "_cp_flat", None)
+                if flat is None or flat.device != params[0].device:
+                    flat = self._cp_flat = torch.empty(9027, dtype=torch.float32, device=params[0].device)
+                torch.cat(params, out=flat)
+                return flat
             return self._dist_flat(obs)
 
     def _dist_flat(self, obs, gather: bool = True):

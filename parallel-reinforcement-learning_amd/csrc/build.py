@@ -20,7 +20,7 @@ PKG = os.path.dirname(HERE)
 SOURCES = ["prl_abi.hip", "prl_envs.hip", "prl_buffers.hip", "prl_gae.hip", "prl_loss.hip",
            "prl_rnd.hip", "prl_gn.hip",
            "prl_update.hip", "prl_ppo_update.hip", "prl_ppo_wide.hip", "prl_wide_rollout.hip"]
-HEADERS = ["prl_common.h", "prl_envs.h", os.path.join("..", "..", "include", "prl_abi.h")]
+HEADERS = ["prl_common.h", "prl_envs.h", "prl_ppo_split.h", os.path.join("..", "..", "include", "prl_abi.h")]
 LIB = os.path.join(PKG, "libprl_hip.so")
 OBJDIR = os.path.join(HERE, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -1,0 +1,615 @@
+// prl_ppo_split.h — the HEAD-SPLIT latency form of the persistent update engine (included by
+// prl_ppo_update.hip inside namespace prl, after the engine's helpers; PPO/PPO.py:216-255).
+//
+// The two-head (discrete) nets — CartPole, the headline's C2 at the reference's mini_batch 512 —
+// have an actor head and a critic head that share only the trunk:
+//     logp  = actor(trunk(x)),  V = critic(trunk(x)),  loss = surrogate(logp) + 0.5 SmoothL1(V)
+// so the actor's loss gradient never needs the critic's outputs and vice versa, and the trunk's
+// gradient is the SUM of what each head sends back through it (GroupNorm's backward is linear in
+// the incoming gradient for fixed forward statistics).  This form gives each head its own
+// workgroup: a tile group of 16 rows is two workgroups on two CUs, role 0 (trunk + actor head)
+// and role 1 (trunk + critic head), each 4 waves = one wave per SIMD, wave w = channel block w.
+// Against the 8-wave kernel (both heads on one CU, two waves per SIMD sharing the matrix pipe
+// and the VALU issue slots), a SIMD issues one head's MFMAs and GroupNorm / loss VALU instead
+// of two, and each workgroup's AdamW updates only the parameters its tile reads (trunk + own
+// head: ~53 % of the image) — the other head's image entries go stale in its LDS, unread.
+//
+// The step:
+//   phase A  role r runs its 16-row tile (3 workgroup barriers) into an LDS gradient image and
+//            publishes its head's quads into part[gt] and its trunk quads (+ its loss-partial
+//            quad) into part[gt] (role 0) or part2[gt] (role 1) — sc1 16-B stores, drained;
+//            arrival on counter A (G = 2 Gt workgroups);
+//   phase B  slice owner g (of G) sums its quads over the Gt partials of part, and for the trunk
+//            and loss quads also over the Gt of part2, in a fixed order with float64
+//            accumulators; publishes the slice (sc1), counter B;
+//   phase C  every workgroup loads the whole reduced gradient and forms clip_grad_norm_'s norm
+//            in ONE canonical order (thread t: quads t + 256 i; the same DPP tree; waves in
+//            order) — the same bits on both roles, so the trunk copies the two roles update stay
+//            bit-identical — then AdamW on its owned quads only.
+// Hand-offs are the engine's (Guideline 16 first row: sc1 payload, drained, one arriving lane
+// behind a barrier, sc1 polls; sharded counters).  The trunk gradient is summed in another
+// order than the 8-wave kernel's (per head, then across heads in float64), so the two forms
+// agree to float32 rounding, not bit for bit (tests/test_engine_gpu.py::test_split_*).
+
+constexpr int SPL_NW = 4, SPL_NT = 64 * SPL_NW;
+
+// one 16-row tile of role r = head h (h = r): forward (trunk + head h), the head's loss, its
+// backward through the trunk; the gradient into the LDS image Ga (first tile of the step: every
+// entry the role publishes is stored, never accumulated, since a split workgroup runs ONE tile
+// per step).  Three workgroup barriers.
+template <int KA>
+__device__ __forceinline__ void spl_tile(const UpdNet& n, const UpdArgs& args, int h, const float* W,
+                                         float* Ga, const UpdScr& sc, const UpdIn<upd_ksm<KA>()>& in,
+                                         int rc, float invB, unsigned long long* tm, bool direct,
+                                         __amdgpu_buffer_rsrc_t rs_mypart) {
+  constexpr int KSM = upd_ksm<KA>();
+  const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  const int b = w;
+  const int D = n.D, KS = (D + 3) >> 2;
+  const bool timer = args.profile && blockIdx.x == 0 && t == 0;
+  unsigned long long tl = timer ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#define SPL_CMARK(i)                                                   \
+  if (timer) {                                                         \
+    const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();  \
+    tm[i] += now_ - tl;                                                \
+    tl = now_;                                                         \
+  }
+  const UpdHead hi = upd_head_info(n, h);
+  const int oc = hi.oc, no = hi.no;
+  // ---- forward: trunk block b (H0^T = W0 X^T, GroupNorm + SiLU), every wave its own block
+  upd_v4 Fw, xh0, xh, G;
+  float r0, rh;
+  {
+    upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* wr = W + n.w0.lds + (16 * b + x) * n.w0.stride;
+#pragma unroll
+    for (int s = 0; s < KSM; ++s) {
+      if (s < KS) {
+        const int d = 4 * s + q;
+        acc = upd_mma(d < D ? wr[d] : 0.0f, in.xin[s], acc);
+      }
+    }
+    upd_gn_fwd_frag(acc, upd_ld4(W + n.g0.lds + 16 * b + 4 * q), upd_ld4(W + n.b0.lds + 16 * b + 4 * q),
+                    xh0, r0, Fw);
+    upd_st4(sc.Fs + x * UPD_ZS + 16 * b + 4 * q, Fw);
+  }
+  __syncthreads();   // #0: Fs
+  {
+    upd_v4 F[4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) F[bb] = upd_ld4(sc.Fs + x * UPD_ZS + 16 * bb + 4 * q);
+    // head h block b: Z^T = W1_h[16b ..][:] F^T — ONE accumulation chain in the order of
+    // upd_tile_fwd (the evaluate kernel's), so the first minibatch's ratio is exactly 1
+    upd_v4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const upd_v4 wa = upd_ld4(W + hi.w1 + (16 * b + x) * UPD_HS + 16 * bb + 4 * q);
+      z = upd_mma(wa[0], F[bb][0], z);
+      z = upd_mma(wa[1], F[bb][1], z);
+      z = upd_mma(wa[2], F[bb][2], z);
+      z = upd_mma(wa[3], F[bb][3], z);
+    }
+    upd_gn_fwd_frag(z, upd_ld4(W + hi.g1 + 16 * b + 4 * q), upd_ld4(W + hi.b1 + 16 * b + 4 * q), xh, rh, G);
+    // output layer partial over this block's 16 channels: O^T[j][row] += W2[j][16b + 4q + i] G^T
+    const bool mine = x >= oc && x < oc + no;
+    const upd_v4 wv = mine ? upd_ld4(W + hi.w2 + (x - oc) * UPD_HS + 16 * b + 4 * q) : upd_v4{0.f, 0.f, 0.f, 0.f};
+    upd_v4 o = {0.f, 0.f, 0.f, 0.f};
+    o = upd_mma(wv[0], G[0], o);
+    o = upd_mma(wv[1], G[1], o);
+    o = upd_mma(wv[2], G[2], o);
+    o = upd_mma(wv[3], G[3], o);
+    upd_st4(sc.Op + (w * 16 + x) * 16 + 4 * q, o);   // [w][row x][j = 4q + i]
+    if (t < UPD_RT * UPD_RIN) sc.Rin[t] = in.rin;
+  }
+  SPL_CMARK(0)
+  __syncthreads();   // #1: Op, Rin
+  SPL_CMARK(1)
+  // ---- the head's per-row loss on lanes q == 0 of every wave (each wave needs dO; one wave per
+  //      SIMD, so the redundant chains do not share issue slots): the actor's surrogate chain
+  //      (dO of the actor's outputs, lp[0] = -min(s1, s2), lp[2] = H) or the critic's SmoothL1
+  //      (dO of V, lp[1]) — the same arithmetic as the other forms (upd_row_loss)
+  float lp[3] = {0.f, 0.f, 0.f};
+  float* dOrow = sc.dOs + (w * 16 + x) * 16;
+  {
+    float O[UPD_MAXO], dO[UPD_MAXO];
+    upd_tile_outputs_reg<SPL_NW>(n, W, sc, O);
+    if (q == 0) {
+      if (x < rc) {
+        if (h == 0)
+          upd_row_loss<1, KA, 2>(n, O, sc.Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dO, lp);
+        else
+          upd_row_loss<1, KA, 1>(n, O, sc.Rin + x * UPD_RIN, invB, args.clip, args.vf_coef, dO, lp);
+      } else {
+#pragma unroll
+        for (int j = 0; j < UPD_MAXO; ++j) dO[j] = 0.f;
+      }
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4)
+        if (4 * j4 < n.nout) upd_st4(dOrow + 4 * j4, upd_v4{dO[4 * j4], dO[4 * j4 + 1], dO[4 * j4 + 2], dO[4 * j4 + 3]});
+    }
+  }
+  const float* dOw = sc.dOs + w * 16 * 16;
+  float* Tw = sc.Ts + w * upd_ts(n) * UPD_RT * 16;
+  upd_st4(Tw + x * 16 + 4 * q, G);   // G transposed for dW2 (rows x channels of block b)
+  upd_wave_sync();
+  SPL_CMARK(2)
+  {
+    // dW2_h[j][16b + x] = sum_rows dO[row][oc + j] G[row][16b + x]
+    upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float a = x < no ? dOw[(4 * s + q) * 16 + oc + x] : 0.0f;
+      acc = upd_mma(a, Tw[(4 * s + q) * 16 + x], acc);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * q + i < no) Ga[hi.w2 + (4 * q + i) * UPD_HS + 16 * b + x] = acc[i];
+    // dG^T block b = W2_h^T dO_h^T (K = the head's outputs), GroupNorm + SiLU backward -> dZ
+    upd_v4 dg = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < UPD_MAXA / 4; ++s) {
+      if (4 * s < no) {
+        const int j = 4 * s + q;
+        const float a = j < no ? W[hi.w2 + j * UPD_HS + 16 * b + x] : 0.0f;
+        const float bb = j < no ? dOw[x * 16 + oc + j] : 0.0f;
+        dg = upd_mma(a, bb, dg);
+      }
+    }
+    upd_v4 dy;
+    const upd_v4 dz = upd_gn_bwd_frag(dg, xh, upd_ld4(W + hi.g1 + 16 * b + 4 * q),
+                                      upd_ld4(W + hi.b1 + 16 * b + 4 * q), rh, dy);
+    upd_st4(sc.Zs + x * UPD_ZS + 16 * b + 4 * q, dz);
+    upd_v4 dyx;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dyx[i] = dy[i] * xh[i];
+    upd_colsum_add(dyx, Ga + hi.g1 + 16 * b + 4 * q, x == 0, true);
+    upd_colsum_add(dy, Ga + hi.b1 + 16 * b + 4 * q, x == 0, true);
+  }
+  // inputs, rows x features, for dW0
+#pragma unroll
+  for (int s = 0; s < KSM; ++s)
+    if (s < KS && (s % SPL_NW) == w) sc.Xs[x * sc.XS + 4 * s + q] = in.xin[s];
+  SPL_CMARK(3)
+  __syncthreads();   // #2: Zs, Xs
+  SPL_CMARK(4)
+  {
+    // ---- dF^T block b = W1_h^T dZ^T first (it heads the trunk's chain: GroupNorm backward ->
+    //      dW0), K = 64 head channels permuted so the A reads are conflict-free
+    const float* Zh = sc.Zs + x * UPD_ZS;
+    const float* Wh = W + hi.w1 + 16 * b + x;
+    upd_v4 zb[4];
+#pragma unroll
+    for (int sg = 0; sg < 4; ++sg) zb[sg] = upd_ld4(Zh + 16 * sg + 4 * q);
+    upd_v4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int o = 16 * (s & 3) + 4 * q + (s >> 2);
+      if (s & 1) d1 = upd_mma(Wh[o * UPD_HS], zb[s & 3][s >> 2], d1);
+      else d0 = upd_mma(Wh[o * UPD_HS], zb[s & 3][s >> 2], d0);
+    }
+    // ---- dW1_h[16b + 4q + i][16bb + x] = sum_rows dZ[row][16b + 4q + i] F[row][16bb + x]:
+    //      independent of dF, issued behind it
+    upd_v4 acc[4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) acc[bb] = upd_v4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float a = sc.Zs[(4 * s + q) * UPD_ZS + 16 * b + x];
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) acc[bb] = upd_mma(a, sc.Fs[(4 * s + q) * UPD_ZS + 16 * bb + x], acc[bb]);
+    }
+    upd_v4 dF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dF[i] = d0[i] + d1[i];
+    // trunk GroupNorm + SiLU backward of THIS head's share -> dH0 (block b), γ0 / β0 sums
+    upd_v4 dy0;
+    const upd_v4 dH0 = upd_gn_bwd_frag(dF, xh0, upd_ld4(W + n.g0.lds + 16 * b + 4 * q),
+                                       upd_ld4(W + n.b0.lds + 16 * b + 4 * q), r0, dy0);
+    upd_v4 dyx;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dyx[i] = dy0[i] * xh0[i];
+    upd_colsum_add(dyx, Ga + n.g0.lds + 16 * b + 4 * q, x == 0, true);
+    upd_colsum_add(dy0, Ga + n.b0.lds + 16 * b + 4 * q, x == 0, true);
+    if (direct) {
+      // dW1 (16 of the role's ~20 KB) straight from the accumulators into this tile group's
+      // partial (4-B sc1 stores, 64-B runs per 16 lanes), under the trunk backward below, instead
+      // of through the LDS image and the publish loop (PRL_UPD_SPL_DIRECT, A/B)
+      const int k0 = hi.w1 + (16 * b + 4 * q) * UPD_HS + x;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st1_sc1(rs_mypart, k0 + i * UPD_HS + 16 * bb, acc[bb][i]);
+    } else {
+      float* gw1 = Ga + hi.w1 + (16 * b + 4 * q) * UPD_HS + x;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gw1[i * UPD_HS + 16 * bb] = acc[bb][i];
+    }
+    SPL_CMARK(5)
+    // ---- dW0[16b + 4q + i][16e + x] = sum_rows dH0[row][ch] X[row][d] (dH0 transposed via Tw;
+    //      Tw's G was last read by this wave's dW2 before barrier #2)
+    upd_st4(Tw + x * 16 + 4 * q, dH0);
+    upd_wave_sync();
+#pragma unroll
+    for (int e = 0; e < (KSM + 3) / 4; ++e) {
+      if (16 * e < D) {
+        upd_v4 a0 = {0.f, 0.f, 0.f, 0.f};
+        const int d = 16 * e + x;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          a0 = upd_mma(Tw[(4 * s + q) * 16 + x], d < D ? sc.Xs[(4 * s + q) * sc.XS + d] : 0.0f, a0);
+        if (d < D) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) Ga[n.w0.lds + (16 * b + 4 * q + i) * n.w0.stride + d] = a0[i];
+        }
+      }
+    }
+  }
+  SPL_CMARK(6)
+  // ---- the head's output biases and loss partials (wave 3; its own dO rows and lp lanes)
+  if (w == SPL_NW - 1) {
+    if (l < no) {   // f64 sum: the softmax outputs' dO cancel across rows
+      double acc = 0.0;
+#pragma unroll
+      for (int r = 0; r < UPD_RT; ++r) acc += (double)dOw[r * 16 + oc + l];
+      Ga[(h == 0 ? n.b2[0].lds : n.b2[1].lds) + l] = (float)acc;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const bool mine = h == 0 ? k != 1 : k == 1;
+      if (mine) {
+        const float s = upd_rsum16(lp[k]);
+        if (l == 0) Ga[n.Lp + k] = s;
+      }
+    }
+  }
+  SPL_CMARK(7)
+#undef SPL_CMARK
+}
+
+// Phase B's slices, balanced by loads: a trunk or loss quad sums 2 Gt partials, a head quad Gt,
+// and phase B's time per workgroup follows the bytes it loads (~20 KB per us per CU, measured:
+// equal-quad slices left the trunk's owners loading twice the others' bytes, 3.7 vs 2.0 us).
+// So quad q weighs 2 for q < QT and q == Qp, else 1: weighted position w(q) = q + min(q, QT),
+// U = Qp + QT + 2 units, and slice g starts at the first quad with w(q) >= U g / G.
+__device__ inline int spl_slice_start(int g, int G, int Qp, int QT) {
+  const int Qtot = Qp + 1;
+  const int64_t U = (int64_t)Qp + QT + 2;
+  const int64_t u = U * g / G;
+  const int64_t q = u <= 2 * (int64_t)QT ? (u + 1) / 2 : u - QT;
+  return (int)(q < Qtot ? q : Qtot);
+}
+
+// Sum of quad q over the virtual partials v = first, first + stride, ... < nv, where v < Gt is
+// part[v] and v >= Gt is part2[v - Gt] (the trunk / loss quads' second Gt partials, quad qd
+// there), in that order; loads issued in batches of 16, so a dual quad's two partial sets are in
+// flight together (one memory round trip, not two in series).
+__device__ inline void spl_sum_partials(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_part2,
+                                        int Qtot, int P2, int q, int qd, int first, int stride,
+                                        int Gt, int nv, double& ax, double& ay, double& az,
+                                        double& aw) {
+  constexpr int NB = 16;
+  for (int v0 = first; v0 < nv; v0 += NB * stride) {
+    float4 v[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int vv = v0 + u * stride;
+      if (vv < nv)
+        v[u] = vv < Gt ? ld4_sc1(rs_part, ((size_t)vv * Qtot + q) * 4)
+                       : ld4_sc1(rs_part2, ((size_t)(vv - Gt) * P2 + qd) * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      if (v0 + u * stride < nv) {
+        ax += v[u].x; ay += v[u].y; az += v[u].z; aw += v[u].w;
+      }
+    }
+  }
+}
+
+// Phase B of the split form: slice g of G (spl_slice_start) over the Gt role partials; the
+// trunk quads [0, QT) and the loss quad Qp also over part2 (role 1's trunk partials,
+// [Gt][QT + 1] quads).  Per quad: part[0 .. Gt) then part2[0 .. Gt) in the order sub,
+// sub + spl, ... for each of spl threads, combined in sub order (deterministic).
+__device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_part2,
+                                        __amdgpu_buffer_rsrc_t rs_red, int Qtot, int Qp, int QT, int g,
+                                        int G, int Gt, float* scratch, bool sys, int fill,
+                                        UpdSub sub) {
+  const int t = threadIdx.x;
+  const int qlo = spl_slice_start(g, G, Qp, QT), qhi = spl_slice_start(g + 1, G, Qp, QT);
+  const int nq = qhi - qlo;
+  if (nq <= 0) return;
+  const int P2 = QT + 1;
+  auto fin = [&](int q, double ax, double ay, double az, double aw) {
+    const float4 r = float4{(float)ax, (float)ay, (float)az, (float)aw};
+    if (sys) st4_aux<UPD_AUX_SYS>(rs_red, (size_t)q * 4, r);   // data-parallel: the rank's slice buffer
+    else st4_sc1(rs_red, (size_t)q * 4, r);
+  };
+  if (2 * nq > SPL_NT) {
+    // wide slices (few workgroups, small minibatches): each thread owns whole quads
+    for (int q = qlo + t; q < qhi; q += SPL_NT) {
+      double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
+      const bool dual = q < QT || q == Qp;
+      spl_sum_partials(rs_part, rs_part2, Qtot, P2, q, q < QT ? q : QT, 0, 1, Gt, dual ? 2 * Gt : Gt,
+                       ax, ay, az, aw);
+      fin(q, ax, ay, az, aw);
+    }
+    return;
+  }
+  // spl threads per quad, each summing every spl-th partial: a power of two (fill 0), or as
+  // many as the 256 threads allow (fill 1: more loads in flight; the slice loads are latency-bound)
+  int spl = 1;
+  if (fill) spl = std::max(1, std::min(Gt, SPL_NT / nq));
+  else
+    while (spl * 2 * nq <= SPL_NT && spl * 2 <= Gt) spl *= 2;
+  double* red = reinterpret_cast<double*>(scratch);   // [spl][nq][4]
+  if (t < spl * nq) {
+    const int qi = t % nq, sb = t / nq, q = qlo + qi;
+    double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
+    const bool dual = q < QT || q == Qp;
+    spl_sum_partials(rs_part, rs_part2, Qtot, P2, q, q < QT ? q : QT, sb, spl, Gt, dual ? 2 * Gt : Gt,
+                     ax, ay, az, aw);
+    double* o = red + 4 * (sb * nq + qi);
+    o[0] = ax; o[1] = ay; o[2] = az; o[3] = aw;
+  }
+  sub.mark(0);   // thread 0's partial loads landed and summed
+  __syncthreads();
+  if (t < nq) {
+    double ax = red[4 * t], ay = red[4 * t + 1], az = red[4 * t + 2], aw = red[4 * t + 3];
+    for (int k = 1; k < spl; ++k) {
+      const double* o = red + 4 * (k * nq + t);
+      ax += o[0]; ay += o[1]; az += o[2]; aw += o[3];
+    }
+    fin(qlo + t, ax, ay, az, aw);
+  }
+  sub.mark(1);   // slice combined, its stores issued
+}
+
+// NQC = ceil(Qp / 256): quads per thread of phase C's canonical sweep (the moment registers
+// cover the same slots; a slot holds moments only where this role owns the quad).
+// DP: data-parallel ranks (prl_ppo_update_dpx): union-minibatch row weights inv_count[j] and,
+// after phase B, the cross-rank sum of each slice (upd_dp_union_slice, as the 8-wave kernel);
+// the 2 Gt workgroups of every rank cut the gradient into the same 2 Gt slices.
+template <int NQC, int KA, bool DP>
+__device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& args) {
+  extern __shared__ __align__(16) float upd_lds[];
+  const int t = threadIdx.x, g = blockIdx.x, G = args.G, Gt = args.Gt;
+  const int role = g / Gt, gt = g - role * Gt;   // role = the head this workgroup runs
+  const int Lp = n.Lp, Qp = Lp / 4, Qtot = Qp + 1;
+  const int QT = n.w1[0].lds / 4;   // trunk quads [0, QT)
+  const int QH = n.w1[1].lds / 4;   // head 0: [QT, QH), head 1: [QH, Qp)
+  // owned quads: the trunk and this role's head (the only parameters its tile reads)
+  auto owned = [&](int q) { return role == 0 ? q < QH : (q < QT || q >= QH); };
+  float* hdr = upd_lds;
+  float* scratch = upd_lds + UPD_HDR;
+  const int scr_floats = (upd_scratch_floats(n.D, SPL_NW, upd_ts(n)) + 3) & ~3;
+  float* W = scratch + scr_floats;   // [Lp]
+  float* Ga = W + Lp;                // [Lp + 4]
+  const UpdScr sc = upd_scr(scratch, n.D, SPL_NW);
+  int* s_abort = reinterpret_cast<int*>(hdr + 8);
+  float* s_adam = hdr + 10;
+
+  float4 mreg[NQC], vreg[NQC];
+  for (int q = t; q < Qp; q += SPL_NT)
+    *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(args.params + 4 * q);
+#pragma unroll
+  for (int i = 0; i < NQC; ++i) {
+    const int q = t + i * SPL_NT;
+    const bool own = q < Qp && owned(q);
+    mreg[i] = own ? *reinterpret_cast<const float4*>(args.exp_avg + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+    vreg[i] = own ? *reinterpret_cast<const float4*>(args.exp_avg_sq + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float step0 = args.adam_step[0];
+  if (t < 24) reinterpret_cast<unsigned long long*>(hdr + 16)[t] = 0ull;
+  for (int k = t; k < Lp + 4; k += SPL_NT) Ga[k] = 0.0f;   // entries no tile writes stay 0 for good
+  __syncthreads();
+
+  unsigned long long* const pts = reinterpret_cast<unsigned long long*>(hdr + 64);
+  if (g == 0 && t == 0) {
+    for (int i = 0; i < 7; ++i) pts[i] = 0ull;
+    pts[7] = __builtin_amdgcn_s_memrealtime();
+    pts[8] = pts[7];
+    pts[9] = __builtin_amdgcn_s_memtime();
+  }
+  auto mark = [&](int i) {
+    if (args.profile && g == 0 && t == 0) {
+      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+      pts[i] += now - pts[7];
+      pts[7] = now;
+    }
+  };
+  unsigned long long* const tm = reinterpret_cast<unsigned long long*>(hdr + 16);
+  const UpdSub subm{(args.profile && g == 0) ? tm + 8 : nullptr, pts + 7};
+  const int R = args.R;   // == UPD_RT: one tile per workgroup and step
+  UpdIn<upd_ksm<KA>()> nin;
+  auto first_row = [&](int s) { return (int64_t)(s % args.nb) * args.mb + (int64_t)gt * R; };
+  auto first_rows = [&](int s) {
+    const int64_t fmb0 = (int64_t)(s % args.nb) * args.mb;
+    const int fB = (int)std::min<int64_t>(args.mb, args.N - fmb0);
+    return args.profile == 2 ? 0 : std::max(0, std::min(R, fB - gt * R));
+  };
+  upd_tile_load<1, KA, true>(n, args.S, args.act, args.old_logp, args.adv, args.ret, first_row(0),
+                             std::min(UPD_RT, first_rows(0)), nin);
+  const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_part2 = upd_rsrc(args.part2),
+                               rs_red = upd_rsrc(args.red);
+  const __amdgpu_buffer_rsrc_t rs_mypart = upd_rsrc(args.part + (size_t)gt * Qtot * 4);
+  const bool direct = args.spl_direct != 0;
+  // the dW1 quads of this role's head: [W1lo, W1hi); stored from registers when direct, so their
+  // padding columns (64..67 of each row) are zeroed once here and never written again
+  const int W1lo = n.w1[role].lds / 4, W1hi = (n.w1[role].lds + UPD_H * UPD_HS) / 4;
+  if (direct) {
+    for (int q = W1lo + t; q < W1hi; q += SPL_NT) st4_sc1(rs_mypart, (size_t)q * 4, float4{0.f, 0.f, 0.f, 0.f});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  float loss_last = 0.f;
+  for (int s = 0; s < args.total_steps; ++s) {
+    const int j = s % args.nb;
+    const int64_t mb0 = (int64_t)j * args.mb;
+    const int B = (int)std::min<int64_t>(args.mb, args.N - mb0);
+    const float invB = DP ? args.inv_count[j] : 1.0f / (float)B;
+    const int myrows = args.profile == 2 ? 0 : std::max(0, std::min(R, B - gt * R));
+    // ---- phase A: this role's share of tile group gt's gradient ------------------------------
+    if (myrows > 0) {
+      const UpdIn<upd_ksm<KA>()> cur = upd_in_real(nin);
+      // prefetch the next step's tile under this one and the hand-offs (unconditional: clamped
+      // arguments, see the engine's load_next)
+      upd_tile_load<1, KA, true>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
+                                 first_row(s + 1), std::min(UPD_RT, first_rows(s + 1)), nin);
+      spl_tile<KA>(n, args, role, W, Ga, sc, cur, myrows, invB, tm, direct, rs_mypart);
+    } else {
+      for (int k = t; k < Lp + 4; k += SPL_NT) Ga[k] = 0.0f;
+      upd_tile_load<1, KA, true>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
+                                 first_row(s + 1), std::min(UPD_RT, first_rows(s + 1)), nin);
+    }
+    __syncthreads();
+    mark(0);   // phase A compute
+    // (direct and rows this step: the dW1 quads are in the partial already; with no rows they
+    // are published from the zeroed image like the rest)
+    const bool skip = direct && myrows > 0;
+    auto pub = [&](int q) {
+      if (!(skip && q >= W1lo && q < W1hi))
+        st4_sc1(rs_part, ((size_t)gt * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
+    };
+    if (role == 0) {
+      const int qe = QH;   // trunk + head 0
+      for (int q = t; q < qe; q += SPL_NT) pub(q);
+      if (t == 0) st4_sc1(rs_part, ((size_t)gt * Qtot + Qp) * 4, *reinterpret_cast<const float4*>(Ga + Lp));
+    } else {
+      for (int q = QH + t; q < Qp; q += SPL_NT) pub(q);
+      for (int q = t; q < QT; q += SPL_NT)
+        st4_sc1(rs_part2, ((size_t)gt * (QT + 1) + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
+      if (t == 0) st4_sc1(rs_part2, ((size_t)gt * (QT + 1) + QT) * 4, *reinterpret_cast<const float4*>(Ga + Lp));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    mark(1);   // publish
+    if (t < 64) {
+      if (t == 0) upd_arrive(args.ctr, UPD_CTR_A, g);
+      const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));
+      if (t == 0) *s_abort = ok ? 0 : 1;
+    } else if (t == 64) {
+      const double tstep = (double)step0 + (double)(s + 1);
+      const double bc1 = 1.0 - pow((double)args.beta1, tstep);
+      const double bc2 = 1.0 - pow((double)args.beta2, tstep);
+      s_adam[0] = (float)((double)args.lr / bc1);
+      s_adam[1] = (float)(1.0 / sqrt(bc2));
+    }
+    __syncthreads();
+    if (*s_abort) return;
+    mark(2);   // wait A
+    // ---- phase B ---------------------------------------------------------------------------
+    {
+      const unsigned long long gstep = args.dp_seq0 + (unsigned long long)s;
+      const int par = (int)(gstep & 1ull);
+      spl_slice_reduce(rs_part, rs_part2, DP ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
+                       Qtot, Qp, QT, g, G, Gt, scratch, DP, args.spl_fill, subm);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (DP && !upd_dp_union_slice(args, rs_red, Qtot, g, G, gstep, par, s_abort,
+                                    spl_slice_start(g, G, Qp, QT), spl_slice_start(g + 1, G, Qp, QT)))
+        return;
+    }
+    mark(3);   // slice reduce
+    if (t < 64) {
+      if (t == 0) upd_arrive(args.ctr, UPD_CTR_B, g);
+      const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_B, (unsigned)G * (unsigned)(s + 1));
+      if (t == 0) *s_abort = ok ? 0 : 1;
+    }
+    __syncthreads();
+    if (*s_abort) return;
+    mark(4);   // wait B
+    // ---- phase C: the norm in the canonical order, then AdamW on the owned quads -------------
+    float4 gq[NQC];
+#pragma unroll
+    for (int i = 0; i < NQC; ++i)
+      if (i * SPL_NT < Qp) gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
+    float clipc;
+    {
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < NQC; ++i)
+        if (i * SPL_NT < Qp && t + i * SPL_NT < Qp)
+          acc += (gq[i].x * gq[i].x + gq[i].y * gq[i].y) + (gq[i].z * gq[i].z + gq[i].w * gq[i].w);
+      subm.mark(2);   // thread 0's gradient quads landed
+      acc = wave_sum_f32_to63(acc);
+      float* s_nrm = hdr + 96;
+      if ((t & 63) == 63) s_nrm[t >> 6] = acc;
+      __syncthreads();
+      float tot = 0.f;
+#pragma unroll
+      for (int w = 0; w < SPL_NW; ++w) tot += s_nrm[w];
+      const float coef = args.max_norm / (sqrtf(tot) + 1e-6f);
+      clipc = coef < 1.0f ? coef : 1.0f;
+      if (args.profile && g == 0 && t == 0 && coef < 1.0f) tm[20] += 1ull;
+      if (g == 0 && t == 0 && s + 1 == args.total_steps) {
+        const float4 lpq = ld4_sc1(rs_red, (size_t)Qp * 4);
+        loss_last = lpq.x * invB + args.vf_coef * (lpq.y * invB) - args.ent_coef * (lpq.z * invB);
+      }
+    }
+    mark(5);   // norm + loss
+    {
+      const float step_size = s_adam[0];
+      const float inv_bc2_sqrt = s_adam[1];
+      const float decay = (float)(1.0 - (double)args.lr * (double)args.wd);
+      const float b2 = (float)args.beta2;
+      const float omb1 = (float)(1.0 - (double)args.beta1), omb2 = (float)(1.0 - (double)args.beta2);
+#pragma unroll
+      for (int i = 0; i < NQC; ++i) {
+        const int q = t + i * SPL_NT;
+        if (i * SPL_NT < Qp && q < Qp && owned(q)) {
+          float4 pw = *reinterpret_cast<float4*>(W + 4 * q);
+          float4 m4 = mreg[i], v4 = vreg[i];
+          const float4 g4 = gq[i];
+          // the engine's AdamW arithmetic (ppo_update_body, 4-wave scalar form)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float gr = f4get(g4, e) * clipc;
+            float m = f4get(m4, e), v = f4get(v4, e), p = f4get(pw, e);
+            p = p * decay;
+            m = fmaf(omb1, gr - m, m);
+            v = fmaf(omb2 * gr, gr, v * b2);
+            const float denom = fmaf(__builtin_amdgcn_sqrtf(v), inv_bc2_sqrt, args.eps);
+            float rq = __builtin_amdgcn_rcpf(denom);
+            rq = fmaf(rq, fmaf(-denom, rq, 1.0f), rq);
+            p = fmaf(-step_size, m * rq, p);
+            f4set(m4, e, m);
+            f4set(v4, e, v);
+            f4set(pw, e, p);
+          }
+          mreg[i] = m4;
+          vreg[i] = v4;
+          *reinterpret_cast<float4*>(W + 4 * q) = pw;
+        }
+      }
+    }
+    __syncthreads();
+    mark(6);   // AdamW
+  }
+  // ---- write back: role 0's first workgroup the trunk + head 0, role 1's the critic head ------
+  if (gt == 0) {
+    for (int i = 0; i < NQC; ++i) {
+      const int q = t + i * SPL_NT;
+      if (q < Qp && (role == 0 ? q < QH : q >= QH)) {
+        *reinterpret_cast<float4*>(args.params + 4 * q) = *reinterpret_cast<const float4*>(W + 4 * q);
+        *reinterpret_cast<float4*>(args.exp_avg + 4 * q) = mreg[i];
+        *reinterpret_cast<float4*>(args.exp_avg_sq + 4 * q) = vreg[i];
+      }
+    }
+    if (g == 0 && t == 0) {
+      for (int i = 0; i < 7; ++i) args.prof[i] = pts[i];
+      args.prof[7] = (unsigned long long)args.total_steps;
+      args.prof[30] = __builtin_amdgcn_s_memrealtime() - pts[8];
+      args.prof[31] = __builtin_amdgcn_s_memtime() - pts[9];
+      for (int i = 0; i < 22; ++i) args.prof[8 + i] = reinterpret_cast<unsigned long long*>(hdr + 16)[i];
+      args.adam_step[0] = step0 + (float)args.total_steps;
+      if (args.loss_out) args.loss_out[0] = loss_last;
+    }
+  }
+}
+
+template <int NQC, int KA, int KDIM, bool DP = false>
+__global__ __launch_bounds__(SPL_NT, 1) void ppo_update_split_kernel(UpdArgs args) {
+  constexpr UpdNet N = upd_make(KDIM, KA, 1);
+  ppo_split_body<NQC, KA, DP>(N, args);
+}

@@ -142,6 +142,9 @@ struct UpdArgs {
   float* adam_step;
   float* loss_out;
   float* part;      // [G][Qtot * 4]
+  float* part2;     // head-split form: role 1's trunk + loss-partial quads [Gt][QT + 1][4]
+  int spl_fill;     // head-split form's phase B: threads per quad (PRL_UPD_SPL_FILL, A/B)
+  int spl_direct;   // head-split form: dW1 stored from registers into the partial (PRL_UPD_SPL_DIRECT)
   float* red;       // [Qtot * 4]
   float* sq;        // [NW G] per-wave squared-norm pieces of the slices
   unsigned* ctr;    // [0] arrivals A, [1] arrivals B, [2] abort, [3] status (zeroed per launch),
@@ -1469,7 +1472,8 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
 // acquire.
 
 __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t rs_red, int Qtot,
-                                   int g, int G, unsigned long long gstep, int par, int* s_abort) {
+                                   int g, int G, unsigned long long gstep, int par, int* s_abort,
+                                   int qlo_in = -1, int qhi_in = -1) {
   const int t = threadIdx.x, NT = blockDim.x;
   const unsigned long long want = gstep + 1ull;
   if (t == 0) {
@@ -1516,7 +1520,9 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
   }
   __syncthreads();
   if (*s_abort) return false;
-  const int qlo = (int)((int64_t)Qtot * g / G), qhi = (int)((int64_t)Qtot * (g + 1) / G);
+  // this workgroup's slice: phase B's (uniform, or the split form's load-balanced one)
+  const int qlo = qlo_in >= 0 ? qlo_in : (int)((int64_t)Qtot * g / G);
+  const int qhi = qhi_in >= 0 ? qhi_in : (int)((int64_t)Qtot * (g + 1) / G);
   const size_t base = (size_t)par * Qtot * 4;
   for (int q = qlo + t; q < qhi; q += NT) {
     float4 acc = ld4_aux<UPD_AUX_SYS>(upd_rsrc(args.xbuf[0] + base), (size_t)q * 4);
@@ -2172,6 +2178,8 @@ __global__ __launch_bounds__(UPD_THREADS) void ppo_adam_kernel(int Lp, float* im
   if (blockIdx.x == 0 && t == 0 && loss_out) loss_out[0] = adam_loss(grad, Lp, inv_count, vf_coef, ent_coef);
 }
 
+#include "prl_ppo_split.h"
+
 // torch flat vectors <-> images (to_image: flat -> image, else image -> flat)
 __global__ __launch_bounds__(UPD_THREADS) void ppo_image_kernel(UpdNet n, float* fp, float* fm,
                                                               float* fv, float* ip, float* im,
@@ -2306,6 +2314,23 @@ int g_repl = [] {
   const int v = e ? atoi(e) : 2;
   return v >= 1 ? v : 1;
 }();
+// The head-split latency form (prl_ppo_split.h) for the two-head discrete nets of the CartPole
+// shape: PRL_UPD_SPLIT / prl_ppo_update_set_split (1 = on, the default; 0 = the 8-wave kernel).
+int g_split = [] {
+  const char* e = getenv("PRL_UPD_SPLIT");
+  return (e && e[0] == '0') ? 0 : 1;
+}();
+// Quads per thread of the split kernel's phase-C sweep that are instantiated
+constexpr int SPL_NQC = 10;
+bool upd_split_host(const UpdNet& n, int Gt, int R, bool tp) {
+  if (tp || !g_split || upd_force_generic() || !upd_is_cartpole(n) || R != UPD_RT) return false;
+  if (cdiv(n.Lp / 4, SPL_NT) > SPL_NQC) return false;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  return 2 * Gt <= cus;
+}
 int upd_repl(int Gt) {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -2346,10 +2371,12 @@ struct UpdWs {
   float* part;
   float* img;   // [3][Lp + 4]: parameter, exp_avg, exp_avg_sq images of the persistent launch
   float* mv;    // [4][Lp + 4]: the throughput form's moment buffers m0, v0, m1, v1
+  float* part2; // [Gt][QT + 1][4]: the head-split form's role-1 trunk (+ loss) partials
 };
 
 // workspace: ctr[UPD_CTR_WORDS] (words 0-3 and the shards zeroed per launch, word 4 sticky) |
-// prof[32] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4] | img[3][Qtot*4] | mv[4][Qtot*4] | slack
+// prof[32] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4] | img[3][Qtot*4] | mv[4][Qtot*4] |
+// part2[G][(QT+1)*4] | slack
 // (phase C's sweeps read up to one thread block of quads past an image: the slack keeps the
 // last one inside the allocation)
 size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
@@ -2358,7 +2385,8 @@ size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
   auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
   const size_t o_ctr = take(4 * UPD_CTR_WORDS), o_prof = take(256), o_sq = take(2048 * 4), o_red = take(Qtot * 16),
                o_part = take((size_t)G * Qtot * 16), o_img = take((size_t)3 * Qtot * 16),
-               o_mv = take((size_t)4 * Qtot * 16);
+               o_mv = take((size_t)4 * Qtot * 16),
+               o_part2 = take((size_t)G * ((size_t)n.w1[0].lds / 4 + 1) * 16);
   (void)take(512 * 16);
   if (ws) {
     ws->ctr = reinterpret_cast<unsigned*>(base + o_ctr);
@@ -2368,6 +2396,7 @@ size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
     ws->part = reinterpret_cast<float*>(base + o_part);
     ws->img = reinterpret_cast<float*>(base + o_img);
     ws->mv = reinterpret_cast<float*>(base + o_mv);
+    ws->part2 = reinterpret_cast<float*>(base + o_part2);
   }
   return off;
 }
@@ -2403,7 +2432,7 @@ struct UpdDp {
 // the slice buffers [2][Qtot * 4] f32, then the per-workgroup step flags [G] u64
 size_t upd_xbuf_flags_off(const UpdNet& n) { return (((size_t)n.Lp / 4 + 1) * 32 + 255) & ~(size_t)255; }
 unsigned g_dp_spin_limit = UPD_DP_SPIN_LIMIT;
-int32_t g_last_plan[6] = {-1, -1, -1, -1, -1, -1};   // prl_ppo_update_last_plan
+int32_t g_last_plan[7] = {-1, -1, -1, -1, -1, -1, -1};   // prl_ppo_update_last_plan
 
 int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, int32_t D,
             int32_t A, int32_t discrete, const float* S, const float* actions,
@@ -2482,6 +2511,13 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     args.xbuf_self = args.xbuf[dp->rank];
     args.xflag_self = args.xflag[dp->rank];
   }
+  args.part2 = ws.part2;
+  {
+    const char* e = getenv("PRL_UPD_SPL_FILL");   // default 1 (mb 512: 13.58 vs 14.07 us per step)
+    args.spl_fill = (e && e[0] == '0') ? 0 : 1;
+    const char* d = getenv("PRL_UPD_SPL_DIRECT");
+    args.spl_direct = (d && d[0] == '1') ? 1 : 0;
+  }
   args.tp_m0 = ws.mv;
   args.tp_v0 = ws.mv + L4;
   args.tp_m1 = ws.mv + 2 * L4;
@@ -2493,8 +2529,13 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     if (p2.kern) plan = p2;
     else tp = false;
   }
-  // replicated tiles: the latency form on one GPU only
-  const int G = (tp || dp) ? Gt : Gt * upd_repl(Gt);
+  const bool split = upd_split_host(args.net, Gt, args.R, tp);
+  if (split)
+    plan = UpdPlan{dp ? reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, true>)
+                      : reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, false>),
+                   SPL_NW, 1};
+  // replicated tiles: the latency form on one GPU only; the split form: two roles per tile group
+  const int G = split ? 2 * Gt : ((tp || dp) ? Gt : Gt * upd_repl(Gt));
   args.G = G;
   const size_t lds = upd_lds_bytes_plan(args.net, plan.nw, tp, plan.tiles);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_update: %zu B of LDS needed", lds);
@@ -2508,6 +2549,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   g_last_plan[4] = (!upd_force_generic() && (upd_is_cartpole(args.net) ||
                                              (!args.net.discrete && args.net.A == 1 && args.net.D == 3))) ? 1 : 0;
   g_last_plan[5] = G / Gt;
+  g_last_plan[6] = split ? 1 : 0;
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr + UPD_CTR_A, 0, 4 * (UPD_CTR_WORDS - UPD_CTR_A), st));
@@ -2567,8 +2609,14 @@ extern "C" int32_t prl_ppo_update_set_repl(int32_t replicas) {
   return prev;
 }
 
-extern "C" void prl_ppo_update_last_plan(int32_t out[6]) {
-  for (int i = 0; i < 6; ++i) out[i] = g_last_plan[i];
+extern "C" int32_t prl_ppo_update_set_split(int32_t mode) {
+  const int prev = g_split;
+  g_split = mode ? 1 : 0;
+  return prev;
+}
+
+extern "C" void prl_ppo_update_last_plan(int32_t out[7]) {
+  for (int i = 0; i < 7; ++i) out[i] = g_last_plan[i];
 }
 
 extern "C" uint32_t prl_dp_set_spin_limit(uint32_t polls) {
@@ -2580,7 +2628,8 @@ extern "C" uint32_t prl_dp_set_spin_limit(uint32_t polls) {
 extern "C" int64_t prl_dp_xbuf_bytes(int32_t D, int32_t A, int32_t discrete, int32_t mini_batch) {
   UpdNet net{};
   if (!upd_layout(D, A, discrete, net) || mini_batch <= 0) return -1;
-  return (int64_t)(upd_xbuf_flags_off(net) + (size_t)upd_grid(mini_batch) * 8);
+  // per-workgroup flags: the head-split form runs two workgroups per tile group
+  return (int64_t)(upd_xbuf_flags_off(net) + 2 * (size_t)upd_grid(mini_batch) * 8);
 }
 
 extern "C" int prl_dp_xbuf_alloc(int64_t bytes, int32_t* kind, void** out) {

@@ -42,6 +42,7 @@ SIGNATURES = {
     "prl_wide_rollout_supported": [_INT, _I32, _I32, _I32],
     "prl_wide_rollout": [_INT, _P, _I32, _I32, _I32, _I64, _P, _P, _P, _F32, _U64, _I32, _P, _P,
                          _P, _P, _P, _P, _P, _P],
+    "prl_cartpole_rollout": [_P, _I64, _P, _P, _P, _U64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "prl_active_indices": [_P, _I64, _P, _P, _P, _P],
     "prl_mask_update": [_P, _I64, _P, _I64, _P, _P],
     "prl_compact_rows": [_P, _I64, _I64, _P, _P, _P, _P, _P],
@@ -86,6 +87,7 @@ SIGNATURES = {
     "prl_dp_set_spin_limit": [ctypes.c_uint32],
     "prl_ppo_update_set_tp": [_I32],
     "prl_ppo_update_set_repl": [_I32],
+    "prl_ppo_update_set_split": [_I32],
     "prl_debug_fill_lds": [_F32, _P],
     "prl_ppo_update_last_plan": [_P],
     "prl_source_id": [],
@@ -111,7 +113,7 @@ SIGNATURES = {
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_source_id": ctypes.c_char_p,
              "prl_ppo_update_last_plan": None, "prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,
              "prl_dp_set_spin_limit": ctypes.c_uint32, "prl_ppo_update_set_tp": _I32,
-             "prl_ppo_update_set_repl": _I32,
+             "prl_ppo_update_set_repl": _I32, "prl_ppo_update_set_split": _I32,
              "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
 
 _lib = None
@@ -128,6 +130,10 @@ def _sources_id():
     spec = importlib.util.spec_from_file_location("_prl_csrc_build", os.path.join(csrc, "build.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
+    # a package shipped with csrc/ but without every stamped file (e.g. the repo-level include/
+    # dir): no stamp to compare against, so the check is skipped rather than failing to load
+    if not all(os.path.exists(os.path.join(csrc, f)) for f in mod.SOURCES + mod.HEADERS):
+        return None
     return mod.source_id(csrc)
 
 
@@ -321,6 +327,28 @@ def wide_rollout(kind, params, D, A, discrete, phys, t_elapsed, terminal, action
                                   _dev(active_after, torch.int32, "active_after"),
                                   _dev(reward_sum, torch.float64, "reward_sum"), _stream()),
            "prl_wide_rollout")
+
+
+def cartpole_rollout(params, phys, t_elapsed, terminal, seed, t_max, traj_obs, traj_act, traj_rew,
+                     traj_done, ep_len, active_after, reward_sum, probs_out=None):
+    """The whole CartPole rollout of the discrete actor in one launch (prl_cartpole_rollout): every
+    non-terminal env stepped to the end of its episode; probs_out ([t_max, E, 2] f32, tests)
+    receives the probabilities each step sampled from."""
+    E = t_elapsed.numel()
+    _check(lib().prl_cartpole_rollout(_dev(params, torch.float32, "params"), E,
+                                      _dev(phys, torch.float64, "phys"),
+                                      _dev(t_elapsed, torch.int32, "t"),
+                                      _dev(terminal, torch.uint8, "terminal"),
+                                      int(seed) & (2**64 - 1), int(t_max),
+                                      _dev(traj_obs, torch.float32, "traj_obs"),
+                                      _dev(traj_act, torch.float32, "traj_act"),
+                                      _dev(traj_rew, torch.float32, "traj_rew"),
+                                      _dev(traj_done, torch.uint8, "traj_done"),
+                                      _dev(ep_len, torch.int32, "ep_len"),
+                                      _dev(active_after, torch.int32, "active_after"),
+                                      _dev(reward_sum, torch.float64, "reward_sum"),
+                                      _dev(probs_out, torch.float32, "probs_out"), _stream()),
+           "prl_cartpole_rollout")
 
 
 # ------------------------------------------------------------------------- masks / buffers
@@ -700,6 +728,12 @@ def ppo_update_set_repl(replicas: int) -> int:
     return int(lib().prl_ppo_update_set_repl(int(replicas)))
 
 
+def ppo_update_set_split(mode: int) -> int:
+    """The engine's head-split latency form for the two-head CartPole shape (1, the default) or
+    the 8-wave kernel (0); returns the previous value.  The two agree to float32 rounding."""
+    return int(lib().prl_ppo_update_set_split(int(mode)))
+
+
 def flat_adamw(params, exp_avg, exp_avg_sq, step, grad, lr, beta1, beta2, eps, weight_decay,
                max_norm, total_norm=None):
     """clip_grad_norm_(max_norm) + AdamW.step() over flat f32 vectors (two launches).  Returns
@@ -724,12 +758,14 @@ def ppo_update_last_plan() -> dict:
     """What the last prl_ppo_update / _dpx launch in this process ran: form ("throughput" /
     "latency"), waves per workgroup, workgroups, 16-row tiles per workgroup and step, whether
     the kernel was a compile-time-layout specialisation, and the workgroups per tile group (the
-    latency form's replicated tiles)."""
-    out = (ctypes.c_int32 * 6)()
+    latency form's replicated tiles; the split form: its two head roles), and whether the
+    head-split latency form ran (csrc/prl_ppo_split.h)."""
+    out = (ctypes.c_int32 * 7)()
     lib().prl_ppo_update_last_plan(out)
-    tp, nw, G, tiles, spec, repl = list(out)
+    tp, nw, G, tiles, spec, repl, split = list(out)
     return {"form": {1: "throughput", 0: "latency"}.get(tp), "waves": nw, "grid": G,
-            "tiles": tiles, "specialised": bool(spec == 1), "replicas": repl}
+            "tiles": tiles, "specialised": bool(spec == 1), "replicas": repl,
+            "split": bool(split == 1)}
 
 
 XBUF_KINDS = {"auto": 0, "uncached": 1, "fine": 2}

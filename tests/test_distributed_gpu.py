@@ -206,7 +206,9 @@ def _nccl_one_rank_worker(port, out_dir):
     eng.close()
     ok = ok and not eng._comm and eng.dp_comm() is None
     # rollouts with the nccl process group (and its watchdog thread) alive: the vector-step
-    # graph is captured and replayed (thread-local capture mode)
+    # graph is captured and replayed (thread-local capture mode; the per-step path, not the
+    # one-launch CartPole rollout)
+    os.environ["PRL_CP_ROLLOUT"] = "0"
     from AsyncTools.AsyncPPO import AsyncPPO
     a = AsyncPPO("CartPole-v1", p, num_envs=4096, seed=1)
     for _ in range(3):

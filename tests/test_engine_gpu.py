@@ -13,6 +13,22 @@ pytestmark = pytest.mark.gpu
 ATOL = 3e-5   # weights after tens of AdamW steps (lr 1e-3): reduction-order differences only
 
 
+class _split:
+    """Run the block with the engine's head-split latency form on (1) or off (0: the 8-wave
+    kernel), restoring the previous setting (prl_ppo_update_set_split)."""
+
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        import prl_native
+        self.prev = prl_native.ppo_update_set_split(self.mode)
+
+    def __exit__(self, *exc):
+        import prl_native
+        prl_native.ppo_update_set_split(self.prev)
+
+
 def _data(N, D, cont, seed=5):
     rng = np.random.default_rng(seed)
     S = torch.from_numpy((rng.normal(size=(N, D)) * 0.5).astype(np.float32)).cuda()
@@ -176,6 +192,9 @@ def test_fused_gradient_off_policy(cont, spread, rows):
     fwd = float((logp_eng.cpu().double() - l64).abs().max()) / (1.0 + float(l64.abs().max()))
     assert fwd <= 2e-6, fwd
     eng.run(S_, A_, old2, adv, ret, 1)
+    import prl_native
+    # CartPole at mb 512 runs the head-split latency form by default (csrc/prl_ppo_split.h)
+    assert prl_native.ppo_update_last_plan()["split"] == (not cont)
     g64 = _grad_f64(p, (S_, A_, old2, adv, ret), logp_val=logp_eng)
     per = {}
     for (name, prm), gr in zip(p.policy.named_parameters(), g64):
@@ -383,12 +402,21 @@ def test_native_dp_loop_equals_python_loop(cont):
     assert s0 == s1 == 3 * 6 and l0 == l1
 
 
+@pytest.mark.parametrize("split", [0, 1])
 @pytest.mark.parametrize("cont", [False, True])
-def test_dpx_one_rank_equals_engine(cont):
+def test_dpx_one_rank_equals_engine(cont, split):
     """The data-parallel persistent kernel (prl_ppo_update_dpx) with ONE rank — its own slice
     buffer, inv_count = float(1 / rows) — gives the single-GPU engine's bits (parameters, both
     moments, step count, loss) over two learn() calls on one buffer set: its in-GPU part is the
-    engine's, the cross-rank phase adds only the rank-order sum."""
+    engine's, the cross-rank phase adds only the rank-order sum.  split: both sides run the
+    head-split form (CartPole) or both the 8-wave kernel."""
+    if cont and split == 0:
+        pytest.skip("the split setting applies to the two-head CartPole shape only")
+    with _split(split):
+        _dpx_one_rank_equals_engine(cont)
+
+
+def _dpx_one_rank_equals_engine(cont):
     import prl_native
     from PPO import PPO
     N = 3000 + 7
@@ -597,7 +625,8 @@ def test_throughput_form_equals_latency_form(cont, mb, N):
     moments streamed through the workspace by the slice owners), at one tile per workgroup
     (mb 512, the form forced), two (mb 8192) and sixteen (mb 65536, ragged last minibatch).
     CartPole: both run the 8-wave kernel with the same tiles, order and per-tile sums, so
-    parameters, moments, step count and loss are the same BITS.  Pendulum: the throughput form
+    parameters, moments, step count and loss are the same BITS (the head-split latency form is
+    off here; test_split_form_matches_8wave_form covers it).  Pendulum: the throughput form
     runs 8 waves (the latency form's LDS image does not fit with 8), so the clip norm is summed
     in another order (and dW1 accumulates across tiles in the MFMA): float32 rounding apart,
     checked on the learned function (log-probs / values on probe states, rtol 1e-4) and the
@@ -622,6 +651,7 @@ def test_throughput_form_equals_latency_form(cont, mb, N):
     outs, pols = {}, {}
     for mode in (0, 1):
         prev = prl_native.ppo_update_set_tp(mode)
+        prev_split = prl_native.ppo_update_set_split(0)
         try:
             for dst, src in zip((eng.flat, eng.m, eng.v, eng.step), init):
                 dst.copy_(src)
@@ -633,6 +663,7 @@ def test_throughput_form_equals_latency_form(cont, mb, N):
             pols[mode] = types.SimpleNamespace(policy=copy.deepcopy(p.policy))
         finally:
             prl_native.ppo_update_set_tp(prev)
+            prl_native.ppo_update_set_split(prev_split)
     assert not torch.equal(outs[0][0], init[0].cpu())
     names = ("params", "exp_avg", "exp_avg_sq", "step", "loss")
     if not cont:
@@ -675,6 +706,7 @@ def test_replicated_tiles_equal_single(cont, mb, N):
     outs = {}
     for x in (1, 2, 3, 4, 8):
         prev = prl_native.ppo_update_set_repl(x)
+        prev_split = prl_native.ppo_update_set_split(0)   # replicas are the 8-wave form's
         try:
             for dst, src in zip((eng.flat, eng.m, eng.v, eng.step), init):
                 dst.copy_(src)
@@ -688,8 +720,62 @@ def test_replicated_tiles_equal_single(cont, mb, N):
             outs[x] = [t.cpu().clone() for t in (eng.flat, eng.m, eng.v, eng.step, loss)]
         finally:
             prl_native.ppo_update_set_repl(prev)
+            prl_native.ppo_update_set_split(prev_split)
     assert not torch.equal(outs[1][0], init[0].cpu())
     names = ("params", "exp_avg", "exp_avg_sq", "step", "loss")
     for x in (2, 3, 4, 8):
         for a, b, name in zip(outs[1], outs[x], names):
             assert torch.equal(a, b), (x, name, float((a.double() - b.double()).abs().max()))
+
+
+@pytest.mark.parametrize("mb,N", [(512, 512 * 6 + 7), (64, 700), (1000, 1000 * 3 + 1),
+                                  (2048, 2048 * 2 + 33)])
+def test_split_form_matches_8wave_form(mb, N):
+    """The head-split latency form (csrc/prl_ppo_split.h: actor and critic head of a 16-row tile
+    on two workgroups, 2 Gt workgroups of 4 waves) against the 8-wave kernel, from the same state
+    on the same learn() inputs: the trunk gradient is summed per head and then across heads in
+    float64 (not inside one MFMA chain), so the two agree to float32 rounding — the learned
+    function (probe log-probs / values, rtol 1e-4), weights (3e-5), moments (1e-3 relative),
+    step count and loss.  mb 64 / 1000 / 2048: few tile groups, a ragged tile group (1000 =
+    62 x 16 + 8) and the largest grid that fits (2 x 128 workgroups)."""
+    import copy
+    import types
+
+    import prl_native
+    from PPO import PPO
+    data = _data(N, 4, False, seed=53)
+    torch.manual_seed(0)
+    p = PPO(False, 4, 2, k_epochs=2, batch_size=64, mini_batch_size=mb)
+    p.show_progress = False
+    eng = p._fused_engine()
+    init = [eng.flat.clone(), eng.m.clone(), eng.v.clone(), eng.step.clone()]
+    p.memory.push_device(*data)
+    p.learn()
+    torch.cuda.synchronize()
+    ins = [x.clone() for x in p._last_update_inputs]
+    Gt = -(-mb // 16)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    outs, pols = {}, {}
+    for mode in (0, 1):
+        with _split(mode):
+            for dst, src in zip((eng.flat, eng.m, eng.v, eng.step), init):
+                dst.copy_(src)
+            eng.ws.fill_(0)
+            loss = eng.run(*ins, 2)
+            torch.cuda.synchronize()
+            plan = prl_native.ppo_update_last_plan()
+            assert plan["form"] == "latency" and plan["split"] == bool(mode and 2 * Gt <= cus), plan
+            if plan["split"]:
+                assert plan["waves"] == 4 and plan["grid"] == 2 * Gt, plan
+            outs[mode] = [t.cpu().clone() for t in (eng.flat, eng.m, eng.v, eng.step, loss)]
+            pols[mode] = types.SimpleNamespace(policy=copy.deepcopy(p.policy))
+    assert not torch.equal(outs[1][0], init[0].cpu())
+    _compare_function(pols[0], pols[1], data, rtol=1e-4)
+    worst = float((outs[0][0] - outs[1][0]).abs().max())
+    assert worst <= ATOL, worst
+    for k in (1, 2):
+        a, b = outs[0][k].double(), outs[1][k].double()
+        assert float((a - b).abs().max()) <= 1e-3 * float(a.abs().max()) + 1e-12, k
+    assert torch.equal(outs[0][3], outs[1][3])
+    assert abs(float(outs[0][4]) - float(outs[1][4])) <= 1e-4 * max(1.0, abs(float(outs[0][4])))
+

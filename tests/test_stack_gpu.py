@@ -134,6 +134,68 @@ def test_device_worker_bit_exact_vs_oracle_worker(E):
     assert len(stub.memory) == n + len(stub.memory._segments[1][0])
 
 
+@pytest.mark.parametrize("E", [1, 2048, 65536])
+def test_cartpole_persistent_rollout_matches_oracle_given_its_probs(E):
+    """The whole CartPole rollout as one launch (prl_cartpole_rollout: one thread per env runs
+    the actor's forward, Categorical sampling, the float64 step and the trajectory push to the end
+    of its episode), through AsyncPPO.worker() with the real policy.  Its forward sums in another
+    order than the per-step path's PyTorch GEMMs, so the check is: (1) its probabilities at t = 0
+    against a float64 forward of policy_old (1e-5), and (2) given the probabilities it sampled
+    from at every step (probs_out), the oracle worker (AsyncPPO.py:117-146 with the oracle's
+    Philox sampling and gymnasium 1.1.1 physics) reproduces the memory bit for bit — states,
+    actions, rewards, done flags, lengths and the score counters."""
+    import copy
+
+    import prl_native
+    from AsyncTools.AsyncPPO import AsyncPPO
+    from PPO import PPO
+    torch.manual_seed(3)
+    seed = 5
+    ppo = PPO(False, 4, 2)
+    ppo.show_progress = False
+    T = 500
+    probs = torch.zeros(T, E, 2, dtype=torch.float32, device="cuda")
+    calls = []
+    orig = prl_native.wide_rollout
+
+    def wrapped(kind, flat, D, A, discrete, phys, t, term, scaling, sd, t_max, *rest):
+        calls.append(kind)
+        prl_native.cartpole_rollout(flat, phys, t, term, sd, t_max, *rest, probs_out=probs)
+
+    a = AsyncPPO("CartPole-v1", ppo, num_envs=E, seed=seed)
+    S0 = None
+    prl_native.wide_rollout = wrapped
+    try:
+        n = a.worker()
+    finally:
+        prl_native.wide_rollout = orig
+    assert calls == [prl_native.ENV_KINDS["CartPole-v1"]]
+    S, A, R, Dn = (x.cpu().numpy() for x in ppo.memory.device_tensors("cuda"))
+    P = probs.cpu().numpy()
+    orc = O.CartPoleOracle(E)
+    orc.seed(np.arange(E) + seed)
+    ss = a.sample_seed
+    first = {}
+
+    def act(states, idx, t):
+        if t == 0:
+            first["S"] = states.copy()
+        return O.sample_categorical(P[t], ss, np.full(E, t, np.int32))[idx]
+
+    ref = O.worker_oracle(orc, act)
+    assert n == len(ref["S"]) == int(a.step_score)
+    np.testing.assert_array_equal(S, ref["S"])
+    np.testing.assert_array_equal(A, ref["A"])
+    np.testing.assert_array_equal(R, ref["R"])
+    np.testing.assert_array_equal(Dn, ref["D"])
+    assert float(a.reward_score) == float(ref["reward_score"])
+    # (1) the probabilities at t = 0 against a float64 forward of policy_old
+    pol = copy.deepcopy(ppo.policy_old).cpu().double()
+    with torch.no_grad():
+        p64 = pol.actor(pol.model(torch.from_numpy(first["S"]).double())).numpy()
+    np.testing.assert_allclose(P[0].astype(np.float64), p64, rtol=0, atol=1e-5)
+
+
 def test_evaluate_matches_oracle_episodes():
     """AsyncPPO.evaluate() (Test.py:19-35 batched, no render): per-env episode returns and
     lengths equal the oracle's replay of the same rollout (same PCG64 resets, the evaluation's
@@ -362,6 +424,9 @@ def test_graphed_rollout_equals_eager_rollout(env, cont, step_at, monkeypatch):
     into active_after[k] and advances k itself (prl_rollout_step_at); "0": round 3's scalar +
     index copy + increment nodes (PRL_ROLLOUT_STEP_AT=0)."""
     monkeypatch.setenv("PRL_ROLLOUT_STEP_AT", step_at)
+    # the per-step path (CartPole's real policy otherwise runs the one-launch rollout,
+    # test_cartpole_persistent_rollout_matches_oracle_given_its_probs)
+    monkeypatch.setenv("PRL_CP_ROLLOUT", "0")
     from AsyncTools.AsyncPPO import AsyncPPO
     from PPO import PPO
     outs = []

@@ -47,7 +47,7 @@ def _worker(rank, world, port, n, out):
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 if name == "dpx":
-                    eng.run_dp_persistent(*data, k, [n] * world)
+                    eng.run_dp_persistent(*data, k, [n] * world, p.all_reduce)
                 elif rank == 0:   # the single-GPU engine alone (the other ranks wait)
                     eng.run(*data, k)
                 e.record()
