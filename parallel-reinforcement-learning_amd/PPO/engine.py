@@ -263,6 +263,10 @@ class FusedUpdate:
         tdist.all_gather_object(handles, (handle, kind))
         # the flags are fenced when ANY rank's buffer is fine-grained (prl_ppo_update_dpx)
         self._dp_fine = any(k == "fine" for _, k in handles)
+        # the push form of the exchange (PRL_DP_PUSH=1) only when every rank asks for it
+        push = [None] * world
+        tdist.all_gather_object(push, os.environ.get("PRL_DP_PUSH", "0") == "1")
+        self._dp_push = all(push)
         self.dp_xbuf_kinds = [k for _, k in handles]
         handles = [h for h, _ in handles]
         ptrs, ok = [], all(len(h) > 0 for h in handles)
@@ -323,7 +327,7 @@ class FusedUpdate:
                 inv, self.ppo.policy_clip, self.ppo.value_coef, self.ppo.entropy_coef,
                 group["lr"], group["betas"][0], group["betas"][1], group["eps"],
                 group["weight_decay"], 2.0, loss, world, self._dp_rank, self._xbufs,
-                self._dp_seq, self.ws, fine_grained=self._dp_fine)
+                self._dp_seq, self.ws, fine_grained=self._dp_fine, push=self._dp_push)
             self._dp_seq += 2
             torch.cuda.synchronize()
             status = max(prl_native.ppo_update_status(self.ws).tolist())
@@ -375,7 +379,7 @@ class FusedUpdate:
                 ret.contiguous(), mb, k_epochs, nb, inv, self.ppo.policy_clip,
                 self.ppo.value_coef, self.ppo.entropy_coef, group["lr"], beta1, beta2,
                 group["eps"], group["weight_decay"], 2.0, self.loss, world, self._dp_rank, xb,
-                self._dp_seq, self.ws, fine_grained=self._dp_fine)
+                self._dp_seq, self.ws, fine_grained=self._dp_fine, push=self._dp_push)
             launch_error = None
         except (RuntimeError, ValueError) as e:
             # this rank did not launch (e.g. an argument check): it still joins the gather

@@ -31,19 +31,28 @@
 // order than the 8-wave kernel's (per head, then across heads in float64), so the two forms
 // agree to float32 rounding, not bit for bit (tests/test_engine_gpu.py::test_split_*).
 
-constexpr int SPL_NW = 4, SPL_NT = 64 * SPL_NW;
+// SPL_NW waves run the tile (wave w = channel block w); the kernel has TW = 4 or 8 waves: with
+// 8, waves 4-7 only join the tile's barriers and add their threads to the publish, phase B's
+// loads and phase C (PRL_UPD_SPL_WAVES; A/B)
+constexpr int SPL_NW = 4;
 
 // one 16-row tile of role r = head h (h = r): forward (trunk + head h), the head's loss, its
 // backward through the trunk; the gradient into the LDS image Ga (first tile of the step: every
 // entry the role publishes is stored, never accumulated, since a split workgroup runs ONE tile
 // per step).  Three workgroup barriers.
-template <int KA>
+template <int KA, int TW>
 __device__ __forceinline__ void spl_tile(const UpdNet& n, const UpdArgs& args, int h, const float* W,
                                          float* Ga, const UpdScr& sc, const UpdIn<upd_ksm<KA>()>& in,
                                          int rc, float invB, unsigned long long* tm, bool direct,
                                          __amdgpu_buffer_rsrc_t rs_mypart) {
   constexpr int KSM = upd_ksm<KA>();
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
+  if (TW > SPL_NW && w >= SPL_NW) {   // the tile's three barriers, nothing else
+    __syncthreads();
+    __syncthreads();
+    __syncthreads();
+    return;
+  }
   const int b = w;
   const int D = n.D, KS = (D + 3) >> 2;
   const bool timer = args.profile && blockIdx.x == 0 && t == 0;
@@ -312,10 +321,12 @@ __device__ inline void spl_sum_partials(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
 // trunk quads [0, QT) and the loss quad Qp also over part2 (role 1's trunk partials,
 // [Gt][QT + 1] quads).  Per quad: part[0 .. Gt) then part2[0 .. Gt) in the order sub,
 // sub + spl, ... for each of spl threads, combined in sub order (deterministic).
+template <int NT, bool PC>
 __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_part2,
                                         __amdgpu_buffer_rsrc_t rs_red, int Qtot, int Qp, int QT, int g,
                                         int G, int Gt, float* scratch, bool sys, int fill,
-                                        UpdSub sub) {
+                                        UpdSub sub, __amdgpu_buffer_rsrc_t rs_sq, const UpdArgs& args,
+                                        int par) {
   const int t = threadIdx.x;
   const int qlo = spl_slice_start(g, G, Qp, QT), qhi = spl_slice_start(g + 1, G, Qp, QT);
   const int nq = qhi - qlo;
@@ -323,12 +334,23 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
   const int P2 = QT + 1;
   auto fin = [&](int q, double ax, double ay, double az, double aw) {
     const float4 r = float4{(float)ax, (float)ay, (float)az, (float)aw};
-    if (sys) st4_aux<UPD_AUX_SYS>(rs_red, (size_t)q * 4, r);   // data-parallel: the rank's slice buffer
-    else st4_sc1(rs_red, (size_t)q * 4, r);
+    if (sys && args.dp_push) {
+      // push form: straight into every rank's receive slot [par][this rank] (upd_dp_union_slice_push)
+#pragma unroll
+      for (int rr = 0; rr < UPD_MAX_RANKS; ++rr)
+        if (rr < args.world)
+          st4_aux<UPD_AUX_SYS>(upd_rsrc(args.xbuf[rr] + args.xpush_off +
+                                        ((size_t)par * UPD_MAX_RANKS + args.rank) * Qtot * 4),
+                               (size_t)q * 4, r);
+    } else if (sys) {
+      st4_aux<UPD_AUX_SYS>(rs_red, (size_t)q * 4, r);   // data-parallel: the rank's slice buffer
+    } else {
+      st4_sc1(rs_red, (size_t)q * 4, r);
+    }
   };
-  if (2 * nq > SPL_NT) {
+  if (2 * nq > NT) {
     // wide slices (few workgroups, small minibatches): each thread owns whole quads
-    for (int q = qlo + t; q < qhi; q += SPL_NT) {
+    for (int q = qlo + t; q < qhi; q += NT) {
       double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
       const bool dual = q < QT || q == Qp;
       spl_sum_partials(rs_part, rs_part2, Qtot, P2, q, q < QT ? q : QT, 0, 1, Gt, dual ? 2 * Gt : Gt,
@@ -340,9 +362,9 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
   // spl threads per quad, each summing every spl-th partial: a power of two (fill 0), or as
   // many as the 256 threads allow (fill 1: more loads in flight; the slice loads are latency-bound)
   int spl = 1;
-  if (fill) spl = std::max(1, std::min(Gt, SPL_NT / nq));
+  if (fill) spl = std::max(1, std::min(Gt, NT / nq));
   else
-    while (spl * 2 * nq <= SPL_NT && spl * 2 <= Gt) spl *= 2;
+    while (spl * 2 * nq <= NT && spl * 2 <= Gt) spl *= 2;
   double* red = reinterpret_cast<double*>(scratch);   // [spl][nq][4]
   if (t < spl * nq) {
     const int qi = t % nq, sb = t / nq, q = qlo + qi;
@@ -355,6 +377,7 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
   }
   sub.mark(0);   // thread 0's partial loads landed and summed
   __syncthreads();
+  float sq = 0.f;
   if (t < nq) {
     double ax = red[4 * t], ay = red[4 * t + 1], az = red[4 * t + 2], aw = red[4 * t + 3];
     for (int k = 1; k < spl; ++k) {
@@ -362,6 +385,20 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
       ax += o[0]; ay += o[1]; az += o[2]; aw += o[3];
     }
     fin(qlo + t, ax, ay, az, aw);
+    if (PC && qlo + t < Qp) {
+      const float4 r = float4{(float)ax, (float)ay, (float)az, (float)aw};
+      sq = (r.x * r.x + r.y * r.y) + (r.z * r.z + r.w * r.w);
+    }
+  }
+  if constexpr (PC) {
+    // clip_grad_norm_'s piece of this slice: the sum of squares of its parameter quads as
+    // stored (float32), over wave 0's owner lanes in one DPP tree (the host enables the form
+    // only when every slice has <= 64 quads), stored 16-B sc1 on a 64-B line of its own by lane
+    // 63 beside the slice's stores, so the same drain covers both
+    if (t < 64) {
+      sq = wave_sum_f32_to63(sq);
+      if (t == 63) st4_sc1(rs_sq, (size_t)g * 16, float4{sq, 0.f, 0.f, 0.f});
+    }
   }
   sub.mark(1);   // slice combined, its stores issued
 }
@@ -371,8 +408,13 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
 // DP: data-parallel ranks (prl_ppo_update_dpx): union-minibatch row weights inv_count[j] and,
 // after phase B, the cross-rank sum of each slice (upd_dp_union_slice, as the 8-wave kernel);
 // the 2 Gt workgroups of every rank cut the gradient into the same 2 Gt slices.
-template <int NQC, int KA, bool DP>
+// PC (single GPU only): clip_grad_norm_ from the slice owners' pieces (spl_slice_reduce) — phase
+// C loads the G pieces and only this role's OWNED quads of the reduced gradient (NQC then
+// counts owned slots: ceil(owned quads / threads)) instead of every quad.
+template <int NQC, int KA, bool DP, int TW, bool PC = false>
 __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& args) {
+  constexpr int SPL_NT = 64 * TW;
+  static_assert(!(PC && DP), "the norm pieces cover one rank's reduced gradient only");
   extern __shared__ __align__(16) float upd_lds[];
   const int t = threadIdx.x, g = blockIdx.x, G = args.G, Gt = args.Gt;
   const int role = g / Gt, gt = g - role * Gt;   // role = the head this workgroup runs
@@ -381,6 +423,18 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   const int QH = n.w1[1].lds / 4;   // head 0: [QT, QH), head 1: [QH, Qp)
   // owned quads: the trunk and this role's head (the only parameters its tile reads)
   auto owned = [&](int q) { return role == 0 ? q < QH : (q < QT || q >= QH); };
+  // slot i of this thread: the quad its moments / AdamW cover (-1: none).  Canonical sweep
+  // (quads t + NT i, owned ones only) or, with PC, the owned quads packed: role 0 [0, QH),
+  // role 1 [0, QT) then [QH, Qp)
+  auto slotq = [&](int i) {
+    const int o = t + i * SPL_NT;
+    if constexpr (PC) {
+      const int q = role == 0 ? o : (o < QT ? o : o - QT + QH);
+      return (role == 0 ? q < QH : q < Qp) ? q : -1;
+    } else {
+      return (o < Qp && owned(o)) ? o : -1;
+    }
+  };
   float* hdr = upd_lds;
   float* scratch = upd_lds + UPD_HDR;
   const int scr_floats = (upd_scratch_floats(n.D, SPL_NW, upd_ts(n)) + 3) & ~3;
@@ -395,8 +449,8 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(args.params + 4 * q);
 #pragma unroll
   for (int i = 0; i < NQC; ++i) {
-    const int q = t + i * SPL_NT;
-    const bool own = q < Qp && owned(q);
+    const int q = slotq(i);
+    const bool own = q >= 0;
     mreg[i] = own ? *reinterpret_cast<const float4*>(args.exp_avg + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
     vreg[i] = own ? *reinterpret_cast<const float4*>(args.exp_avg_sq + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
   }
@@ -456,7 +510,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       // arguments, see the engine's load_next)
       upd_tile_load<1, KA, true>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
                                  first_row(s + 1), std::min(UPD_RT, first_rows(s + 1)), nin);
-      spl_tile<KA>(n, args, role, W, Ga, sc, cur, myrows, invB, tm, direct, rs_mypart);
+      spl_tile<KA, TW>(n, args, role, W, Ga, sc, cur, myrows, invB, tm, direct, rs_mypart);
     } else {
       for (int k = t; k < Lp + 4; k += SPL_NT) Ga[k] = 0.0f;
       upd_tile_load<1, KA, true>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
@@ -486,7 +540,8 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     mark(1);   // publish
     if (t < 64) {
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_A, g);
-      const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));
+      const bool ok = args.spl_poll ? upd_wait_sharded_pipe(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1))
+                                    : upd_wait_sharded(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));
       if (t == 0) *s_abort = ok ? 0 : 1;
     } else if (t == 64) {
       const double tstep = (double)step0 + (double)(s + 1);
@@ -502,18 +557,23 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     {
       const unsigned long long gstep = args.dp_seq0 + (unsigned long long)s;
       const int par = (int)(gstep & 1ull);
-      spl_slice_reduce(rs_part, rs_part2, DP ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
-                       Qtot, Qp, QT, g, G, Gt, scratch, DP, args.spl_fill, subm);
+      spl_slice_reduce<SPL_NT, PC>(rs_part, rs_part2, DP ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
+                       Qtot, Qp, QT, g, G, Gt, scratch, DP, args.spl_fill, subm, upd_rsrc(args.sq),
+                       args, par);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (DP && !upd_dp_union_slice(args, rs_red, Qtot, g, G, gstep, par, s_abort,
-                                    spl_slice_start(g, G, Qp, QT), spl_slice_start(g + 1, G, Qp, QT)))
-        return;
+      if (DP) {
+        const int qlo = spl_slice_start(g, G, Qp, QT), qhi = spl_slice_start(g + 1, G, Qp, QT);
+        if (!(args.dp_push ? upd_dp_union_slice_push(args, rs_red, Qtot, g, gstep, par, s_abort, qlo, qhi)
+                           : upd_dp_union_slice(args, rs_red, Qtot, g, G, gstep, par, s_abort, qlo, qhi)))
+          return;
+      }
     }
     mark(3);   // slice reduce
     if (t < 64) {
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_B, g);
-      const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_B, (unsigned)G * (unsigned)(s + 1));
+      const bool ok = args.spl_poll ? upd_wait_sharded_pipe(args.ctr, UPD_CTR_B, (unsigned)G * (unsigned)(s + 1))
+                                    : upd_wait_sharded(args.ctr, UPD_CTR_B, (unsigned)G * (unsigned)(s + 1));
       if (t == 0) *s_abort = ok ? 0 : 1;
     }
     __syncthreads();
@@ -521,11 +581,38 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     mark(4);   // wait B
     // ---- phase C: the norm in the canonical order, then AdamW on the owned quads -------------
     float4 gq[NQC];
-#pragma unroll
-    for (int i = 0; i < NQC; ++i)
-      if (i * SPL_NT < Qp) gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
     float clipc;
-    {
+    if constexpr (PC) {
+      // this role's owned quads, and the G pieces: lane l sums pieces l, l + 64, ... in that
+      // order, then the wave's DPP tree — the same data, order and code in every wave of every
+      // workgroup, so every copy forms the same coefficient
+#pragma unroll
+      for (int i = 0; i < NQC; ++i) {
+        const int q = slotq(i);
+        gq[i] = ld4_sc1(rs_red, (size_t)(q >= 0 ? q : 0) * 4);
+      }
+      const int l = t & 63;
+      const __amdgpu_buffer_rsrc_t rs_sq = upd_rsrc(args.sq);
+      float4 pcs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) pcs[u] = ld4_sc1(rs_sq, (size_t)(l + 64 * u < G ? l + 64 * u : 0) * 16);
+      float pc = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (l + 64 * u < G) pc += pcs[u].x;
+      subm.mark(2);   // thread 0's pieces landed
+      const float tot = __builtin_amdgcn_readlane(wave_sum_f32_to63(pc), 63);
+      const float coef = args.max_norm / (sqrtf(tot) + 1e-6f);
+      clipc = coef < 1.0f ? coef : 1.0f;
+      if (args.profile && g == 0 && t == 0 && coef < 1.0f) tm[20] += 1ull;
+      if (g == 0 && t == 0 && s + 1 == args.total_steps) {
+        const float4 lpq = ld4_sc1(rs_red, (size_t)Qp * 4);
+        loss_last = lpq.x * invB + args.vf_coef * (lpq.y * invB) - args.ent_coef * (lpq.z * invB);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NQC; ++i)
+        if (i * SPL_NT < Qp) gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
       float acc = 0.f;
 #pragma unroll
       for (int i = 0; i < NQC; ++i)
@@ -538,7 +625,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       __syncthreads();
       float tot = 0.f;
 #pragma unroll
-      for (int w = 0; w < SPL_NW; ++w) tot += s_nrm[w];
+      for (int w = 0; w < TW; ++w) tot += s_nrm[w];
       const float coef = args.max_norm / (sqrtf(tot) + 1e-6f);
       clipc = coef < 1.0f ? coef : 1.0f;
       if (args.profile && g == 0 && t == 0 && coef < 1.0f) tm[20] += 1ull;
@@ -556,8 +643,8 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       const float omb1 = (float)(1.0 - (double)args.beta1), omb2 = (float)(1.0 - (double)args.beta2);
 #pragma unroll
       for (int i = 0; i < NQC; ++i) {
-        const int q = t + i * SPL_NT;
-        if (i * SPL_NT < Qp && q < Qp && owned(q)) {
+        const int q = slotq(i);
+        if (q >= 0) {
           float4 pw = *reinterpret_cast<float4*>(W + 4 * q);
           float4 m4 = mreg[i], v4 = vreg[i];
           const float4 g4 = gq[i];
@@ -589,8 +676,8 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   // ---- write back: role 0's first workgroup the trunk + head 0, role 1's the critic head ------
   if (gt == 0) {
     for (int i = 0; i < NQC; ++i) {
-      const int q = t + i * SPL_NT;
-      if (q < Qp && (role == 0 ? q < QH : q >= QH)) {
+      const int q = slotq(i);
+      if (q >= 0 && (role == 0 ? q < QH : q >= QH)) {
         *reinterpret_cast<float4*>(args.params + 4 * q) = *reinterpret_cast<const float4*>(W + 4 * q);
         *reinterpret_cast<float4*>(args.exp_avg + 4 * q) = mreg[i];
         *reinterpret_cast<float4*>(args.exp_avg_sq + 4 * q) = vreg[i];
@@ -608,8 +695,8 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   }
 }
 
-template <int NQC, int KA, int KDIM, bool DP = false>
-__global__ __launch_bounds__(SPL_NT, 1) void ppo_update_split_kernel(UpdArgs args) {
+template <int NQC, int KA, int KDIM, bool DP = false, int TW = 4, bool PC = false>
+__global__ __launch_bounds__(64 * TW, 1) void ppo_update_split_kernel(UpdArgs args) {
   constexpr UpdNet N = upd_make(KDIM, KA, 1);
-  ppo_split_body<NQC, KA, DP>(N, args);
+  ppo_split_body<NQC, KA, DP, TW, PC>(N, args);
 }

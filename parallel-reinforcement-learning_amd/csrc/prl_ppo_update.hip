@@ -145,6 +145,7 @@ struct UpdArgs {
   float* part2;     // head-split form: role 1's trunk + loss-partial quads [Gt][QT + 1][4]
   int spl_fill;     // head-split form's phase B: threads per quad (PRL_UPD_SPL_FILL, A/B)
   int spl_direct;   // head-split form: dW1 stored from registers into the partial (PRL_UPD_SPL_DIRECT)
+  int spl_poll;     // head-split form: counter waits with four polls in flight (PRL_UPD_SPL_POLL)
   float* red;       // [Qtot * 4]
   float* sq;        // [NW G] per-wave squared-norm pieces of the slices
   unsigned* ctr;    // [0] arrivals A, [1] arrivals B, [2] abort, [3] status (zeroed per launch),
@@ -162,6 +163,12 @@ struct UpdArgs {
   unsigned long long* xflag[UPD_MAX_RANKS];   // rank r's [G] per-workgroup step flags
   float* xbuf_self;                       // == xbuf[rank] (no dynamic kernarg indexing)
   unsigned long long* xflag_self;         // == xflag[rank]
+  // push form of the cross-rank exchange (dp_push, head-split kernel): every rank's buffer also
+  // holds receive slices [2 parity][UPD_MAX_RANKS][Qtot][4] f32 at float offset xpush_off and
+  // receive flags [UPD_MAX_RANKS][xpush_gmax] u64 at u64 offset xpush_flags_off
+  int dp_push;
+  size_t xpush_off, xpush_flags_off;
+  int xpush_gmax;
   float *tp_m0, *tp_v0, *tp_m1, *tp_v1;   // the throughput form's moment buffers (image layout)
 };
 
@@ -261,6 +268,52 @@ __device__ inline bool upd_wait_sharded(unsigned* ctr, int base, unsigned target
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// upd_wait_sharded with FOUR polls in flight: a poll is re-issued as soon as the oldest one is
+// checked, so a counter reaching its target is seen about a quarter of a poll round trip after
+// it lands instead of up to a whole one (every check waits only for its own load: the compiler's
+// counted vmcnt).  Same words, same abort / timeout handling.
+__device__ inline unsigned upd_poll8(unsigned* ctr, int base, int l) {
+  return l < UPD_SHARDS ? ld_sc1u(ctr + base + 32 * l) : (l == UPD_SHARDS ? ld_sc1u(ctr + 2) : 0u);
+}
+__device__ inline int upd_poll_check(unsigned v, int l, unsigned target) {
+  const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)upd_isum8(l < UPD_SHARDS ? v : 0u), 0);
+  if (tot >= target) return 1;
+  if ((unsigned)__builtin_amdgcn_readlane((int)v, UPD_SHARDS) != 0u) return -1;
+  return 0;
+}
+__device__ inline bool upd_wait_sharded_pipe(unsigned* ctr, int base, unsigned target) {
+  const int l = threadIdx.x & 63;
+  unsigned v0 = upd_poll8(ctr, base, l);
+  __builtin_amdgcn_s_sleep(1);
+  unsigned v1 = upd_poll8(ctr, base, l);
+  __builtin_amdgcn_s_sleep(1);
+  unsigned v2 = upd_poll8(ctr, base, l);
+  __builtin_amdgcn_s_sleep(1);
+  unsigned v3 = upd_poll8(ctr, base, l);
+  for (unsigned spins = 0;; spins += 4) {
+    int c = upd_poll_check(v0, l, target);
+    if (c) return c > 0;
+    v0 = upd_poll8(ctr, base, l);
+    c = upd_poll_check(v1, l, target);
+    if (c) return c > 0;
+    v1 = upd_poll8(ctr, base, l);
+    c = upd_poll_check(v2, l, target);
+    if (c) return c > 0;
+    v2 = upd_poll8(ctr, base, l);
+    c = upd_poll_check(v3, l, target);
+    if (c) return c > 0;
+    v3 = upd_poll8(ctr, base, l);
+    if (spins > UPD_SPIN_LIMIT) {
+      if (l == 0) {
+        __hip_atomic_store(upd_g(ctr + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(upd_g(ctr + 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_or(upd_g(ctr + 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky
+      }
+      return false;
+    }
   }
 }
 
@@ -1543,6 +1596,86 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
   return true;
 }
 
+// The PUSH form of the cross-rank step (dp_push; the head-split kernel's data-parallel form):
+// phase B has already stored this workgroup's slice into EVERY rank's receive slot
+// [par][this rank] (system-scope stores, drained by the caller); one lane now raises this
+// workgroup's flag in every rank's receive flags [this rank][g] (remote writes are posted: one
+// one-way trip over xGMI instead of the pull form's remote poll + remote slice read), then a wave
+// polls its OWN buffer's flags [r][g] for every rank r (local loads) and the slices are summed
+// from local memory in rank order into red.  Ordering as the pull form: system-scope stores
+// drained before the flag store, system-scope loads after the matched poll, a system-scope
+// release / acquire around them when any buffer is fine-grained.  Reuse of a receive slot: rank
+// r rewrites [par][r] two steps later, after every rank raised the flag of the step between,
+// i.e. finished reading this one.
+__device__ bool upd_dp_union_slice_push(const UpdArgs& args, __amdgpu_buffer_rsrc_t rs_red, int Qtot,
+                                        int g, unsigned long long gstep, int par, int* s_abort,
+                                        int qlo, int qhi) {
+  const int t = threadIdx.x, NT = blockDim.x;
+  const unsigned long long want = gstep + 1ull;
+  if (t == 0) {
+    if (args.dp_fine) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#pragma unroll
+    for (int r = 0; r < UPD_MAX_RANKS; ++r) {
+      if (r < args.world) {
+        unsigned long long* fl = reinterpret_cast<unsigned long long*>(args.xbuf[r]) + args.xpush_flags_off +
+                                 (size_t)args.rank * args.xpush_gmax + g;
+        __hip_atomic_store(upd_g(fl), want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  if (t < 64) {
+    const unsigned long long* fl = reinterpret_cast<const unsigned long long*>(args.xbuf_self) +
+                                   args.xpush_flags_off + (size_t)(t < UPD_MAX_RANKS ? t : 0) * args.xpush_gmax + g;
+    bool ok = true;
+    for (unsigned spins = 0;; ++spins) {
+      const bool ready = t >= args.world ||
+                         __hip_atomic_load(upd_g(fl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= want;
+      const unsigned ab = t == 63 ? ld_sc1u(args.ctr + 2) : 0u;
+      if (__ballot(!ready) == 0ull) break;
+      if ((unsigned)__builtin_amdgcn_readlane((int)ab, 63) != 0u) { ok = false; break; }
+      if (spins > args.dp_spin_limit) {
+        if (t == 0) {
+          __hip_atomic_store(upd_g(args.ctr + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(upd_g(args.ctr + 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_or(upd_g(args.ctr + 4), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (t == 0) *s_abort = ok ? 0 : 1;
+    if (args.dp_fine && ok) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (*s_abort) return false;
+  const __amdgpu_buffer_rsrc_t rs_rx = upd_rsrc(args.xbuf_self + args.xpush_off +
+                                                (size_t)par * UPD_MAX_RANKS * Qtot * 4);
+  for (int q = qlo + t; q < qhi; q += NT) {
+    float4 acc = ld4_aux<UPD_AUX_SYS>(rs_rx, (size_t)q * 4);
+#pragma unroll
+    for (int r = 1; r < UPD_MAX_RANKS; ++r) {
+      if (r < args.world) {
+        const float4 x = ld4_aux<UPD_AUX_SYS>(rs_rx, ((size_t)r * Qtot + q) * 4);
+        acc.x += x.x;
+        acc.y += x.y;
+        acc.z += x.z;
+        acc.w += x.w;
+      }
+    }
+    st4_sc1(rs_red, (size_t)q * 4, acc);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  return true;
+}
+
 // NQ = parameter quads per thread (ceil(Lp / 4 / 256)): AdamW's moments live in registers.
 // DP: the data-parallel form (prl_ppo_update_dpx): union-minibatch row weights and the
 // cross-rank slice sum; a separate instantiation, so the single-GPU kernel carries none of it.
@@ -2320,11 +2453,16 @@ int g_split = [] {
   const char* e = getenv("PRL_UPD_SPLIT");
   return (e && e[0] == '0') ? 0 : 1;
 }();
-// Quads per thread of the split kernel's phase-C sweep that are instantiated
-constexpr int SPL_NQC = 10;
+// Quads per thread of the split kernel's phase-C sweep that are instantiated (4 / 8 waves)
+constexpr int SPL_NQC = 10, SPL_NQC8 = 5;
+// PRL_UPD_SPL_WAVES=8: the split kernel's 8-wave form (waves 4-7 in the exchange phases only)
+int upd_split_waves() {
+  const char* e = getenv("PRL_UPD_SPL_WAVES");
+  return (e && e[0] == '8') ? 8 : 4;
+}
 bool upd_split_host(const UpdNet& n, int Gt, int R, bool tp) {
   if (tp || !g_split || upd_force_generic() || !upd_is_cartpole(n) || R != UPD_RT) return false;
-  if (cdiv(n.Lp / 4, SPL_NT) > SPL_NQC) return false;
+  if (cdiv(n.Lp / 4, 64 * upd_split_waves()) > (upd_split_waves() == 8 ? SPL_NQC8 : SPL_NQC)) return false;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -2429,8 +2567,19 @@ struct UpdDp {
   int64_t seq0;
   int fine;
 };
-// the slice buffers [2][Qtot * 4] f32, then the per-workgroup step flags [G] u64
+// the slice buffers [2][Qtot * 4] f32, then the per-workgroup step flags [2 G] u64 (pull form);
+// then the push form's receive slices [2][UPD_MAX_RANKS][Qtot * 4] f32 and receive flags
+// [UPD_MAX_RANKS][2 G] u64 (G = upd_grid(mini_batch); two workgroups per tile group at most)
 size_t upd_xbuf_flags_off(const UpdNet& n) { return (((size_t)n.Lp / 4 + 1) * 32 + 255) & ~(size_t)255; }
+size_t upd_xbuf_push_off(const UpdNet& n, int mb) {
+  return (upd_xbuf_flags_off(n) + 2 * (size_t)upd_grid(mb) * 8 + 255) & ~(size_t)255;
+}
+size_t upd_xbuf_push_flags_off(const UpdNet& n, int mb) {
+  return upd_xbuf_push_off(n, mb) + (size_t)2 * UPD_MAX_RANKS * ((size_t)n.Lp / 4 + 1) * 16;
+}
+size_t upd_xbuf_bytes(const UpdNet& n, int mb) {
+  return upd_xbuf_push_flags_off(n, mb) + (size_t)UPD_MAX_RANKS * 2 * upd_grid(mb) * 8;
+}
 unsigned g_dp_spin_limit = UPD_DP_SPIN_LIMIT;
 int32_t g_last_plan[7] = {-1, -1, -1, -1, -1, -1, -1};   // prl_ppo_update_last_plan
 
@@ -2501,7 +2650,11 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     args.inv_count = dp->inv_count;
     args.dp_seq0 = (unsigned long long)dp->seq0;
     args.dp_spin_limit = g_dp_spin_limit;
-    args.dp_fine = dp->fine ? 1 : 0;
+    args.dp_fine = (dp->fine & 1) ? 1 : 0;
+    args.dp_push = (dp->fine & 2) ? 1 : 0;
+    args.xpush_off = upd_xbuf_push_off(args.net, mini_batch) / 4;
+    args.xpush_flags_off = upd_xbuf_push_flags_off(args.net, mini_batch) / 8;
+    args.xpush_gmax = 2 * upd_grid(mini_batch);
     const size_t fo = upd_xbuf_flags_off(args.net);
     for (int r = 0; r < dp->world; ++r) {
       PRL_REQUIRE(dp->xbufs[r], "prl_ppo_update_dpx: null slice buffer of rank %d", r);
@@ -2517,6 +2670,8 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     args.spl_fill = (e && e[0] == '0') ? 0 : 1;
     const char* d = getenv("PRL_UPD_SPL_DIRECT");
     args.spl_direct = (d && d[0] == '1') ? 1 : 0;
+    const char* pp = getenv("PRL_UPD_SPL_POLL");
+    args.spl_poll = (pp && pp[0] == '1') ? 1 : 0;
   }
   args.tp_m0 = ws.mv;
   args.tp_v0 = ws.mv + L4;
@@ -2530,10 +2685,35 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     else tp = false;
   }
   const bool split = upd_split_host(args.net, Gt, args.R, tp);
-  if (split)
-    plan = UpdPlan{dp ? reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, true>)
-                      : reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, false>),
-                   SPL_NW, 1};
+  if (!split) args.dp_push = 0;   // the push form is the head-split kernel's (ranks decide alike)
+  if (split) {
+    const int tw = upd_split_waves();
+    // PRL_UPD_SPL_PIECES=1 (single GPU, every slice <= 64 quads and narrow): the norm from the
+    // slice owners' pieces, phase C loading only the owned quads (A/B)
+    bool pieces = false;
+    {
+      const char* e = getenv("PRL_UPD_SPL_PIECES");
+      if (!dp && e && e[0] == '1') {
+        const int Qp = args.net.Lp / 4, QT = args.net.w1[0].lds / 4, Gs = 2 * Gt;
+        const int64_t U = (int64_t)Qp + QT + 2;
+        auto st = [&](int gg) {
+          const int64_t u = U * gg / Gs;
+          const int64_t q = u <= 2 * (int64_t)QT ? (u + 1) / 2 : u - QT;
+          return (int)std::min<int64_t>(q, Qp + 1);
+        };
+        int mx = 0;
+        for (int gg = 0; gg < Gs; ++gg) mx = std::max(mx, st(gg + 1) - st(gg));
+        pieces = mx <= 64 && 2 * mx <= 64 * tw && Gs <= 256;
+      }
+    }
+    const void* k = pieces ? (tw == 8 ? reinterpret_cast<const void*>(ppo_update_split_kernel<3, 2, 4, false, 8, true>)
+                                      : reinterpret_cast<const void*>(ppo_update_split_kernel<5, 2, 4, false, 4, true>)) :
+                    tw == 8 ? (dp ? reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC8, 2, 4, true, 8>)
+                                  : reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC8, 2, 4, false, 8>))
+                            : (dp ? reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, true, 4>)
+                                  : reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, false, 4>));
+    plan = UpdPlan{k, tw, 1};
+  }
   // replicated tiles: the latency form on one GPU only; the split form: two roles per tile group
   const int G = split ? 2 * Gt : ((tp || dp) ? Gt : Gt * upd_repl(Gt));
   args.G = G;
@@ -2628,8 +2808,8 @@ extern "C" uint32_t prl_dp_set_spin_limit(uint32_t polls) {
 extern "C" int64_t prl_dp_xbuf_bytes(int32_t D, int32_t A, int32_t discrete, int32_t mini_batch) {
   UpdNet net{};
   if (!upd_layout(D, A, discrete, net) || mini_batch <= 0) return -1;
-  // per-workgroup flags: the head-split form runs two workgroups per tile group
-  return (int64_t)(upd_xbuf_flags_off(net) + 2 * (size_t)upd_grid(mini_batch) * 8);
+  // pull flags for two workgroups per tile group (the head-split form) and the push form's region
+  return (int64_t)upd_xbuf_bytes(net, mini_batch);
 }
 
 extern "C" int prl_dp_xbuf_alloc(int64_t bytes, int32_t* kind, void** out) {

@@ -810,10 +810,12 @@ def dp_ipc_close(p):
 def ppo_update_dpx(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp,
                    adv, ret, mini_batch, k_epochs, nb_union, inv_count, clip, vf_coef, ent_coef,
                    lr, beta1, beta2, eps, weight_decay, max_norm, loss_out, world, rank, xbufs,
-                   seq0, workspace, fine_grained=False):
+                   seq0, workspace, fine_grained=False, push=False):
     """The persistent engine as one data-parallel rank: the cross-rank gradient sum runs inside
     the launch over the ranks' IPC-mapped slice buffers `xbufs` (rank order); fine_grained: any
-    rank's buffer is fine-grained memory (the flags are then fenced)."""
+    rank's buffer is fine-grained memory (the flags are then fenced); push: the push form of the
+    exchange (every rank writes its slice and flag into every rank's buffer and polls its own;
+    the head-split kernel only, else the pull form runs) — every rank must pass the same."""
     N = int(S.shape[0])
     arr = (ctypes.c_void_p * len(xbufs))(*[ctypes.c_void_p(getattr(x, "value", x)) for x in xbufs])
     _check(lib().prl_ppo_update_dpx(
@@ -826,7 +828,8 @@ def ppo_update_dpx(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, ac
         float(vf_coef), float(ent_coef), float(lr), float(beta1), float(beta2), float(eps),
         float(weight_decay), float(max_norm), _dev(loss_out, torch.float32, "loss_out"),
         int(world), int(rank), ctypes.cast(arr, ctypes.c_void_p), int(seq0),
-        int(bool(fine_grained)), _dev(workspace, torch.uint8, "workspace"), workspace.numel(),
+        int(bool(fine_grained)) | (int(bool(push)) << 1), _dev(workspace, torch.uint8, "workspace"),
+        workspace.numel(),
         _stream()),
         "prl_ppo_update_dpx")
 

@@ -89,10 +89,10 @@ def test_two_ranks_graphed_equal_one_process_on_the_union(tmp_path, fused):
         np.testing.assert_allclose(outs[0][key], ref[key], rtol=0, atol=2e-5, err_msg=key)
 
 
-def _dpx_worker(rank, world, port, mb, nb, k, out_dir, xbuf="auto"):
+def _dpx_worker(rank, world, port, mb, nb, k, out_dir, xbuf="auto", push=False):
     sys.path[:0] = PATHS
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PRL_DP_PERSISTENT="1",
-                      PRL_DP_XBUF=xbuf)
+                      PRL_DP_XBUF=xbuf, PRL_DP_PUSH="1" if push else "0")
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
@@ -105,9 +105,12 @@ def _dpx_worker(rank, world, port, mb, nb, k, out_dir, xbuf="auto"):
         p.learn()       # a second launch on the same slice buffers (flags carry global steps)
         torch.cuda.synchronize()
         sd = {kk: v.cpu().numpy() for kk, v in p.policy.state_dict().items()}
-        np.savez(os.path.join(out_dir, f"{'' if xbuf == 'auto' else xbuf}rank{rank}.npz"), **sd,
+        import prl_native
+        tag = ('' if xbuf == 'auto' else xbuf) + ('push' if push else '')
+        np.savez(os.path.join(out_dir, f"{tag}rank{rank}.npz"), **sd,
                  _path=np.array(p.last_update_path), _loss=np.float32(p.last_loss.item()),
-                 _kinds=np.array(p._engine.dp_xbuf_kinds))
+                 _kinds=np.array(p._engine.dp_xbuf_kinds), _push=np.int32(p._engine._dp_push),
+                 _split=np.int32(prl_native.ppo_update_last_plan()["split"]))
         p._engine.close()
     finally:
         torch.distributed.destroy_process_group()
@@ -191,6 +194,32 @@ def test_two_ranks_persistent_dp_engine_fine_grained_buffers(tmp_path):
         for r in range(2):
             np.testing.assert_array_equal(fine[r][key], auto[0][key], err_msg=key)
     assert float(fine[0]["_loss"]) == float(auto[0]["_loss"])
+
+
+@pytest.mark.parametrize("xbuf", ["auto", "fine"])
+def test_two_ranks_persistent_dp_engine_push_form(tmp_path, xbuf):
+    """The PUSH form of the cross-rank exchange (PRL_DP_PUSH=1, the head-split kernel): each
+    workgroup writes its reduced slice into EVERY rank's receive slot and raises its flag there,
+    then polls only its own buffer — against the pull form on the same 2-rank
+    workload (unequal shards, two learn() calls): the same rank-order float32 sums, so both ranks
+    end with exactly the pull form's bits, on uncached and on fine-grained buffers."""
+    import random
+    mb, nb, k = 64, 5, 3
+    port = 29800 + random.randint(0, 30)
+    mp.spawn(_dpx_worker, args=(2, port, mb, nb, k, str(tmp_path), xbuf, False), nprocs=2, join=True)
+    mp.spawn(_dpx_worker, args=(2, port + 40, mb, nb, k, str(tmp_path), xbuf, True), nprocs=2,
+             join=True)
+    tag = '' if xbuf == 'auto' else xbuf
+    pull = [np.load(os.path.join(tmp_path, f"{tag}rank{r}.npz")) for r in range(2)]
+    push = [np.load(os.path.join(tmp_path, f"{tag}pushrank{r}.npz")) for r in range(2)]
+    assert int(push[0]["_push"]) == 1 and int(pull[0]["_push"]) == 0
+    assert int(push[0]["_split"]) == 1 and str(push[0]["_path"]) == "fused-dp-persistent"
+    for key in pull[0].files:
+        if key.startswith("_"):
+            continue
+        for r in range(2):
+            np.testing.assert_array_equal(push[r][key], pull[0][key], err_msg=key)
+    assert float(push[0]["_loss"]) == float(pull[0]["_loss"])
 
 
 def _nccl_one_rank_worker(port, out_dir):
