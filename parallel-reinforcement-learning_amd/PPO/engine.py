@@ -137,7 +137,8 @@ class FusedUpdate:
         # sub-phase marks (time since the phase began): phase B's partial loads landed, its
         # slice stores issued; phase C's gradient loads landed
         out["sub"] = {name: round(p[16 + i] * 0.01 / steps, 2) for i, name in
-                      enumerate(("B: partials landed", "B: slice stored", "C: gradient landed"))}
+                      enumerate(("B: partials landed", "B: slice stored", "C: gradient landed",
+                                 "A: loop top to tile start"))}
         if p[30] > 0:
             out["shader_clock_GHz"] = round(p[31] / (p[30] * 10.0), 3)
         out["clipped_steps_frac"] = round(p[28] / steps, 4)   # clip_grad_norm_ active

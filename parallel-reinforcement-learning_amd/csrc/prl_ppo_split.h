@@ -57,6 +57,8 @@ __device__ __forceinline__ void spl_tile(const UpdNet& n, const UpdArgs& args, i
   const int D = n.D, KS = (D + 3) >> 2;
   const bool timer = args.profile && blockIdx.x == 0 && t == 0;
   unsigned long long tl = timer ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  // (profile: from the previous phase mark to the tile's start — the loop top and the prefetch)
+  if (timer) tm[11] += tl - tm[31];   // tm[31] = pts[7] (hdr + 64), the last phase mark
 #define SPL_CMARK(i)                                                   \
   if (timer) {                                                         \
     const unsigned long long now_ = __builtin_amdgcn_s_memrealtime();  \
@@ -290,28 +292,45 @@ __device__ inline int spl_slice_start(int g, int G, int Qp, int QT) {
   return (int)(q < Qtot ? q : Qtot);
 }
 
-// Sum of quad q over the virtual partials v = first, first + stride, ... < nv, where v < Gt is
-// part[v] and v >= Gt is part2[v - Gt] (the trunk / loss quads' second Gt partials, quad qd
-// there), in that order; loads issued in batches of 16, so a dual quad's two partial sets are in
-// flight together (one memory round trip, not two in series).
+// Sum of quad q over partials first, first + stride, ... of part (< Gt) and, for a dual quad
+// (nv = 2 Gt: the trunk / loss quads), over the same positions of part2 (quad qd there): the
+// part and part2 loads of a chunk are issued together (one memory round trip), each from its own
+// WAVE-UNIFORM buffer resource (a per-lane choice of resource compiles to a waterfall loop per
+// load), with 32-bit byte offsets stepped by a uniform stride.  Order: chunk by chunk, part's
+// partials then part2's (deterministic).
 __device__ inline void spl_sum_partials(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_part2,
                                         int Qtot, int P2, int q, int qd, int first, int stride,
                                         int Gt, int nv, double& ax, double& ay, double& az,
                                         double& aw) {
-  constexpr int NB = 16;
-  for (int v0 = first; v0 < nv; v0 += NB * stride) {
-    float4 v[NB];
+  constexpr int NB = 8;
+  const bool dual = nv > Gt;
+  const unsigned d1 = (unsigned)stride * (unsigned)Qtot * 16u, d2 = (unsigned)stride * (unsigned)P2 * 16u;
+  for (int v0 = first; v0 < Gt; v0 += NB * stride) {
+    const unsigned o1 = ((unsigned)v0 * (unsigned)Qtot + (unsigned)q) * 16u;
+    const unsigned o2 = ((unsigned)v0 * (unsigned)P2 + (unsigned)qd) * 16u;
+    v4u a[NB], b[NB];
 #pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int vv = v0 + u * stride;
-      if (vv < nv)
-        v[u] = vv < Gt ? ld4_sc1(rs_part, ((size_t)vv * Qtot + q) * 4)
-                       : ld4_sc1(rs_part2, ((size_t)(vv - Gt) * P2 + qd) * 4);
+    for (int u = 0; u < NB; ++u)
+      if (v0 + u * stride < Gt) a[u] = __builtin_amdgcn_raw_buffer_load_b128(rs_part, o1 + (unsigned)u * d1, 0, UPD_AUX_SC1);
+    if (dual) {
+#pragma unroll
+      for (int u = 0; u < NB; ++u)
+        if (v0 + u * stride < Gt) b[u] = __builtin_amdgcn_raw_buffer_load_b128(rs_part2, o2 + (unsigned)u * d2, 0, UPD_AUX_SC1);
     }
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      if (v0 + u * stride < nv) {
-        ax += v[u].x; ay += v[u].y; az += v[u].z; aw += v[u].w;
+      if (v0 + u * stride < Gt) {
+        ax += __uint_as_float(a[u].x); ay += __uint_as_float(a[u].y);
+        az += __uint_as_float(a[u].z); aw += __uint_as_float(a[u].w);
+      }
+    }
+    if (dual) {
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        if (v0 + u * stride < Gt) {
+          ax += __uint_as_float(b[u].x); ay += __uint_as_float(b[u].y);
+          az += __uint_as_float(b[u].z); aw += __uint_as_float(b[u].w);
+        }
       }
     }
   }
@@ -321,12 +340,11 @@ __device__ inline void spl_sum_partials(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
 // trunk quads [0, QT) and the loss quad Qp also over part2 (role 1's trunk partials,
 // [Gt][QT + 1] quads).  Per quad: part[0 .. Gt) then part2[0 .. Gt) in the order sub,
 // sub + spl, ... for each of spl threads, combined in sub order (deterministic).
-template <int NT, bool PC>
+template <int NT>
 __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_part2,
                                         __amdgpu_buffer_rsrc_t rs_red, int Qtot, int Qp, int QT, int g,
                                         int G, int Gt, float* scratch, bool sys, int fill,
-                                        UpdSub sub, __amdgpu_buffer_rsrc_t rs_sq, const UpdArgs& args,
-                                        int par) {
+                                        UpdSub sub, const UpdArgs& args, int par) {
   const int t = threadIdx.x;
   const int qlo = spl_slice_start(g, G, Qp, QT), qhi = spl_slice_start(g + 1, G, Qp, QT);
   const int nq = qhi - qlo;
@@ -377,7 +395,6 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
   }
   sub.mark(0);   // thread 0's partial loads landed and summed
   __syncthreads();
-  float sq = 0.f;
   if (t < nq) {
     double ax = red[4 * t], ay = red[4 * t + 1], az = red[4 * t + 2], aw = red[4 * t + 3];
     for (int k = 1; k < spl; ++k) {
@@ -385,20 +402,6 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
       ax += o[0]; ay += o[1]; az += o[2]; aw += o[3];
     }
     fin(qlo + t, ax, ay, az, aw);
-    if (PC && qlo + t < Qp) {
-      const float4 r = float4{(float)ax, (float)ay, (float)az, (float)aw};
-      sq = (r.x * r.x + r.y * r.y) + (r.z * r.z + r.w * r.w);
-    }
-  }
-  if constexpr (PC) {
-    // clip_grad_norm_'s piece of this slice: the sum of squares of its parameter quads as
-    // stored (float32), over wave 0's owner lanes in one DPP tree (the host enables the form
-    // only when every slice has <= 64 quads), stored 16-B sc1 on a 64-B line of its own by lane
-    // 63 beside the slice's stores, so the same drain covers both
-    if (t < 64) {
-      sq = wave_sum_f32_to63(sq);
-      if (t == 63) st4_sc1(rs_sq, (size_t)g * 16, float4{sq, 0.f, 0.f, 0.f});
-    }
   }
   sub.mark(1);   // slice combined, its stores issued
 }
@@ -408,13 +411,9 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
 // DP: data-parallel ranks (prl_ppo_update_dpx): union-minibatch row weights inv_count[j] and,
 // after phase B, the cross-rank sum of each slice (upd_dp_union_slice, as the 8-wave kernel);
 // the 2 Gt workgroups of every rank cut the gradient into the same 2 Gt slices.
-// PC (single GPU only): clip_grad_norm_ from the slice owners' pieces (spl_slice_reduce) — phase
-// C loads the G pieces and only this role's OWNED quads of the reduced gradient (NQC then
-// counts owned slots: ceil(owned quads / threads)) instead of every quad.
-template <int NQC, int KA, bool DP, int TW, bool PC = false>
+template <int NQC, int KA, bool DP, int TW>
 __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& args) {
   constexpr int SPL_NT = 64 * TW;
-  static_assert(!(PC && DP), "the norm pieces cover one rank's reduced gradient only");
   extern __shared__ __align__(16) float upd_lds[];
   const int t = threadIdx.x, g = blockIdx.x, G = args.G, Gt = args.Gt;
   const int role = g / Gt, gt = g - role * Gt;   // role = the head this workgroup runs
@@ -423,17 +422,11 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   const int QH = n.w1[1].lds / 4;   // head 0: [QT, QH), head 1: [QH, Qp)
   // owned quads: the trunk and this role's head (the only parameters its tile reads)
   auto owned = [&](int q) { return role == 0 ? q < QH : (q < QT || q >= QH); };
-  // slot i of this thread: the quad its moments / AdamW cover (-1: none).  Canonical sweep
-  // (quads t + NT i, owned ones only) or, with PC, the owned quads packed: role 0 [0, QH),
-  // role 1 [0, QT) then [QH, Qp)
+  // slot i of this thread: the quad of the canonical sweep (t + NT i) its moments / AdamW cover,
+  // where this role owns it (-1: none)
   auto slotq = [&](int i) {
     const int o = t + i * SPL_NT;
-    if constexpr (PC) {
-      const int q = role == 0 ? o : (o < QT ? o : o - QT + QH);
-      return (role == 0 ? q < QH : q < Qp) ? q : -1;
-    } else {
-      return (o < Qp && owned(o)) ? o : -1;
-    }
+    return (o < Qp && owned(o)) ? o : -1;
   };
   float* hdr = upd_lds;
   float* scratch = upd_lds + UPD_HDR;
@@ -557,9 +550,8 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     {
       const unsigned long long gstep = args.dp_seq0 + (unsigned long long)s;
       const int par = (int)(gstep & 1ull);
-      spl_slice_reduce<SPL_NT, PC>(rs_part, rs_part2, DP ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
-                       Qtot, Qp, QT, g, G, Gt, scratch, DP, args.spl_fill, subm, upd_rsrc(args.sq),
-                       args, par);
+      spl_slice_reduce<SPL_NT>(rs_part, rs_part2, DP ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
+                       Qtot, Qp, QT, g, G, Gt, scratch, DP, args.spl_fill, subm, args, par);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (DP) {
@@ -582,34 +574,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     // ---- phase C: the norm in the canonical order, then AdamW on the owned quads -------------
     float4 gq[NQC];
     float clipc;
-    if constexpr (PC) {
-      // this role's owned quads, and the G pieces: lane l sums pieces l, l + 64, ... in that
-      // order, then the wave's DPP tree — the same data, order and code in every wave of every
-      // workgroup, so every copy forms the same coefficient
-#pragma unroll
-      for (int i = 0; i < NQC; ++i) {
-        const int q = slotq(i);
-        gq[i] = ld4_sc1(rs_red, (size_t)(q >= 0 ? q : 0) * 4);
-      }
-      const int l = t & 63;
-      const __amdgpu_buffer_rsrc_t rs_sq = upd_rsrc(args.sq);
-      float4 pcs[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) pcs[u] = ld4_sc1(rs_sq, (size_t)(l + 64 * u < G ? l + 64 * u : 0) * 16);
-      float pc = 0.f;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (l + 64 * u < G) pc += pcs[u].x;
-      subm.mark(2);   // thread 0's pieces landed
-      const float tot = __builtin_amdgcn_readlane(wave_sum_f32_to63(pc), 63);
-      const float coef = args.max_norm / (sqrtf(tot) + 1e-6f);
-      clipc = coef < 1.0f ? coef : 1.0f;
-      if (args.profile && g == 0 && t == 0 && coef < 1.0f) tm[20] += 1ull;
-      if (g == 0 && t == 0 && s + 1 == args.total_steps) {
-        const float4 lpq = ld4_sc1(rs_red, (size_t)Qp * 4);
-        loss_last = lpq.x * invB + args.vf_coef * (lpq.y * invB) - args.ent_coef * (lpq.z * invB);
-      }
-    } else {
+    {
 #pragma unroll
       for (int i = 0; i < NQC; ++i)
         if (i * SPL_NT < Qp) gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
@@ -695,8 +660,8 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   }
 }
 
-template <int NQC, int KA, int KDIM, bool DP = false, int TW = 4, bool PC = false>
+template <int NQC, int KA, int KDIM, bool DP = false, int TW = 4>
 __global__ __launch_bounds__(64 * TW, 1) void ppo_update_split_kernel(UpdArgs args) {
   constexpr UpdNet N = upd_make(KDIM, KA, 1);
-  ppo_split_body<NQC, KA, DP, TW, PC>(N, args);
+  ppo_split_body<NQC, KA, DP, TW>(N, args);
 }

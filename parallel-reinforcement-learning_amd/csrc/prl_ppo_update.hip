@@ -2688,27 +2688,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   if (!split) args.dp_push = 0;   // the push form is the head-split kernel's (ranks decide alike)
   if (split) {
     const int tw = upd_split_waves();
-    // PRL_UPD_SPL_PIECES=1 (single GPU, every slice <= 64 quads and narrow): the norm from the
-    // slice owners' pieces, phase C loading only the owned quads (A/B)
-    bool pieces = false;
-    {
-      const char* e = getenv("PRL_UPD_SPL_PIECES");
-      if (!dp && e && e[0] == '1') {
-        const int Qp = args.net.Lp / 4, QT = args.net.w1[0].lds / 4, Gs = 2 * Gt;
-        const int64_t U = (int64_t)Qp + QT + 2;
-        auto st = [&](int gg) {
-          const int64_t u = U * gg / Gs;
-          const int64_t q = u <= 2 * (int64_t)QT ? (u + 1) / 2 : u - QT;
-          return (int)std::min<int64_t>(q, Qp + 1);
-        };
-        int mx = 0;
-        for (int gg = 0; gg < Gs; ++gg) mx = std::max(mx, st(gg + 1) - st(gg));
-        pieces = mx <= 64 && 2 * mx <= 64 * tw && Gs <= 256;
-      }
-    }
-    const void* k = pieces ? (tw == 8 ? reinterpret_cast<const void*>(ppo_update_split_kernel<3, 2, 4, false, 8, true>)
-                                      : reinterpret_cast<const void*>(ppo_update_split_kernel<5, 2, 4, false, 4, true>)) :
-                    tw == 8 ? (dp ? reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC8, 2, 4, true, 8>)
+    const void* k = tw == 8 ? (dp ? reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC8, 2, 4, true, 8>)
                                   : reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC8, 2, 4, false, 8>))
                             : (dp ? reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, true, 4>)
                                   : reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, false, 4>));

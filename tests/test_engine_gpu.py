@@ -768,7 +768,7 @@ def test_split_form_matches_8wave_form(mb, N):
             plan = prl_native.ppo_update_last_plan()
             assert plan["form"] == "latency" and plan["split"] == bool(mode and 2 * Gt <= cus), plan
             if plan["split"]:
-                assert plan["waves"] == 4 and plan["grid"] == 2 * Gt, plan
+                assert plan["waves"] in (4, 8) and plan["grid"] == 2 * Gt, plan   # (8: PRL_UPD_SPL_WAVES)
             outs[mode] = [t.cpu().clone() for t in (eng.flat, eng.m, eng.v, eng.step, loss)]
             pols[mode] = types.SimpleNamespace(policy=copy.deepcopy(p.policy))
     assert not torch.equal(outs[1][0], init[0].cpu())
