@@ -270,6 +270,10 @@ def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
         achieved = flops / (avg_ms * 1e-3) / 1e12
         what = {"ppo_update_kernel": "persistent fused PPO update: the whole k_epochs x "
                                      "minibatch loop in one launch",
+                "ppo_update_split_kernel": "persistent fused PPO update, head-split form: the "
+                                           "whole k_epochs x minibatch loop in one launch, a "
+                                           "16-row tile's actor and critic head on two "
+                                           "workgroups",
                 "ppo_update_kernel_dp": "data-parallel persistent engine: the whole loop in one "
                                         "launch per rank, each step's gradient summed across "
                                         "ranks inside it over IPC-mapped peer memory",
@@ -387,6 +391,39 @@ def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
         if env_scale:
             roofline_env["at_scale"] = env_at_scale(cfg["env"], spec_, scaling, bpe)
 
+    # C2 / C4: the CartPole rollout as one launch (prl_cartpole_rollout), re-timed on one more
+    # rollout of the trained policy after the timed region: HIP events around the launch; the
+    # actor's forward is VALU f32 work (a thread per env), 2 x (4 x 64 + 64 x 64 + 64 x 2) =
+    # 8,960 flop per env-step (GroupNorm / SiLU / sampling / physics not counted)
+    roofline_rollout = None
+    if (cfg["env"] == "CartPole-v1" and runner._traj is not None
+            and os.environ.get("PRL_CP_ROLLOUT", "1") != "0"
+            and getattr(ppo, "rollout_params", None) is not None):
+        env, tr = runner.env, runner._traj
+        scaling = float(getattr(ppo, "action_scaling", None) or 1.0)
+        env.reset_device(tr.obs[0])
+        tr.active_after.zero_()
+        tr.reward_sum.zero_()
+        torch.cuda.synchronize()
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0.record()
+        k_last = runner._fused_rollout(0xC0FFEE, scaling)
+        r1.record()
+        r1.synchronize()
+        if k_last is not None:
+            n_es = int(tr.ep_len.sum().item())
+            ms_r = r0.elapsed_time(r1)
+            ach = 8960.0 * n_es / (ms_r * 1e-3) / 1e12
+            roofline_rollout = {"kernel": "prl_cartpole_rollout: cp_rollout_kernel (the whole "
+                                          "rollout in one launch, thread per env)",
+                                "bound": "valu", "achieved": round(ach, 2),
+                                "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                "frac": round(ach / F32_PEAK_TFLOPS, 4), "traffic": None,
+                                "launch_ms": round(ms_r, 3), "env_steps": n_es,
+                                "vector_steps": k_last + 1,
+                                "env_steps_per_s": round(n_es / (ms_r * 1e-3), 1),
+                                "flops_per_env_step": 8960}
+
     # world > 1: the N = 1 rate of the same per-GPU workload in the same run — rank 0 alone runs
     # one more iteration as a single-GPU job (learn() with world 1: no collective, the
     # single-GPU engine) while the other ranks wait at a barrier, so value / n1 reads as the
@@ -414,7 +451,7 @@ def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
            "transitions_per_step": round(total_n / steps, 1),
            "vector_steps_per_rollout": vec_steps,
            "roofline": roofline, "roofline_gae": roofline_gae, "roofline_env": roofline_env,
-           "roofline_rnd": roofline_rnd}
+           "roofline_rnd": roofline_rnd, "roofline_rollout": roofline_rollout}
     if eng is not None:
         eng.events = None     # release the HIP events before interpreter teardown
         eng.close()           # the engine's own RCCL communicator / slice buffers (world > 1)
@@ -546,6 +583,7 @@ def main():
             out["speedup_vs_1gpu"] = round(res["value"] / res["n1_same_run"]["value"], 3)
         for k in ("rollout_env_steps_per_s", "learn_ms_per_1M", "transitions_per_step",
                   "vector_steps_per_rollout", "roofline", "roofline_gae", "roofline_env",
+                  "roofline_rollout",
                   "roofline_rnd"):
             out[k] = res[k]
         out["learn_fixed_2p20"] = fixed

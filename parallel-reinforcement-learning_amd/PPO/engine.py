@@ -139,6 +139,14 @@ class FusedUpdate:
         out["sub"] = {name: round(p[16 + i] * 0.01 / steps, 2) for i, name in
                       enumerate(("B: partials landed", "B: slice stored", "C: gradient landed",
                                  "A: loop top to tile start"))}
+        if p[24] > 0:   # the split form's arrival skew at counters A / B (every 16th step)
+            n = p[24]
+            out["skew"] = {"samples": n,
+                           "A: last arrival - wg0": round(p[20] * 0.01 / n, 2),
+                           "A: last - first": round(p[21] * 0.01 / n, 2),
+                           "B: last arrival - wg0": round(p[22] * 0.01 / n, 2),
+                           "B: last - first": round(p[23] * 0.01 / n, 2),
+                           "A: last arriver critic frac": round(p[25] / n, 3)}
         if p[30] > 0:
             out["shader_clock_GHz"] = round(p[31] / (p[30] * 10.0), 3)
         out["clipped_steps_frac"] = round(p[28] / steps, 4)   # clip_grad_norm_ active
@@ -163,7 +171,9 @@ class FusedUpdate:
         if self.events is not None:
             ev[1].record()
             nb = -(-int(S.shape[0]) // self.mini_batch)
-            self.events.append(("ppo_update_kernel", ev[0], ev[1], int(S.shape[0]) * int(k_epochs),
+            kern = ("ppo_update_split_kernel" if prl_native.ppo_update_last_plan()["split"]
+                    else "ppo_update_kernel")
+            self.events.append((kern, ev[0], ev[1], int(S.shape[0]) * int(k_epochs),
                                 int(k_epochs) * nb))
         self._sync_optimizer_state()
         status = max(prl_native.ppo_update_status(self.ws).tolist())

@@ -336,18 +336,86 @@ __device__ inline void spl_sum_partials(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
   }
 }
 
+// Profile only (PRL_UPD_PROFILE=1, every 16th step: A at s = 0 mod 16, B at 8 mod 16): arrival
+// skew at counter `slot` (0: A, 1: B).
+// Each workgroup stamps its arrival (prof[32 + 256 slot + g]); after the wait, workgroup 0's
+// wave 0 reads the stamps back (one extra round trip on the sampled steps, kept out of the
+// phase marks) and sums the last arrival - its own and the last - the first into
+// tm[12 + 2 slot], tm[13 + 2 slot]; tm[16] counts the samples, tm[17] those whose last arrival
+// at A was a role-1 (critic) workgroup.
+__device__ inline void spl_prof_stamp(const UpdArgs& a, int slot, int g) {
+  __hip_atomic_store(a.prof + 32 + 256 * slot + g, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void spl_prof_skew(const UpdArgs& a, int slot, int G, int Gt, unsigned long long* tm) {
+  const int l = threadIdx.x & 63;
+  unsigned long long mx = 0ull, mn = ~0ull, own = 0ull;
+  int arg = 0;
+  for (int i0 = 0; i0 < G && i0 < 256; i0 += 64) {
+    const int i = i0 + l;
+    const unsigned long long v = i < G ? __hip_atomic_load(a.prof + 32 + 256 * slot + i, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    unsigned long long vmx = i < G ? v : 0ull, vmn = i < G ? v : ~0ull;
+    int vi = i;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const unsigned long long ox = __shfl_xor(vmx, o), on = __shfl_xor(vmn, o);
+      const int oi = __shfl_xor(vi, o);
+      if (ox > vmx || (ox == vmx && oi < vi)) { vmx = ox; vi = oi; }
+      vmn = on < vmn ? on : vmn;
+    }
+    if (i0 == 0) own = __shfl(v, 0);
+    if (vmx > mx) { mx = vmx; arg = vi; }
+    mn = vmn < mn ? vmn : mn;
+  }
+  if (l == 0 && mx >= own && mx >= mn) {
+    tm[12 + 2 * slot] += mx - own;
+    tm[13 + 2 * slot] += mx - mn;
+    if (slot == 0) {
+      tm[16] += 1ull;
+      tm[17] += arg >= Gt ? 1ull : 0ull;
+    }
+  }
+}
+
+// The slice and this thread's place in it are loop-invariant: planned once before the step
+// loop (64-bit and integer divisions: ~0.1 us of dependent instructions per step otherwise).
+struct SplSlice {
+  int qlo, qhi, nq;
+  int spl;      // threads per quad (narrow slices)
+  int qi, sb;   // this thread's quad (qlo + qi) and its first partial
+};
+template <int NT>
+__device__ inline SplSlice spl_slice_plan(int g, int G, int Qp, int QT, int Gt, int fill) {
+  SplSlice p;
+  p.qlo = spl_slice_start(g, G, Qp, QT);
+  p.qhi = spl_slice_start(g + 1, G, Qp, QT);
+  p.nq = p.qhi - p.qlo;
+  // spl threads per quad, each summing every spl-th partial: a power of two (fill 0), or as
+  // many as the NT threads allow (fill 1: more loads in flight; the slice loads are latency-bound)
+  int spl = 1;
+  if (p.nq > 0) {
+    if (fill) spl = std::max(1, std::min(Gt, NT / p.nq));
+    else
+      while (spl * 2 * p.nq <= NT && spl * 2 <= Gt) spl *= 2;
+  }
+  p.spl = spl;
+  const int t = threadIdx.x;
+  p.qi = p.nq > 0 ? t % p.nq : 0;
+  p.sb = p.nq > 0 ? t / p.nq : 0;
+  return p;
+}
 // Phase B of the split form: slice g of G (spl_slice_start) over the Gt role partials; the
 // trunk quads [0, QT) and the loss quad Qp also over part2 (role 1's trunk partials,
 // [Gt][QT + 1] quads).  Per quad: part[0 .. Gt) then part2[0 .. Gt) in the order sub,
 // sub + spl, ... for each of spl threads, combined in sub order (deterministic).
 template <int NT>
 __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_part2,
-                                        __amdgpu_buffer_rsrc_t rs_red, int Qtot, int Qp, int QT, int g,
-                                        int G, int Gt, float* scratch, bool sys, int fill,
+                                        __amdgpu_buffer_rsrc_t rs_red, int Qtot, int Qp, int QT,
+                                        const SplSlice& pl, int Gt, float* scratch, bool sys,
                                         UpdSub sub, const UpdArgs& args, int par) {
   const int t = threadIdx.x;
-  const int qlo = spl_slice_start(g, G, Qp, QT), qhi = spl_slice_start(g + 1, G, Qp, QT);
-  const int nq = qhi - qlo;
+  const int qlo = pl.qlo, qhi = pl.qhi, nq = pl.nq;
   if (nq <= 0) return;
   const int P2 = QT + 1;
   auto fin = [&](int q, double ax, double ay, double az, double aw) {
@@ -377,15 +445,10 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
     }
     return;
   }
-  // spl threads per quad, each summing every spl-th partial: a power of two (fill 0), or as
-  // many as the 256 threads allow (fill 1: more loads in flight; the slice loads are latency-bound)
-  int spl = 1;
-  if (fill) spl = std::max(1, std::min(Gt, NT / nq));
-  else
-    while (spl * 2 * nq <= NT && spl * 2 <= Gt) spl *= 2;
+  const int spl = pl.spl;
   double* red = reinterpret_cast<double*>(scratch);   // [spl][nq][4]
   if (t < spl * nq) {
-    const int qi = t % nq, sb = t / nq, q = qlo + qi;
+    const int qi = pl.qi, sb = pl.sb, q = qlo + qi;
     double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
     const bool dual = q < QT || q == Qp;
     spl_sum_partials(rs_part, rs_part2, Qtot, P2, q, q < QT ? q : QT, sb, spl, Gt, dual ? 2 * Gt : Gt,
@@ -469,15 +532,52 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   unsigned long long* const tm = reinterpret_cast<unsigned long long*>(hdr + 16);
   const UpdSub subm{(args.profile && g == 0) ? tm + 8 : nullptr, pts + 7};
   const int R = args.R;   // == UPD_RT: one tile per workgroup and step
-  UpdIn<upd_ksm<KA>()> nin;
-  auto first_row = [&](int s) { return (int64_t)(s % args.nb) * args.mb + (int64_t)gt * R; };
-  auto first_rows = [&](int s) {
-    const int64_t fmb0 = (int64_t)(s % args.nb) * args.mb;
-    const int fB = (int)std::min<int64_t>(args.mb, args.N - fmb0);
-    return args.profile == 2 ? 0 : std::max(0, std::min(R, fB - gt * R));
+  // The loop top is on every step's critical path (AdamW -> next tile), so the per-step scalars
+  // and the tile loads' addresses are loop-invariant pieces plus a row base: minibatch j = s mod
+  // nb advanced by one per step, B (and this workgroup's rows) of a full and of the last
+  // minibatch, and each thread's input offsets fixed at the start (upd_tile_load's addresses,
+  // less its per-step branching: 0.56 us from the AdamW barrier to the tile's start).
+  constexpr int KSM = upd_ksm<KA>();
+  const int nb = args.nb;
+  // rows of minibatch jj (B <= 0: past this data-parallel rank's rows), this workgroup's share
+  auto B_of = [&](int jj) { return (int)std::min<int64_t>(args.mb, args.N - (int64_t)jj * args.mb); };
+  auto rows_of = [&](int B) { return args.profile == 2 ? 0 : std::max(0, std::min(R, B - gt * R)); };
+  const int Blast = B_of(nb - 1);   // (one rank: the only minibatch short of mb)
+  const float invB_full = 1.0f / (float)args.mb, invB_last = 1.0f / (float)std::max(Blast, 1);
+  const int ll = t & 63, lx = ll & 15, lq = ll >> 4;
+  int xo[KSM];
+  unsigned okb = 0u;
+#pragma unroll
+  for (int s = 0; s < KSM; ++s) {
+    const int d = 4 * s + lq;
+    xo[s] = lx * n.D + d;
+    okb |= (s < ((n.D + 3) >> 2) && d < n.D) ? 1u << s : 0u;
+  }
+  const float* rb = nullptr;   // this thread's row-input column (act[k] / old_logp / adv / ret)
+  int rst = 0, rr_ = 0;
+  if (t < UPD_RT * UPD_RIN) {
+    const int k = t % UPD_RIN, Aw = n.discrete ? 1 : n.A;
+    rr_ = t / UPD_RIN;
+    if (k < UPD_MAXA) { if (k < Aw) { rb = args.act + k; rst = Aw; } }
+    else if (k == 8) { rb = args.old_logp; rst = 1; }
+    else if (k == 9) { rb = args.adv; rst = 1; }
+    else if (k == 10) { rb = args.ret; rst = 1; }
+  }
+  const float* const Sg = args.S;
+  // the inputs of minibatch jj's tile gt (upd_tile_load<.., RAW>: dummy loads of S[0] where empty)
+  auto tile_load = [&](int jj, int rc, UpdIn<KSM>& in) {
+    const int64_t row0 = (int64_t)jj * args.mb + (int64_t)gt * R;
+    const float* Sb = Sg + row0 * n.D;
+    const bool rowok = lx < rc;
+    const unsigned ok = rowok ? okb : 0u;
+#pragma unroll
+    for (int s = 0; s < KSM; ++s) in.xin[s] = *(((ok >> s) & 1u) ? Sb + xo[s] : Sg);
+    const bool rv = rb != nullptr && rr_ < rc;
+    in.rin = *(rv ? rb + (row0 + rr_) * rst : Sg);
+    in.ok = ok | (rv ? 1u << 31 : 0u);
   };
-  upd_tile_load<1, KA, true>(n, args.S, args.act, args.old_logp, args.adv, args.ret, first_row(0),
-                             std::min(UPD_RT, first_rows(0)), nin);
+  UpdIn<KSM> nin;
+  tile_load(0, rows_of(B_of(0)), nin);
   const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_part2 = upd_rsrc(args.part2),
                                rs_red = upd_rsrc(args.red);
   const __amdgpu_buffer_rsrc_t rs_mypart = upd_rsrc(args.part + (size_t)gt * Qtot * 4);
@@ -490,25 +590,26 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   float loss_last = 0.f;
+  const SplSlice slc = spl_slice_plan<SPL_NT>(g, G, Qp, QT, Gt, args.spl_fill);
+  int j = 0;   // s mod nb
+  int Bj = B_of(0);
   for (int s = 0; s < args.total_steps; ++s) {
-    const int j = s % args.nb;
-    const int64_t mb0 = (int64_t)j * args.mb;
-    const int B = (int)std::min<int64_t>(args.mb, args.N - mb0);
-    const float invB = DP ? args.inv_count[j] : 1.0f / (float)B;
-    const int myrows = args.profile == 2 ? 0 : std::max(0, std::min(R, B - gt * R));
+    const int jn = j == nb - 1 ? 0 : j + 1;
+    const int Bn = B_of(jn);
+    const float invB = DP ? args.inv_count[j] : (Bj == args.mb ? invB_full : invB_last);
+    const int myrows = rows_of(Bj);
     // ---- phase A: this role's share of tile group gt's gradient ------------------------------
     if (myrows > 0) {
-      const UpdIn<upd_ksm<KA>()> cur = upd_in_real(nin);
-      // prefetch the next step's tile under this one and the hand-offs (unconditional: clamped
-      // arguments, see the engine's load_next)
-      upd_tile_load<1, KA, true>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
-                                 first_row(s + 1), std::min(UPD_RT, first_rows(s + 1)), nin);
+      const UpdIn<KSM> cur = upd_in_real(nin);
+      // prefetch the next step's tile under this one and the hand-offs
+      tile_load(jn, rows_of(Bn), nin);
       spl_tile<KA, TW>(n, args, role, W, Ga, sc, cur, myrows, invB, tm, direct, rs_mypart);
     } else {
       for (int k = t; k < Lp + 4; k += SPL_NT) Ga[k] = 0.0f;
-      upd_tile_load<1, KA, true>(n, args.S, args.act, args.old_logp, args.adv, args.ret,
-                                 first_row(s + 1), std::min(UPD_RT, first_rows(s + 1)), nin);
+      tile_load(jn, rows_of(Bn), nin);
     }
+    j = jn;
+    Bj = Bn;
     __syncthreads();
     mark(0);   // phase A compute
     // (direct and rows this step: the dW1 quads are in the partial already; with no rows they
@@ -531,7 +632,9 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     mark(1);   // publish
+    const bool skew = args.profile && (s & 15) == 0;
     if (t < 64) {
+      if (skew && t == 0) spl_prof_stamp(args, 0, g);
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_A, g);
       const bool ok = args.spl_poll ? upd_wait_sharded_pipe(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1))
                                     : upd_wait_sharded(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));
@@ -546,16 +649,21 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     __syncthreads();
     if (*s_abort) return;
     mark(2);   // wait A
+    if (skew && g == 0) {
+      if (t < 64) spl_prof_skew(args, 0, G, Gt, tm);
+      __syncthreads();
+      if (t == 0) pts[7] = __builtin_amdgcn_s_memrealtime();   // (the read-back is no phase's)
+    }
     // ---- phase B ---------------------------------------------------------------------------
     {
       const unsigned long long gstep = args.dp_seq0 + (unsigned long long)s;
       const int par = (int)(gstep & 1ull);
       spl_slice_reduce<SPL_NT>(rs_part, rs_part2, DP ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
-                       Qtot, Qp, QT, g, G, Gt, scratch, DP, args.spl_fill, subm, args, par);
+                               Qtot, Qp, QT, slc, Gt, scratch, DP, subm, args, par);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (DP) {
-        const int qlo = spl_slice_start(g, G, Qp, QT), qhi = spl_slice_start(g + 1, G, Qp, QT);
+        const int qlo = slc.qlo, qhi = slc.qhi;
         if (!(args.dp_push ? upd_dp_union_slice_push(args, rs_red, Qtot, g, gstep, par, s_abort, qlo, qhi)
                            : upd_dp_union_slice(args, rs_red, Qtot, g, G, gstep, par, s_abort, qlo, qhi)))
           return;
@@ -563,6 +671,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     }
     mark(3);   // slice reduce
     if (t < 64) {
+      if (args.profile && (s & 15) == 8 && t == 0) spl_prof_stamp(args, 1, g);
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_B, g);
       const bool ok = args.spl_poll ? upd_wait_sharded_pipe(args.ctr, UPD_CTR_B, (unsigned)G * (unsigned)(s + 1))
                                     : upd_wait_sharded(args.ctr, UPD_CTR_B, (unsigned)G * (unsigned)(s + 1));
@@ -571,6 +680,11 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     __syncthreads();
     if (*s_abort) return;
     mark(4);   // wait B
+    if (args.profile && (s & 15) == 8 && g == 0) {   // (not A's sampled steps: its read-back delays g 0)
+      if (t < 64) spl_prof_skew(args, 1, G, Gt, tm);
+      __syncthreads();
+      if (t == 0) pts[7] = __builtin_amdgcn_s_memrealtime();
+    }
     // ---- phase C: the norm in the canonical order, then AdamW on the owned quads -------------
     float4 gq[NQC];
     float clipc;
@@ -613,7 +727,31 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
           float4 pw = *reinterpret_cast<float4*>(W + 4 * q);
           float4 m4 = mreg[i], v4 = vreg[i];
           const float4 g4 = gq[i];
-          // the engine's AdamW arithmetic (ppo_update_body, 4-wave scalar form)
+          // the engine's AdamW arithmetic (ppo_update_body): the 4-wave scalar form, or two
+          // elements per packed-f32 instruction (the same operations per element, so the same bits)
+          if (args.spl_pk) {
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              const upd_f2 gr = upd_f2{f4get(g4, 2 * hh), f4get(g4, 2 * hh + 1)} * clipc;
+              upd_f2 m = upd_f2{f4get(m4, 2 * hh), f4get(m4, 2 * hh + 1)};
+              upd_f2 v = upd_f2{f4get(v4, 2 * hh), f4get(v4, 2 * hh + 1)};
+              upd_f2 p = upd_f2{f4get(pw, 2 * hh), f4get(pw, 2 * hh + 1)};
+              p = p * decay;
+              m = upd_pkfma(upd_f2{omb1, omb1}, gr - m, m);
+              v = upd_pkfma((upd_f2)(omb2 * gr), gr, v * b2);
+              const upd_f2 sq{__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
+              const upd_f2 denom = upd_pkfma(sq, upd_f2{inv_bc2_sqrt, inv_bc2_sqrt}, upd_f2{args.eps, args.eps});
+              upd_f2 rq{__builtin_amdgcn_rcpf(denom.x), __builtin_amdgcn_rcpf(denom.y)};
+              rq = upd_pkfma(rq, upd_pkfma(-denom, rq, upd_f2{1.0f, 1.0f}), rq);
+              p = upd_pkfma(upd_f2{-step_size, -step_size}, m * rq, p);
+              f4set(m4, 2 * hh, m.x);
+              f4set(m4, 2 * hh + 1, m.y);
+              f4set(v4, 2 * hh, v.x);
+              f4set(v4, 2 * hh + 1, v.y);
+              f4set(pw, 2 * hh, p.x);
+              f4set(pw, 2 * hh + 1, p.y);
+            }
+          } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float gr = f4get(g4, e) * clipc;
@@ -628,6 +766,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
             f4set(m4, e, m);
             f4set(v4, e, v);
             f4set(pw, e, p);
+          }
           }
           mreg[i] = m4;
           vreg[i] = v4;

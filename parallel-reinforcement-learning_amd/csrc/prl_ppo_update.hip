@@ -146,6 +146,7 @@ struct UpdArgs {
   int spl_fill;     // head-split form's phase B: threads per quad (PRL_UPD_SPL_FILL, A/B)
   int spl_direct;   // head-split form: dW1 stored from registers into the partial (PRL_UPD_SPL_DIRECT)
   int spl_poll;     // head-split form: counter waits with four polls in flight (PRL_UPD_SPL_POLL)
+  int spl_pk;       // head-split form: AdamW two elements per packed-f32 instruction (PRL_UPD_SPL_PK)
   float* red;       // [Qtot * 4]
   float* sq;        // [NW G] per-wave squared-norm pieces of the slices
   unsigned* ctr;    // [0] arrivals A, [1] arrivals B, [2] abort, [3] status (zeroed per launch),
@@ -2513,15 +2514,15 @@ struct UpdWs {
 };
 
 // workspace: ctr[UPD_CTR_WORDS] (words 0-3 and the shards zeroed per launch, word 4 sticky) |
-// prof[32] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4] | img[3][Qtot*4] | mv[4][Qtot*4] |
-// part2[G][(QT+1)*4] | slack
+// prof[32] + arrival stamps[2][256] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4] | img[3][Qtot*4] |
+// mv[4][Qtot*4] | part2[G][(QT+1)*4] | slack
 // (phase C's sweeps read up to one thread block of quads past an image: the slack keeps the
 // last one inside the allocation)
 size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
   const size_t Qtot = (size_t)n.Lp / 4 + 1;
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-  const size_t o_ctr = take(4 * UPD_CTR_WORDS), o_prof = take(256), o_sq = take(2048 * 4), o_red = take(Qtot * 16),
+  const size_t o_ctr = take(4 * UPD_CTR_WORDS), o_prof = take(256 + 2 * 256 * 8), o_sq = take(2048 * 4), o_red = take(Qtot * 16),
                o_part = take((size_t)G * Qtot * 16), o_img = take((size_t)3 * Qtot * 16),
                o_mv = take((size_t)4 * Qtot * 16),
                o_part2 = take((size_t)G * ((size_t)n.w1[0].lds / 4 + 1) * 16);
@@ -2672,6 +2673,8 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     args.spl_direct = (d && d[0] == '1') ? 1 : 0;
     const char* pp = getenv("PRL_UPD_SPL_POLL");
     args.spl_poll = (pp && pp[0] == '1') ? 1 : 0;
+    const char* pk = getenv("PRL_UPD_SPL_PK");
+    args.spl_pk = (pk && pk[0] == '1') ? 1 : 0;
   }
   args.tp_m0 = ws.mv;
   args.tp_v0 = ws.mv + L4;

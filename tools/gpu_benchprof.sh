@@ -20,7 +20,8 @@ python tools/rocprof_summary.py stats $O/prof_bench/bench_kernel_stats.csv --top
 python tools/rocprof_summary.py pmc $O/pmc_fetch/fetch_counter_collection.csv $O/pmc_write/write_counter_collection.csv --match gae_kernel --n $N > $O/gae_pmc.json
 python tools/rocprof_summary.py trace $O/prof_bench/bench_kernel_trace.csv --match gae_kernel > $O/gae_trace.json
 # the update engine's launches of the timed steps (bench.py's default --steps 3 after 1 warm-up)
-python tools/rocprof_summary.py trace $O/prof_bench/bench_kernel_trace.csv --match ppo_update_kernel --last 3 > $O/update_trace.json
+python tools/rocprof_summary.py trace $O/prof_bench/bench_kernel_trace.csv --match ${UPD_KERNEL:-ppo_update_split_kernel} --last 3 > $O/update_trace.json
 python tools/rocprof_summary.py trace $O/prof_bench/bench_kernel_trace.csv --match rollout_step_kernel > $O/env_trace.json
+python tools/rocprof_summary.py trace $O/prof_bench/bench_kernel_trace.csv --match cp_rollout_kernel > $O/cp_rollout_trace.json
 rm -f $O/prof_bench/bench_kernel_trace.csv
-cat $O/gae_pmc.json $O/gae_trace.json $O/update_trace.json
+cat $O/gae_pmc.json $O/gae_trace.json $O/update_trace.json $O/cp_rollout_trace.json
