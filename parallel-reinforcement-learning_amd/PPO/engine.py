@@ -274,9 +274,10 @@ class FusedUpdate:
         tdist.all_gather_object(handles, (handle, kind))
         # the flags are fenced when ANY rank's buffer is fine-grained (prl_ppo_update_dpx)
         self._dp_fine = any(k == "fine" for _, k in handles)
-        # the push form of the exchange (PRL_DP_PUSH=1) only when every rank asks for it
+        # the push form of the exchange (default; PRL_DP_PUSH=0 on any rank: the pull form) only
+        # when every rank asks for it (one-GPU rehearsal: 17.1 vs 17.5 us per step at 2 ranks)
         push = [None] * world
-        tdist.all_gather_object(push, os.environ.get("PRL_DP_PUSH", "0") == "1")
+        tdist.all_gather_object(push, os.environ.get("PRL_DP_PUSH", "1") != "0")
         self._dp_push = all(push)
         self.dp_xbuf_kinds = [k for _, k in handles]
         handles = [h for h, _ in handles]
