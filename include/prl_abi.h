@@ -213,6 +213,21 @@ int prl_rnd_forward(const float* x, int64_t n, int32_t D,
                     const float* t_w2, const float* t_b2,
                     const float* p_w1, const float* p_b1, const float* p_gw, const float* p_gb,
                     const float* p_w2, const float* p_b2, float beta, float* out, void* stream);
+/* RND.update_pred's gradient (PPO/RND.py:96-115: loss = MSELoss('mean')(pred(x), target(x)),
+ * loss.backward()) for one minibatch x[n][D], fused: both forwards, dY = scale (pred - target)
+ * (scale = 2 / (rows D) for the mean; a data-parallel rank passes 2 / (union rows D)), and the
+ * predictor's whole backward, written to grad[129 D + 192] in the predictor's parameters() order
+ * (W1[64][D], b1[64], gamma[64], beta[64], W2[D][64], b2[D]).  One launch per 128-row block into
+ * partial[ceil(n / 128)][129 D + 192] (partial_floats >= prl_rnd_pred_grad_ws_floats(n, D)), then
+ * a fold in block order (f64): deterministic.  D % 4 == 0; x, W1, W2 16-B aligned. */
+int prl_rnd_pred_grad(const float* x, int64_t n, int32_t D,
+                      const float* t_w1, const float* t_b1, const float* t_gw, const float* t_gb,
+                      const float* t_w2, const float* t_b2,
+                      const float* p_w1, const float* p_b1, const float* p_gw, const float* p_gb,
+                      const float* p_w2, const float* p_b2, float scale, float* partial,
+                      int64_t partial_floats, float* grad, void* stream);
+/* Floats of prl_rnd_pred_grad's partial buffer for n rows (0 for n <= 0). */
+int64_t prl_rnd_pred_grad_ws_floats(int64_t n, int32_t D);
 
 /* ---- actor-critic / RND hidden blocks ------------------------------------------------------ */
 /* GroupNorm(groups=8, C=64, eps) + SiLU over x[N][64] (PPO/ActorCritic.py:19-60, PPO/RND.py:25-30):

@@ -184,6 +184,56 @@ class RND(nn.Module):
         # must take the same one whatever its own minibatches look like
         return self._flat_optimizer_ok()
 
+    def _native_ok(self, values) -> bool:
+        """The fused predictor-gradient kernel (prl_rnd_pred_grad) runs every step when the loss
+        and optimizer are the reference's (_flat_optimizer_ok), D % 4 == 0 and the minibatches are
+        contiguous f32 device rows (PRL_RND_NATIVE=0: the graphed / PyTorch steps).  Rank-invariant
+        on data-parallel ranks except for the minibatches, which only choose between two paths
+        that issue the same single all-reduce per step."""
+        if os.environ.get("PRL_RND_NATIVE", "1") == "0" or not torch.cuda.is_available():
+            return False
+        if not self._flat_optimizer_ok():
+            return False
+        D = self.pred_net[0].weight.shape[1]
+        if D % 4 != 0 or self.pred_net[3].weight.shape[0] != D:
+            return False
+        return all(v.is_cuda and v.dtype == torch.float32 and v.dim() == 2 and v.shape[1] == D
+                   for v in values)
+
+    def _update_native(self, values, all_reduce=None, counts=None) -> None:
+        """update_pred with the fused gradient kernel: per minibatch ONE prl_rnd_pred_grad (both
+        forwards, MSE, the predictor's backward, written into the flat gradient the parameters'
+        .grad view) and the native AdamW pair (max_norm = inf), plus, on data-parallel ranks, one
+        all-reduce of the flat gradient (each rank's rows scaled by 2 / (union rows D): the
+        union's mean).  Same steps in the same order as the loops below."""
+        fa = self._flat_state()
+        group = self.optimizer.param_groups[0]
+        beta1, beta2 = group["betas"]
+        D = self.pred_net[0].weight.shape[1]
+
+        tnet = [p.detach().contiguous() for p in self._params(self.target_net)]
+        pnet = [p.detach().contiguous() for p in self._params(self.pred_net)]
+        mb = max([v.shape[0] for v in values] + [1])
+        need = prl_native.rnd_pred_grad_ws_floats(mb, D)
+        part = getattr(self, "_rg_partial", None)
+        if part is None or part.numel() < need or part.device != fa.flat.device:
+            self._rg_partial = part = torch.empty(max(need, 1), dtype=torch.float32,
+                                                  device=fa.flat.device)
+        steps = len(values) if counts is None else len(counts)
+        for j in range(steps):
+            if j < len(values):
+                x = values[j] if values[j].is_contiguous() else values[j].contiguous()
+                rows = x.shape[0] if counts is None else counts[j]
+                prl_native.rnd_pred_grad(x, tnet, pnet, 2.0 / (rows * D), part, self._fgrad)
+            else:
+                self._fgrad.zero_()
+            if all_reduce is not None:
+                all_reduce(self._fgrad)
+            prl_native.flat_adamw(fa.flat, fa.m, fa.v, fa.step, self._fgrad, group["lr"], beta1,
+                                  beta2, group["eps"], group["weight_decay"], float("inf"),
+                                  fa.total_norm)
+        fa.sync()
+
     def _graphed_ok(self, values, all_reduce, counts) -> bool:
         if all_reduce is not None or counts is not None or os.environ.get("PRL_RND_GRAPH", "1") == "0":
             return False
@@ -254,6 +304,10 @@ class RND(nn.Module):
         rank, ranks past their last minibatch contribute zero gradients (lockstep)."""
         self.pred_net.train()
         values = list(values)
+        if self._native_ok(values):
+            self._update_native(values, all_reduce, counts)
+            self.pred_net.eval()
+            return
         if self._graphed_ok(values, all_reduce, counts):
             self._update_graphed(values)
             self.pred_net.eval()

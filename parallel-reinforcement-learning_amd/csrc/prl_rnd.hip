@@ -360,6 +360,319 @@ __global__ __launch_bounds__(256, 1) void rnd_forward_fast_kernel(const float* _
   }
 }
 
+
+// ---- RND.update_pred's gradient (RND.py:96-115), fused -------------------------------------------
+// One optimizer step of the predictor is MSE(pred(x), target(x).detach()) over a minibatch, its
+// backward, AdamW.  This kernel forms the predictor's whole gradient for the minibatch in ONE
+// launch per 128-row block (+ one fold launch), where the PyTorch step ran ~25 kernels (two
+// forwards, hipBLASLt GEMMs for the three weight / input gradients, GroupNorm / SiLU backward,
+// column sums), ~0.6 ms per 65,536-row minibatch at C5:
+//   forward   the forward kernel's layer 1 (both nets) + GroupNorm + SiLU into Z = [S_p | -S_t],
+//             layer 2 as Yp - Yt in 64-column chunks (fp32 MFMA 32x32x2);
+//   dY        = scale (Yp - Yt) per chunk (scale = 2 / (rows D): MSELoss 'mean'; rows >= n: 0),
+//             into LDS; then per chunk dW2 = dY^T S_p (one 32 x 32 tile per wave, K = 128 rows),
+//             db2 (column sums) and dS_p += dY W2_p (the layer-1 accumulators' layout);
+//   GN + SiLU backward on the fragments (the forward recomputed from the kept pre-activations,
+//             the forward kernel's arithmetic), giving dH_p, dgamma, dbeta, db1;
+//   dW1       = dH_p^T X: the block's X re-streamed in 32-column chunks, v_mfma_f32_16x16x4_f32
+//             (wave w: units 16w .. 16w + 15), K = 128 rows.
+// Every block writes its partial gradient in the flat parameter order (W1, b1, gamma, beta, W2,
+// b2: torch parameters() of the predictor), and rnd_grad_fold_kernel sums the blocks in order
+// (f64): deterministic, no atomics.
+constexpr int RG_PD = 65;                 // pitch of dY [128][64] (odd: conflict-free row reads)
+constexpr int RG_PH = 80;                 // pitch of dH [128][64] (16-lane groups on 4 bank offsets)
+constexpr int RG_PX = 48;                 // pitch of the dW1 phase's X chunk [128][32]
+constexpr int RG_W2 = RF_CC * RF_PW;      // one layer-2 weight chunk [64][132]
+constexpr int RG_LDS = RF_STAGE + RF_M * RF_PZ + 4 * 3 * 64 + 4 * 64;
+static_assert(RG_W2 + RF_M * RG_PD <= RF_STAGE, "layer-2 chunk + dY fit the stage");
+static_assert(RF_M * RG_PH <= RF_M * RF_PZ, "dH fits Z");
+static_assert(RF_M * RG_PX <= RF_STAGE, "X chunk fits the stage");
+
+__device__ inline int64_t rg_param_floats(int D) { return 129 * (int64_t)D + 192; }
+
+// X chunk [128][32] of block rows for the dW1 phase: thread tid takes float4 slots tid + 256 i
+__device__ inline void rg_loadx(float4 (&v)[4], const float* x, int64_t n, int D, int64_t row0, int k0) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int slot = tid + 256 * i, r = slot >> 3, k = k0 + 4 * (slot & 7);
+    v[i] = (k < D && row0 + r < n) ? *reinterpret_cast<const float4*>(x + (row0 + r) * D + k)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+__device__ inline void rg_storex(const float4 (&v)[4], float* buf) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int slot = tid + 256 * i, r = slot >> 3, k = 4 * (slot & 7);
+    *reinterpret_cast<float4*>(buf + r * RG_PX + k) = v[i];
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void rnd_pred_grad_kernel(const float* __restrict__ x, int64_t n, int D,
+                                                               RndNet tn, RndNet pn, float scale,
+                                                               float* __restrict__ partial) {
+  extern __shared__ __align__(16) float rg_lds[];
+  float* stage = rg_lds;                               // layer 1: [2][X | W1] chunks
+  float* w2s = rg_lds;                                 // layer 2: one W2 chunk [64][132]
+  float* dys = rg_lds + RG_W2;                         // layer 2: dY chunk [128][65]
+  float* xs = rg_lds;                                  // dW1 phase: X chunk [128][48]
+  float* zs = rg_lds + RF_STAGE;                       // Z [128][129]; then dH [128][80]
+  float* cs = zs + RF_M * RF_PZ;                       // [4 waves][3][64] column sums
+  float* cb = cs + 4 * 3 * 64;                         // [4 waves][64] db2 column sums
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, lr = lane & 31, lh = lane >> 5;
+  const int64_t blk = blockIdx.x, row0 = blk * RF_M;
+  const int nk = (D + RF_KC - 1) / RF_KC, nc = (D + RF_CC - 1) / RF_CC;
+  float* part = partial + blk * rg_param_floats(D);
+  float* pW1 = part;
+  float* pb1 = part + 64 * (int64_t)D;
+  float* pgw = pb1 + 64;
+  float* pgb = pgw + 64;
+  float* pW2 = pgb + 64;
+  float* pb2 = pW2 + 64 * (int64_t)D;
+  // ---- layer 1, both nets (the forward kernel's loop) ----
+  RfChunk ch;
+  rf_load1(ch, x, n, D, row0, 0, tn.w1, pn.w1);
+  f32x16 acc[4] = {};
+  rf_store1(ch, stage);
+  __syncthreads();
+  for (int c = 0; c < nk; ++c) {
+    if (c + 1 < nk) rf_load1(ch, x, n, D, row0, (c + 1) * RF_KC, tn.w1, pn.w1);
+    else rf_load2(ch, D, 0, tn.w2, pn.w2);
+    const float* bx = stage + (c & 1) * 2 * RF_M * RF_P1;
+    const float* ax = bx + (32 * w + lr) * RF_P1 + lh;
+    const float* bw = bx + RF_M * RF_P1 + lr * RF_P1 + lh;
+    float av[RF_KC / 2], bv[4][RF_KC / 2];
+#pragma unroll
+    for (int k = 0; k < RF_KC / 2; ++k) {
+      av[k] = ax[2 * k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j][k] = bw[32 * j * RF_P1 + 2 * k];
+    }
+#pragma unroll
+    for (int k = 0; k < RF_KC / 2; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[k], bv[j][k], acc[j], 0, 0, 0);
+    if (c + 1 < nk) rf_store1(ch, stage + ((c + 1) & 1) * 2 * RF_M * RF_P1);
+    __syncthreads();
+  }
+  // ---- bias + GroupNorm + SiLU into Z = [S_pred | -S_target] (the forward kernel's epilogue) ----
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const RndNet& nn = j < 2 ? tn : pn;
+    const int u = 32 * (j & 1) + lr;
+    const float bb = nn.b1[u], gw = nn.gw[u], gb = nn.gb[u];
+    const int zc = (j < 2 ? 64 : 0) + u;
+    const float sgn = j < 2 ? -1.0f : 1.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float v = acc[j][i] + bb;
+      const float mean = rf_sum8(v) * 0.125f;
+      const float d = v - mean;
+      const float var = rf_sum8(d * d) * 0.125f;
+      const float y = d * __builtin_amdgcn_rsqf(var + 1e-5f) * gw + gb;
+      zs[(32 * w + c_row(i, lane)) * RF_PZ + zc] = sgn * (y * __builtin_amdgcn_rcpf(1.0f + __expf(-y)));
+    }
+  }
+  // ---- layer 2 chunks: dY, dW2, db2, dS_p ----
+  f32x16 ds0 = {}, ds1 = {};   // dS_p [rows 32w ..][units lr, 32 + lr]
+  for (int c = 0; c < nc; ++c) {
+    rf_store2(ch, w2s);        // (the previous chunk's reads ended at the loop's last barrier)
+    __syncthreads();           // Z (first chunk), this W2 chunk
+    if (c + 1 < nc) rf_load2(ch, D, (c + 1) * RF_CC, tn.w2, pn.w2);
+    const int col0 = c * RF_CC;
+    f32x16 y0 = {}, y1 = {};
+    {
+      const float* az = zs + (32 * w + lr) * RF_PZ + lh;
+      const float* b0 = w2s + lr * RF_PW + lh;
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 32) {
+        float a[16], c0[16], c1[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          a[k] = az[k0 + 2 * k];
+          c0[k] = b0[k0 + 2 * k];
+          c1[k] = b0[32 * RF_PW + k0 + 2 * k];
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k], c0[k], y0, 0, 0, 0);
+          y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k], c1[k], y1, 0, 0, 0);
+        }
+      }
+    }
+    const int col_a = col0 + lr, col_b = col_a + 32;
+    const float bd_a = col_a < D ? pn.b2[col_a] - tn.b2[col_a] : 0.f;
+    const float bd_b = col_b < D ? pn.b2[col_b] - tn.b2[col_b] : 0.f;
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = 32 * w + c_row(i, lane);
+      const bool rin = row0 + r < n;
+      const float da = (rin && col_a < D) ? scale * (y0[i] + bd_a) : 0.f;
+      const float db = (rin && col_b < D) ? scale * (y1[i] + bd_b) : 0.f;
+      dys[r * RG_PD + lr] = da;
+      dys[r * RG_PD + 32 + lr] = db;
+      sa += da;
+      sb += db;
+    }
+    sa += __shfl_xor(sa, 32, 64);
+    sb += __shfl_xor(sb, 32, 64);
+    if (lh == 0) {
+      cb[w * 64 + lr] = sa;
+      cb[w * 64 + 32 + lr] = sb;
+    }
+    __syncthreads();           // dY, the column sums
+    // dS_p += dY[rows of wave w][64 cols] . W2_p[cols][units] (K = the chunk's 64 columns)
+    {
+      const float* ad = dys + (32 * w + lr) * RG_PD + lh;
+      const float* bw2 = w2s + lh * RF_PW + lr;
+#pragma unroll
+      for (int k0 = 0; k0 < 64; k0 += 16) {
+        float a[8], b0v[8], b1v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          a[k] = ad[k0 + 2 * k];
+          b0v[k] = bw2[(k0 + 2 * k) * RF_PW];
+          b1v[k] = bw2[(k0 + 2 * k) * RF_PW + 32];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          ds0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k], b0v[k], ds0, 0, 0, 0);
+          ds1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k], b1v[k], ds1, 0, 0, 0);
+        }
+      }
+    }
+    // dW2[col0 + 32 (w & 1) + m][32 (w >> 1) + unit] = sum over the 128 rows of dY[row][col] S_p[row][unit]
+    {
+      const int chf = w & 1, uh = w >> 1;
+      const float* ad = dys + lh * RG_PD + 32 * chf + lr;
+      const float* bz = zs + lh * RF_PZ + 32 * uh + lr;
+      f32x16 t = {};
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 32) {
+        float a[16], b[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          a[k] = ad[(k0 + 2 * k) * RG_PD];
+          b[k] = bz[(k0 + 2 * k) * RF_PZ];
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) t = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k], b[k], t, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int col = col0 + 32 * chf + c_row(i, lane);
+        if (col < D) pW2[(int64_t)col * 64 + 32 * uh + lr] = t[i];
+      }
+    }
+    if (tid < 64 && col0 + tid < D)
+      pb2[col0 + tid] = (cb[tid] + cb[64 + tid]) + (cb[128 + tid] + cb[192 + tid]);
+    __syncthreads();           // every read of this W2 chunk, dY and cb done
+  }
+  // ---- GroupNorm + SiLU backward of the predictor's hidden layer (wave w: rows 32w .. 32w + 31) ----
+  float sgw[2] = {0.f, 0.f}, sgb[2] = {0.f, 0.f}, sb1[2] = {0.f, 0.f};
+  float* dhs = zs;   // Z's last reads (the last chunk's dW2) are behind the loop's last barrier
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int u = 32 * jj + lr;
+    const float bb = pn.b1[u], gw = pn.gw[u], gb = pn.gb[u];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float v = acc[2 + jj][i] + bb;
+      const float mean = rf_sum8(v) * 0.125f;
+      const float d = v - mean;
+      const float var = rf_sum8(d * d) * 0.125f;
+      const float rs = __builtin_amdgcn_rsqf(var + 1e-5f);
+      const float xh = d * rs;
+      const float y = xh * gw + gb;
+      const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-y));
+      const float dsv = jj == 0 ? ds0[i] : ds1[i];
+      const float dy = dsv * (sg * (1.0f + y * (1.0f - sg)));   // d silu(y) / dy
+      const float dxh = dy * gw;
+      const float m1 = rf_sum8(dxh) * 0.125f;
+      const float m2 = rf_sum8(dxh * xh) * 0.125f;
+      const float dv = rs * (dxh - m1 - xh * m2);
+      sgw[jj] += dy * xh;
+      sgb[jj] += dy;
+      sb1[jj] += dv;
+      dhs[(32 * w + c_row(i, lane)) * RG_PH + u] = dv;
+    }
+  }
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    sgw[jj] += __shfl_xor(sgw[jj], 32, 64);
+    sgb[jj] += __shfl_xor(sgb[jj], 32, 64);
+    sb1[jj] += __shfl_xor(sb1[jj], 32, 64);
+    if (lh == 0) {
+      cs[(w * 3 + 0) * 64 + 32 * jj + lr] = sb1[jj];
+      cs[(w * 3 + 1) * 64 + 32 * jj + lr] = sgw[jj];
+      cs[(w * 3 + 2) * 64 + 32 * jj + lr] = sgb[jj];
+    }
+  }
+  float4 xv[4];
+  rg_loadx(xv, x, n, D, row0, 0);
+  __syncthreads();             // dH, the column sums
+  if (tid < 3 * 64) {
+    const int k = tid >> 6, u = tid & 63;
+    const float v = (cs[(0 * 3 + k) * 64 + u] + cs[(1 * 3 + k) * 64 + u]) +
+                    (cs[(2 * 3 + k) * 64 + u] + cs[(3 * 3 + k) * 64 + u]);
+    (k == 0 ? pb1 : k == 1 ? pgw : pgb)[u] = v;
+  }
+  // ---- dW1[unit][col] = sum over the 128 rows of dH[row][unit] X[row][col], 32 columns a chunk ----
+  const int x16 = lane & 15, q = lane >> 4;
+  for (int c = 0; c < nk; ++c) {
+    rg_storex(xv, xs);         // (the previous chunk's reads ended at the loop's last barrier)
+    __syncthreads();
+    if (c + 1 < nk) rg_loadx(xv, x, n, D, row0, (c + 1) * RF_KC);
+    const float* ah = dhs + q * RG_PH + 16 * w + x16;
+    const float* bxs = xs + q * RG_PX + x16;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v u0 = {0.f, 0.f, 0.f, 0.f}, u1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k0 = 0; k0 < 128; k0 += 32) {
+      float a[8], b0v[8], b1v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        a[k] = ah[(k0 + 4 * k) * RG_PH];
+        b0v[k] = bxs[(k0 + 4 * k) * RG_PX];
+        b1v[k] = bxs[(k0 + 4 * k) * RG_PX + 16];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        u0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k], b0v[k], u0, 0, 0, 0);
+        u1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k], b1v[k], u1, 0, 0, 0);
+      }
+    }
+    const int colb = c * RF_KC + x16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t urow = (int64_t)(16 * w + 4 * q + i) * D;
+      if (colb < D) pW1[urow + colb] = u0[i];
+      if (colb + 16 < D) pW1[urow + colb + 16] = u1[i];
+    }
+    __syncthreads();
+  }
+}
+
+// grad[p] = sum over blocks b = 0, 1, ... of partial[b][p] (f64, in block order)
+__global__ __launch_bounds__(256) void rnd_grad_fold_kernel(const float* __restrict__ partial, int64_t nblk,
+                                                            int64_t P, float* __restrict__ grad) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  double s = 0.0;
+  int64_t b = 0;
+  for (; b + 4 <= nblk; b += 4) {
+    const float v0 = partial[b * P + p], v1 = partial[(b + 1) * P + p], v2 = partial[(b + 2) * P + p],
+                v3 = partial[(b + 3) * P + p];
+    s += (double)v0;
+    s += (double)v1;
+    s += (double)v2;
+    s += (double)v3;
+  }
+  for (; b < nblk; ++b) s += (double)partial[b * P + p];
+  grad[p] = (float)s;
+}
 }  // namespace prl
 
 using namespace prl;
@@ -400,5 +713,50 @@ extern "C" int prl_rnd_forward(const float* x, int64_t n, int32_t D, const float
   hipLaunchKernelGGL(rnd_forward_kernel, dim3((unsigned)cdiv(n, RB_M)), dim3(256), 0, st, x, n, (int)D,
                      tn, pn, beta, out);
   PRL_LAUNCH_CHECK("rnd_forward");
+  return PRL_OK;
+}
+
+extern "C" int64_t prl_rnd_pred_grad_ws_floats(int64_t n, int32_t D) {
+  if (n <= 0 || D <= 0) return 0;
+  return cdiv(n, RF_M) * (129 * (int64_t)D + 192);
+}
+
+extern "C" int prl_rnd_pred_grad(const float* x, int64_t n, int32_t D, const float* t_w1,
+                                 const float* t_b1, const float* t_gw, const float* t_gb,
+                                 const float* t_w2, const float* t_b2, const float* p_w1,
+                                 const float* p_b1, const float* p_gw, const float* p_gb,
+                                 const float* p_w2, const float* p_b2, float scale, float* partial,
+                                 int64_t partial_floats, float* grad, void* stream) {
+  PRL_REQUIRE(n >= 0 && D > 0, "prl_rnd_pred_grad: bad sizes");
+  PRL_REQUIRE(D % 4 == 0, "prl_rnd_pred_grad: D = %d is not a multiple of 4", (int)D);
+  const int64_t P = 129 * (int64_t)D + 192;
+  PRL_REQUIRE(grad, "prl_rnd_pred_grad: null gradient");
+  hipStream_t st = as_stream(stream);
+  if (n == 0) {
+    PRL_HIP_TRY(hipMemsetAsync(grad, 0, P * sizeof(float), st));
+    return PRL_OK;
+  }
+  PRL_REQUIRE(x && partial && t_w1 && t_b1 && t_gw && t_gb && t_w2 && t_b2 && p_w1 && p_b1 && p_gw &&
+                  p_gb && p_w2 && p_b2,
+              "prl_rnd_pred_grad: null pointer");
+  PRL_REQUIRE(aligned16(x) && aligned16(t_w1) && aligned16(p_w1) && aligned16(t_w2) && aligned16(p_w2),
+              "prl_rnd_pred_grad: x / W1 / W2 must be 16-B aligned");
+  const int64_t nblk = cdiv(n, RF_M);
+  PRL_REQUIRE(nblk < (int64_t)0x7fffffff, "prl_rnd_pred_grad: n too large");
+  PRL_REQUIRE(partial_floats >= nblk * P, "prl_rnd_pred_grad: partial buffer %lld < %lld floats",
+              (long long)partial_floats, (long long)(nblk * P));
+  static bool attr = false;
+  if (!attr) {
+    PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(rnd_pred_grad_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)(RG_LDS * sizeof(float))));
+    attr = true;
+  }
+  RndNet tn{t_w1, t_b1, t_gw, t_gb, t_w2, t_b2}, pn{p_w1, p_b1, p_gw, p_gb, p_w2, p_b2};
+  hipLaunchKernelGGL(rnd_pred_grad_kernel, dim3((unsigned)nblk), dim3(256), RG_LDS * sizeof(float), st, x, n,
+                     (int)D, tn, pn, scale, partial);
+  PRL_LAUNCH_CHECK("rnd_pred_grad");
+  hipLaunchKernelGGL(rnd_grad_fold_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, st, partial, nblk, P,
+                     grad);
+  PRL_LAUNCH_CHECK("rnd_grad_fold");
   return PRL_OK;
 }

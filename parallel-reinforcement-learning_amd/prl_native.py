@@ -56,6 +56,8 @@ SIGNATURES = {
                               _I64, _P],
     "prl_ppo_surrogate_bwd": [_P, _P, _P, _I64, _P, _P, _P],
     "prl_rnd_forward": [_P, _I64, _I32] + [_P] * 12 + [_F32, _P, _P],
+    "prl_rnd_pred_grad": [_P, _I64, _I32] + [_P] * 12 + [_F32, _P, _I64, _P, _P],
+    "prl_rnd_pred_grad_ws_floats": [_I64, _I32],
     "prl_gn_silu_fwd": [_P, _I64, _I32, _I32, _P, _P, _F32, _I32, _P, _P],
     "prl_gn_silu_bwd": [_P, _P, _I64, _I32, _I32, _P, _P, _F32, _I32, _P, _P, _P, _P, _I64, _P],
     "prl_gather_minibatch": [_P, _P, _P, _I32, _P, _I64, _I64, _P],
@@ -111,7 +113,8 @@ SIGNATURES = {
                               + [_I64, _I32, _I64, _F32] + _UPD_SCALARS + [_P, _P, _P, _I64, _P],
 }
 _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_source_id": ctypes.c_char_p,
-             "prl_ppo_update_last_plan": None, "prl_workspace_bytes": _I64, "prl_dp_xbuf_bytes": _I64,
+             "prl_ppo_update_last_plan": None, "prl_workspace_bytes": _I64,
+             "prl_rnd_pred_grad_ws_floats": _I64, "prl_dp_xbuf_bytes": _I64,
              "prl_dp_set_spin_limit": ctypes.c_uint32, "prl_ppo_update_set_tp": _I32,
              "prl_ppo_update_set_repl": _I32, "prl_ppo_update_set_split": _I32,
              "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
@@ -456,6 +459,21 @@ def rnd_forward(x, tnet, pnet, beta, out):
             for p in (*tnet, *pnet)]
     _check(lib().prl_rnd_forward(_dev(x, torch.float32, "x"), n, D, *ptrs, float(beta),
                                  _dev(out, torch.float32, "out"), _stream()), "prl_rnd_forward")
+
+
+def rnd_pred_grad_ws_floats(n: int, D: int) -> int:
+    return int(lib().prl_rnd_pred_grad_ws_floats(int(n), int(D)))
+
+
+def rnd_pred_grad(x, tnet, pnet, scale, partial, grad):
+    """RND.update_pred's predictor gradient for the minibatch x (prl_rnd_pred_grad): grad (flat,
+    the predictor's parameters() order) = d/dpred MSE('mean') scaled so that scale = 2 / (rows D)
+    is the reference's mean.  tnet / pnet: (w1, b1, gw, gb, w2, b2) float32 device tensors."""
+    n, D = x.shape
+    ptrs = [_dev(p, torch.float32, "rnd param") for p in (*tnet, *pnet)]
+    _check(lib().prl_rnd_pred_grad(_dev(x, torch.float32, "x"), n, D, *ptrs, float(scale),
+                                   _dev(partial, torch.float32, "partial"), partial.numel(),
+                                   _dev(grad, torch.float32, "grad"), _stream()), "prl_rnd_pred_grad")
 
 
 # ------------------------------------------------------------------------- GroupNorm + SiLU

@@ -22,7 +22,7 @@ def test_abi_library_exports_every_declared_symbol():
     import prl_native
     L = prl_native.lib()
     syms = _declared_symbols()
-    assert len(syms) == len(prl_native.SIGNATURES) == 66
+    assert len(syms) == len(prl_native.SIGNATURES) == 68
     for s in syms:
         assert hasattr(L, s), s
         assert s in prl_native.SIGNATURES, f"{s} has no ctypes signature"
