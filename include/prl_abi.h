@@ -219,7 +219,8 @@ int prl_rnd_forward(const float* x, int64_t n, int32_t D,
  * predictor's whole backward, written to grad[129 D + 192] in the predictor's parameters() order
  * (W1[64][D], b1[64], gamma[64], beta[64], W2[D][64], b2[D]).  One launch per 128-row block into
  * partial[ceil(n / 128)][129 D + 192] (partial_floats >= prl_rnd_pred_grad_ws_floats(n, D)), then
- * a fold in block order (f64): deterministic.  D % 4 == 0; x, W1, W2 16-B aligned. */
+ * a fold in a fixed order (f64: 16 segments of blocks, each in block order, then the segments in
+ * order): deterministic.  D % 4 == 0; x, W1, W2, partial 16-B aligned. */
 int prl_rnd_pred_grad(const float* x, int64_t n, int32_t D,
                       const float* t_w1, const float* t_b1, const float* t_gw, const float* t_gb,
                       const float* t_w2, const float* t_b2,

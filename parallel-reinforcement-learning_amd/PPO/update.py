@@ -189,7 +189,10 @@ class GraphedUpdate:
         if info is not None:
             self.wide = info
             self.part = torch.empty(info[1], dtype=torch.float32, device=dev)
-            self.cursor_e = torch.zeros(1, dtype=torch.int64, device=dev)
+            # the eager steps' minibatch indices as one device arange: step j reads the view
+            # [j : j + 1] (no fill kernel per step; the kernel takes the index from the device)
+            nbj = -(-S.shape[0] // mb)
+            self.cursor_all = torch.arange(max(nbj, 1), dtype=torch.int64, device=dev)
             self.sources[1] = self.sources[1].float().contiguous()
             # parameters / gradient / AdamW state as flat vectors: the kernel reads the
             # parameters in place and clip_grad_norm_ + AdamW are one launch (prl_flat_adamw);
@@ -219,8 +222,7 @@ class GraphedUpdate:
     def wide_step(self, j: int):
         """One eager optimizer step on minibatch j through the wide kernel (single rank: the
         ragged last minibatch of an epoch)."""
-        self.cursor_e.fill_(j)
-        self._wide_grad(self.cursor_e, None)
+        self._wide_grad(self.cursor_all[j:j + 1], None)
         if self.fa is not None:
             self.fa.launch(self.ppo._flat_grad)
         else:

@@ -377,8 +377,8 @@ __global__ __launch_bounds__(256, 1) void rnd_forward_fast_kernel(const float* _
 //   dW1       = dH_p^T X: the block's X re-streamed in 32-column chunks, v_mfma_f32_16x16x4_f32
 //             (wave w: units 16w .. 16w + 15), K = 128 rows.
 // Every block writes its partial gradient in the flat parameter order (W1, b1, gamma, beta, W2,
-// b2: torch parameters() of the predictor), and rnd_grad_fold_kernel sums the blocks in order
-// (f64): deterministic, no atomics.
+// b2: torch parameters() of the predictor), and rnd_grad_fold{1,2}_kernel sum the blocks in a
+// fixed order (f64): deterministic, no atomics.
 constexpr int RG_PD = 65;                 // pitch of dY [128][64] (odd: conflict-free row reads)
 constexpr int RG_PH = 80;                 // pitch of dH [128][64] (16-lane groups on 4 bank offsets)
 constexpr int RG_PX = 48;                 // pitch of the dW1 phase's X chunk [128][32]
@@ -655,22 +655,37 @@ __global__ __launch_bounds__(256, 1) void rnd_pred_grad_kernel(const float* __re
   }
 }
 
-// grad[p] = sum over blocks b = 0, 1, ... of partial[b][p] (f64, in block order)
-__global__ __launch_bounds__(256) void rnd_grad_fold_kernel(const float* __restrict__ partial, int64_t nblk,
-                                                            int64_t P, float* __restrict__ grad) {
+// grad[p] = sum over blocks of partial[b][p], in two passes for parallelism: pass 1, thread
+// (4 consecutive p, segment g) sums blocks [g nblk / RG_SEG, (g + 1) nblk / RG_SEG) in f64 block
+// order (16-B loads), into seg[g][p]; pass 2 adds the RG_SEG segments in order.  Deterministic.
+constexpr int RG_SEG = 16;
+__global__ __launch_bounds__(256) void rnd_grad_fold1_kernel(const float* __restrict__ partial, int64_t nblk,
+                                                             int64_t P, double* __restrict__ seg) {
+  const int64_t p4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int g = blockIdx.y;
+  if (p4 >= P) return;
+  const int64_t b0 = nblk * g / RG_SEG, b1 = nblk * (g + 1) / RG_SEG;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  for (int64_t b = b0; b < b1; ++b) {
+    const float4 v = *reinterpret_cast<const float4*>(partial + b * P + p4);
+    s0 += (double)v.x;
+    s1 += (double)v.y;
+    s2 += (double)v.z;
+    s3 += (double)v.w;
+  }
+  double* o = seg + (int64_t)g * P + p4;
+  o[0] = s0;
+  o[1] = s1;
+  o[2] = s2;
+  o[3] = s3;
+}
+__global__ __launch_bounds__(256) void rnd_grad_fold2_kernel(const double* __restrict__ seg, int64_t P,
+                                                             float* __restrict__ grad) {
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (p >= P) return;
   double s = 0.0;
-  int64_t b = 0;
-  for (; b + 4 <= nblk; b += 4) {
-    const float v0 = partial[b * P + p], v1 = partial[(b + 1) * P + p], v2 = partial[(b + 2) * P + p],
-                v3 = partial[(b + 3) * P + p];
-    s += (double)v0;
-    s += (double)v1;
-    s += (double)v2;
-    s += (double)v3;
-  }
-  for (; b < nblk; ++b) s += (double)partial[b * P + p];
+#pragma unroll
+  for (int g = 0; g < RG_SEG; ++g) s += seg[(int64_t)g * P + p];
   grad[p] = (float)s;
 }
 }  // namespace prl
@@ -718,7 +733,8 @@ extern "C" int prl_rnd_forward(const float* x, int64_t n, int32_t D, const float
 
 extern "C" int64_t prl_rnd_pred_grad_ws_floats(int64_t n, int32_t D) {
   if (n <= 0 || D <= 0) return 0;
-  return cdiv(n, RF_M) * (129 * (int64_t)D + 192);
+  const int64_t P = 129 * (int64_t)D + 192;
+  return cdiv(n, RF_M) * P + 2 * RG_SEG * P + 4;   // block partials | f64 segment sums (+ alignment)
 }
 
 extern "C" int prl_rnd_pred_grad(const float* x, int64_t n, int32_t D, const float* t_w1,
@@ -743,8 +759,10 @@ extern "C" int prl_rnd_pred_grad(const float* x, int64_t n, int32_t D, const flo
               "prl_rnd_pred_grad: x / W1 / W2 must be 16-B aligned");
   const int64_t nblk = cdiv(n, RF_M);
   PRL_REQUIRE(nblk < (int64_t)0x7fffffff, "prl_rnd_pred_grad: n too large");
-  PRL_REQUIRE(partial_floats >= nblk * P, "prl_rnd_pred_grad: partial buffer %lld < %lld floats",
-              (long long)partial_floats, (long long)(nblk * P));
+  const int64_t need = nblk * P + 2 * RG_SEG * P + 4;
+  PRL_REQUIRE(partial_floats >= need, "prl_rnd_pred_grad: partial buffer %lld < %lld floats",
+              (long long)partial_floats, (long long)need);
+  PRL_REQUIRE(aligned16(partial), "prl_rnd_pred_grad: partial must be 16-B aligned");
   static bool attr = false;
   if (!attr) {
     PRL_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(rnd_pred_grad_kernel),
@@ -755,8 +773,12 @@ extern "C" int prl_rnd_pred_grad(const float* x, int64_t n, int32_t D, const flo
   hipLaunchKernelGGL(rnd_pred_grad_kernel, dim3((unsigned)nblk), dim3(256), RG_LDS * sizeof(float), st, x, n,
                      (int)D, tn, pn, scale, partial);
   PRL_LAUNCH_CHECK("rnd_pred_grad");
-  hipLaunchKernelGGL(rnd_grad_fold_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, st, partial, nblk, P,
-                     grad);
-  PRL_LAUNCH_CHECK("rnd_grad_fold");
+  // f64 segment sums after the block partials, 8-B aligned (P % 4 == 0: the partials end 16-B aligned)
+  double* seg = reinterpret_cast<double*>(partial + nblk * P);
+  hipLaunchKernelGGL(rnd_grad_fold1_kernel, dim3((unsigned)cdiv(P / 4, 256), RG_SEG), dim3(256), 0, st, partial,
+                     nblk, P, seg);
+  PRL_LAUNCH_CHECK("rnd_grad_fold1");
+  hipLaunchKernelGGL(rnd_grad_fold2_kernel, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, st, seg, P, grad);
+  PRL_LAUNCH_CHECK("rnd_grad_fold2");
   return PRL_OK;
 }
