@@ -258,22 +258,24 @@ __device__ __forceinline__ void spl_tile(const UpdNet& n, const UpdArgs& args, i
     }
   }
   SPL_CMARK(6)
-  // ---- the head's output biases and loss partials (wave 3; its own dO rows and lp lanes)
-  if (w == SPL_NW - 1) {
-    if (l < no) {   // f64 sum: the softmax outputs' dO cancel across rows
-      double acc = 0.0;
+  // ---- the head's output biases and loss partials, spread over waves 1-3 (every wave holds the
+  //      same dO rows and lp lanes; the tile's last barrier waits for the slowest wave): wave 1
+  //      the biases, wave 2 loss partial k = 0 or 1 (the actor's surrogate / the critic's
+  //      SmoothL1), wave 3 the actor's entropy partial k = 2
+  if (w == 1 && l < no) {   // f64 sum: the softmax outputs' dO cancel across rows
+    double acc = 0.0;
 #pragma unroll
-      for (int r = 0; r < UPD_RT; ++r) acc += (double)dOw[r * 16 + oc + l];
-      Ga[(h == 0 ? n.b2[0].lds : n.b2[1].lds) + l] = (float)acc;
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const bool mine = h == 0 ? k != 1 : k == 1;
-      if (mine) {
-        const float s = upd_rsum16(lp[k]);
-        if (l == 0) Ga[n.Lp + k] = s;
-      }
-    }
+    for (int r = 0; r < UPD_RT; ++r) acc += (double)dOw[r * 16 + oc + l];
+    Ga[(h == 0 ? n.b2[0].lds : n.b2[1].lds) + l] = (float)acc;
+  }
+  if (w == 2) {
+    const int k = h == 0 ? 0 : 1;
+    const float s = upd_rsum16(lp[k]);
+    if (l == 0) Ga[n.Lp + k] = s;
+  }
+  if (w == 3 && h == 0) {
+    const float s = upd_rsum16(lp[2]);
+    if (l == 0) Ga[n.Lp + 2] = s;
   }
   SPL_CMARK(7)
 #undef SPL_CMARK
