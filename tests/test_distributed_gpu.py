@@ -222,6 +222,31 @@ def test_two_ranks_persistent_dp_engine_push_form(tmp_path, xbuf):
     assert float(push[0]["_loss"]) == float(pull[0]["_loss"])
 
 
+def test_four_ranks_persistent_dp_engine_push_equals_pull(tmp_path):
+    """4 data-parallel ranks sharing cuda:0 (4 x 8 split workgroups at mb 64), unequal shards
+    (rank 1 one minibatch short), two learn() calls: the push form (the default) gives exactly
+    the pull form's bits, and all four ranks end bit-identical — the exchange's rank-order sums
+    at more than two ranks, as the 8-rank node runs them."""
+    import random
+    mb, nb, k, world = 64, 5, 3, 4
+    port = 29600 + random.randint(0, 30)
+    mp.spawn(_dpx_worker, args=(world, port, mb, nb, k, str(tmp_path), "auto", False), nprocs=world,
+             join=True)
+    mp.spawn(_dpx_worker, args=(world, port + 40, mb, nb, k, str(tmp_path), "auto", True),
+             nprocs=world, join=True)
+    pull = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(world)]
+    push = [np.load(os.path.join(tmp_path, f"pushrank{r}.npz")) for r in range(world)]
+    assert int(push[0]["_push"]) == 1 and int(pull[0]["_push"]) == 0
+    assert int(push[0]["_split"]) == 1 and str(push[0]["_path"]) == "fused-dp-persistent"
+    for key in pull[0].files:
+        if key.startswith("_"):
+            continue
+        for r in range(world):
+            np.testing.assert_array_equal(pull[r][key], pull[0][key], err_msg=key)
+            np.testing.assert_array_equal(push[r][key], pull[0][key], err_msg=key)
+    assert float(push[0]["_loss"]) == float(pull[0]["_loss"])
+
+
 def _nccl_one_rank_worker(port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PRL_DP_NATIVE="1")
     sys.path[:0] = PATHS
