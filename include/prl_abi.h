@@ -487,7 +487,7 @@ int prl_debug_fill_lds(float value, void* stream);
  * out[4] = 1 for a compile-time-layout (CartPole / Pendulum) kernel, 0 for the runtime layout;
  * out[5] = workgroups per tile group (the latency form's replicated tiles, PRL_UPD_REPL; out[2]
  * counts them all; the split form: its two head roles); out[6] = 1 for the head-split latency
- * form.  All -1 before the first launch.  No reference counterpart (tests assert which kernel
+ * form, 2 for its slice-owner variant (AdamW by the slice owners, PRL_UPD_SPL_OWN).  All -1 before the first launch.  No reference counterpart (tests assert which kernel
  * ran). */
 void prl_ppo_update_last_plan(int32_t out[7]);
 /* A zeroed slice buffer of its own (shareable by IPC handle).  *kind in: 0 = uncached, falling

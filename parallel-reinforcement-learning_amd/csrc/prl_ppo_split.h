@@ -415,7 +415,10 @@ template <int NT>
 __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu_buffer_rsrc_t rs_part2,
                                         __amdgpu_buffer_rsrc_t rs_red, int Qtot, int Qp, int QT,
                                         const SplSlice& pl, int Gt, float* scratch, bool sys,
-                                        UpdSub sub, const UpdArgs& args, int par) {
+                                        UpdSub sub, const UpdArgs& args, int par,
+                                        float4* gout = nullptr) {
+  // gout (the slice-owner form, narrow slices only): thread t < nq keeps its quad's reduced
+  // gradient in *gout instead of storing it (the loss quad Qp is stored as always)
   const int t = threadIdx.x;
   const int qlo = pl.qlo, qhi = pl.qhi, nq = pl.nq;
   if (nq <= 0) return;
@@ -466,7 +469,8 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
       const double* o = red + 4 * (k * nq + t);
       ax += o[0]; ay += o[1]; az += o[2]; aw += o[3];
     }
-    fin(qlo + t, ax, ay, az, aw);
+    if (gout && qlo + t != Qp) *gout = float4{(float)ax, (float)ay, (float)az, (float)aw};
+    else fin(qlo + t, ax, ay, az, aw);
   }
   sub.mark(1);   // slice combined, its stores issued
 }
@@ -476,7 +480,18 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
 // DP: data-parallel ranks (prl_ppo_update_dpx): union-minibatch row weights inv_count[j] and,
 // after phase B, the cross-rank sum of each slice (upd_dp_union_slice, as the 8-wave kernel);
 // the 2 Gt workgroups of every rank cut the gradient into the same 2 Gt slices.
-template <int NQC, int KA, bool DP, int TW>
+// OWN: the slice-owner form (one rank, narrow slices: every workgroup's slice has at most NT / 2
+// quads).  The owner of a slice quad keeps that quad's AdamW moments and runs its AdamW in phase
+// B, with clip coefficient 1, and publishes the NEW WEIGHTS (and its waves' pieces of the clip
+// norm) instead of the gradient; phase C loads the weights into LDS.  So AdamW runs once per quad
+// on the chip (one quad per owning thread) instead of once per workgroup over ~1,185 quads, and
+// no workgroup holds moment registers for the whole net.  clip_grad_norm_ scales a step only when
+// the norm (summed from the pieces in one fixed order, the same on every workgroup) exceeds
+// max_norm: then every workgroup sees it, the owners redo their quads from the kept gradient,
+// moments and the LDS weights (not yet replaced) with the true coefficient, and one more
+// hand-off (counter C, the corrected weights in red_c) follows.  The same AdamW arithmetic per
+// element as the workgroup form, so the same bits whenever the clip coefficient is the same.
+template <int NQC, int KA, bool DP, int TW, bool OWN = false>
 __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& args) {
   constexpr int SPL_NT = 64 * TW;
   extern __shared__ __align__(16) float upd_lds[];
@@ -502,15 +517,24 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
   float* s_adam = hdr + 10;
 
-  float4 mreg[NQC], vreg[NQC];
+  constexpr int NMR = OWN ? 1 : NQC;
+  float4 mreg[NMR], vreg[NMR];
   for (int q = t; q < Qp; q += SPL_NT)
     *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(args.params + 4 * q);
+  // OWN: this thread's slice quad (see slc below) and its moments
+  const SplSlice slc0 = spl_slice_plan<SPL_NT>(g, G, Qp, QT, Gt, args.spl_fill);
+  const int oq = (OWN && t < slc0.nq && slc0.qlo + t < Qp) ? slc0.qlo + t : -1;
+  if constexpr (OWN) {
+    mreg[0] = oq >= 0 ? *reinterpret_cast<const float4*>(args.exp_avg + 4 * oq) : float4{0.f, 0.f, 0.f, 0.f};
+    vreg[0] = oq >= 0 ? *reinterpret_cast<const float4*>(args.exp_avg_sq + 4 * oq) : float4{0.f, 0.f, 0.f, 0.f};
+  } else {
 #pragma unroll
-  for (int i = 0; i < NQC; ++i) {
-    const int q = slotq(i);
-    const bool own = q >= 0;
-    mreg[i] = own ? *reinterpret_cast<const float4*>(args.exp_avg + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
-    vreg[i] = own ? *reinterpret_cast<const float4*>(args.exp_avg_sq + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NQC; ++i) {
+      const int q = slotq(i);
+      const bool own = q >= 0;
+      mreg[i] = own ? *reinterpret_cast<const float4*>(args.exp_avg + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+      vreg[i] = own ? *reinterpret_cast<const float4*>(args.exp_avg_sq + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
+    }
   }
   const float step0 = args.adam_step[0];
   if (t < 24) reinterpret_cast<unsigned long long*>(hdr + 16)[t] = 0ull;
@@ -592,7 +616,32 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   float loss_last = 0.f;
-  const SplSlice slc = spl_slice_plan<SPL_NT>(g, G, Qp, QT, Gt, args.spl_fill);
+  const SplSlice& slc = slc0;
+  // the AdamW arithmetic of one quad (the engine's 4-wave scalar form): clipped gradient g4 * c
+  auto adamw_quad = [&](const float4 g4, float4& m4, float4& v4, float4& pw, float clipc) {
+    const float step_size = s_adam[0];
+    const float inv_bc2_sqrt = s_adam[1];
+    const float decay = (float)(1.0 - (double)args.lr * (double)args.wd);
+    const float b2 = (float)args.beta2;
+    const float omb1 = (float)(1.0 - (double)args.beta1), omb2 = (float)(1.0 - (double)args.beta2);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gr = f4get(g4, e) * clipc;
+      float m = f4get(m4, e), v = f4get(v4, e), p = f4get(pw, e);
+      p = p * decay;
+      m = fmaf(omb1, gr - m, m);
+      v = fmaf(omb2 * gr, gr, v * b2);
+      const float denom = fmaf(__builtin_amdgcn_sqrtf(v), inv_bc2_sqrt, args.eps);
+      float rq = __builtin_amdgcn_rcpf(denom);
+      rq = fmaf(rq, fmaf(-denom, rq, 1.0f), rq);
+      p = fmaf(-step_size, m * rq, p);
+      f4set(m4, e, m);
+      f4set(v4, e, v);
+      f4set(pw, e, p);
+    }
+  };
+  float4 og = {0.f, 0.f, 0.f, 0.f}, onm = {0.f, 0.f, 0.f, 0.f}, onv = {0.f, 0.f, 0.f, 0.f};
+  unsigned nclip = 0;   // OWN: clipped steps so far (counter C's target), the same on every workgroup
   int j = 0;   // s mod nb
   int Bj = B_of(0);
   for (int s = 0; s < args.total_steps; ++s) {
@@ -661,7 +710,22 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       const unsigned long long gstep = args.dp_seq0 + (unsigned long long)s;
       const int par = (int)(gstep & 1ull);
       spl_slice_reduce<SPL_NT>(rs_part, rs_part2, DP ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
-                               Qtot, Qp, QT, slc, Gt, scratch, DP, subm, args, par);
+                               Qtot, Qp, QT, slc, Gt, scratch, DP, subm, args, par, OWN ? &og : nullptr);
+      if constexpr (OWN) {
+        // the owner's speculative AdamW (clip coefficient 1) on its quad; the new weights go out
+        // in place of the gradient, with this wave's piece of the squared norm
+        float sqv = 0.f;
+        if (oq >= 0) {
+          float4 pw = *reinterpret_cast<const float4*>(W + 4 * oq);
+          onm = mreg[0];
+          onv = vreg[0];
+          adamw_quad(og, onm, onv, pw, 1.0f);
+          st4_sc1(rs_red, (size_t)oq * 4, pw);
+          sqv = (og.x * og.x + og.y * og.y) + (og.z * og.z + og.w * og.w);
+        }
+        sqv = wave_sum_f32_to63(sqv);
+        if ((t & 63) == 63) st_sc1f(args.sq + (size_t)g * TW + (t >> 6), sqv);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (DP) {
@@ -694,19 +758,37 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
 #pragma unroll
       for (int i = 0; i < NQC; ++i)
         if (i * SPL_NT < Qp) gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
-      float acc = 0.f;
-#pragma unroll
-      for (int i = 0; i < NQC; ++i)
-        if (i * SPL_NT < Qp && t + i * SPL_NT < Qp)
-          acc += (gq[i].x * gq[i].x + gq[i].y * gq[i].y) + (gq[i].z * gq[i].z + gq[i].w * gq[i].w);
-      subm.mark(2);   // thread 0's gradient quads landed
-      acc = wave_sum_f32_to63(acc);
-      float* s_nrm = hdr + 96;
-      if ((t & 63) == 63) s_nrm[t >> 6] = acc;
-      __syncthreads();
       float tot = 0.f;
+      if constexpr (OWN) {
+        // gq: the NEW weights; the norm from the G x TW pieces, in one fixed order everywhere
+        // (lane l: pieces 4 l .. 4 l + 3 of each 256-piece chunk, every chunk's load issued first)
+        const int l = t & 63, npc = G * TW;
+        const __amdgpu_buffer_rsrc_t rs_sq = upd_rsrc(args.sq);
+        float4 pc[8];
 #pragma unroll
-      for (int w = 0; w < TW; ++w) tot += s_nrm[w];
+        for (int c = 0; c < 8; ++c)
+          if (256 * c < npc) pc[c] = ld4_sc1_so(rs_sq, 16u * (unsigned)l, 1024u * (unsigned)c);
+        float v = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (256 * c < npc && 256 * c + 4 * l < npc) v += (pc[c].x + pc[c].y) + (pc[c].z + pc[c].w);
+        v = wave_sum_f32_to63(v);
+        tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+        subm.mark(2);   // thread 0's weight quads and the pieces landed
+      } else {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < NQC; ++i)
+          if (i * SPL_NT < Qp && t + i * SPL_NT < Qp)
+            acc += (gq[i].x * gq[i].x + gq[i].y * gq[i].y) + (gq[i].z * gq[i].z + gq[i].w * gq[i].w);
+        subm.mark(2);   // thread 0's gradient quads landed
+        acc = wave_sum_f32_to63(acc);
+        float* s_nrm = hdr + 96;
+        if ((t & 63) == 63) s_nrm[t >> 6] = acc;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < TW; ++w) tot += s_nrm[w];
+      }
       const float coef = args.max_norm / (sqrtf(tot) + 1e-6f);
       clipc = coef < 1.0f ? coef : 1.0f;
       if (args.profile && g == 0 && t == 0 && coef < 1.0f) tm[20] += 1ull;
@@ -716,7 +798,40 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       }
     }
     mark(5);   // norm + loss
-    {
+    if constexpr (OWN) {
+      if (clipc < 1.0f) {
+        // clip_grad_norm_ scaled this step (rare): the owners redo their quads with the true
+        // coefficient from the kept gradient / moments and the LDS weights (not yet replaced),
+        // publish them in red_c, and one more hand-off (counter C) precedes the weight load
+        if (oq >= 0) {
+          float4 pw = *reinterpret_cast<const float4*>(W + 4 * oq);
+          onm = mreg[0];
+          onv = vreg[0];
+          adamw_quad(og, onm, onv, pw, clipc);
+          st4_sc1(upd_rsrc(args.red + (size_t)Qtot * 4), (size_t)oq * 4, pw);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        ++nclip;
+        if (t < 64) {
+          if (t == 0) upd_arrive(args.ctr, UPD_CTR_C, g);
+          const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_C, (unsigned)G * nclip);
+          if (t == 0) *s_abort = ok ? 0 : 1;
+        }
+        __syncthreads();
+        if (*s_abort) return;
+        const __amdgpu_buffer_rsrc_t rs_redc = upd_rsrc(args.red + (size_t)Qtot * 4);
+#pragma unroll
+        for (int i = 0; i < NQC; ++i)
+          if (i * SPL_NT < Qp) gq[i] = ld4_sc1_so(rs_redc, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
+      }
+      mreg[0] = onm;   // commit the owner's moments
+      vreg[0] = onv;
+#pragma unroll
+      for (int i = 0; i < NQC; ++i)
+        if (i * SPL_NT < Qp && t + i * SPL_NT < Qp)
+          *reinterpret_cast<float4*>(W + 4 * (t + i * SPL_NT)) = gq[i];
+    } else {
       const float step_size = s_adam[0];
       const float inv_bc2_sqrt = s_adam[1];
       const float decay = (float)(1.0 - (double)args.lr * (double)args.wd);
@@ -777,16 +892,26 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       }
     }
     __syncthreads();
-    mark(6);   // AdamW
+    mark(6);   // AdamW (OWN: the new weights into LDS)
   }
-  // ---- write back: role 0's first workgroup the trunk + head 0, role 1's the critic head ------
+  // ---- write back: role 0's first workgroup the trunk + head 0, role 1's the critic head (OWN:
+  //      every owner its slice quad) ------------------------------------------------------------
+  if constexpr (OWN) {
+    if (oq >= 0) {
+      *reinterpret_cast<float4*>(args.params + 4 * oq) = *reinterpret_cast<const float4*>(W + 4 * oq);
+      *reinterpret_cast<float4*>(args.exp_avg + 4 * oq) = mreg[0];
+      *reinterpret_cast<float4*>(args.exp_avg_sq + 4 * oq) = vreg[0];
+    }
+  }
   if (gt == 0) {
-    for (int i = 0; i < NQC; ++i) {
-      const int q = slotq(i);
-      if (q >= 0 && (role == 0 ? q < QH : q >= QH)) {
-        *reinterpret_cast<float4*>(args.params + 4 * q) = *reinterpret_cast<const float4*>(W + 4 * q);
-        *reinterpret_cast<float4*>(args.exp_avg + 4 * q) = mreg[i];
-        *reinterpret_cast<float4*>(args.exp_avg_sq + 4 * q) = vreg[i];
+    if constexpr (!OWN) {
+      for (int i = 0; i < NQC; ++i) {
+        const int q = slotq(i);
+        if (q >= 0 && (role == 0 ? q < QH : q >= QH)) {
+          *reinterpret_cast<float4*>(args.params + 4 * q) = *reinterpret_cast<const float4*>(W + 4 * q);
+          *reinterpret_cast<float4*>(args.exp_avg + 4 * q) = mreg[i];
+          *reinterpret_cast<float4*>(args.exp_avg_sq + 4 * q) = vreg[i];
+        }
       }
     }
     if (g == 0 && t == 0) {
@@ -801,8 +926,8 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   }
 }
 
-template <int NQC, int KA, int KDIM, bool DP = false, int TW = 4>
+template <int NQC, int KA, int KDIM, bool DP = false, int TW = 4, bool OWN = false>
 __global__ __launch_bounds__(64 * TW, 1) void ppo_update_split_kernel(UpdArgs args) {
   constexpr UpdNet N = upd_make(KDIM, KA, 1);
-  ppo_split_body<NQC, KA, DP, TW>(N, args);
+  ppo_split_body<NQC, KA, DP, TW, OWN>(N, args);
 }

@@ -238,7 +238,8 @@ __device__ inline unsigned ld_sc1u(const unsigned* p) {
 constexpr int UPD_SHARDS = 8;
 constexpr int UPD_CTR_A = 32;                              // first shard word of counter A
 constexpr int UPD_CTR_B = UPD_CTR_A + 32 * UPD_SHARDS;     // ... of counter B
-constexpr int UPD_CTR_WORDS = UPD_CTR_B + 32 * UPD_SHARDS;
+constexpr int UPD_CTR_C = UPD_CTR_B + 32 * UPD_SHARDS;     // ... of counter C (split form, OWN)
+constexpr int UPD_CTR_WORDS = UPD_CTR_C + 32 * UPD_SHARDS;
 __device__ inline void upd_arrive(unsigned* ctr, int base, int g) {
   __hip_atomic_fetch_add(upd_g(ctr + base + 32 * (g & (UPD_SHARDS - 1))), 1u, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
@@ -2461,6 +2462,24 @@ int upd_split_waves() {
   const char* e = getenv("PRL_UPD_SPL_WAVES");
   return (e && e[0] == '8') ? 8 : 4;
 }
+// The split form's slice-owner variant (prl_ppo_split.h, OWN): one rank, PRL_UPD_SPL_OWN != 0
+// (default on), and every slice narrow (2 nq <= NT: one owned quad per thread; mb >= 256 at the
+// CartPole shape), with the slices cut as spl_slice_start cuts them.
+int g_last_own = 0;
+bool upd_split_own(const UpdNet& n, int G, int NT) {
+  const char* e = getenv("PRL_UPD_SPL_OWN");
+  if (e && e[0] == '0') return false;
+  const int Qp = n.Lp / 4, QT = n.w1[0].lds / 4;
+  const int64_t U = (int64_t)Qp + QT + 2;
+  auto start = [&](int g) {
+    const int64_t u = U * g / G;
+    const int64_t q = u <= 2 * (int64_t)QT ? (u + 1) / 2 : u - QT;
+    return (int)(q < Qp + 1 ? q : Qp + 1);
+  };
+  for (int g = 0; g < G; ++g)
+    if (2 * (start(g + 1) - start(g)) > NT) return false;
+  return true;
+}
 bool upd_split_host(const UpdNet& n, int Gt, int R, bool tp) {
   if (tp || !g_split || upd_force_generic() || !upd_is_cartpole(n) || R != UPD_RT) return false;
   if (cdiv(n.Lp / 4, 64 * upd_split_waves()) > (upd_split_waves() == 8 ? SPL_NQC8 : SPL_NQC)) return false;
@@ -2514,7 +2533,7 @@ struct UpdWs {
 };
 
 // workspace: ctr[UPD_CTR_WORDS] (words 0-3 and the shards zeroed per launch, word 4 sticky) |
-// prof[32] + arrival stamps[2][256] | sq[NW G] | red[Qtot*4] | part[G][Qtot*4] | img[3][Qtot*4] |
+// prof[32] + arrival stamps[2][256] | sq[NW G] | red[2][Qtot*4] | part[G][Qtot*4] | img[3][Qtot*4] |
 // mv[4][Qtot*4] | part2[G][(QT+1)*4] | slack
 // (phase C's sweeps read up to one thread block of quads past an image: the slack keeps the
 // last one inside the allocation)
@@ -2522,7 +2541,7 @@ size_t upd_ws_carve(const UpdNet& n, int G, char* base, UpdWs* ws) {
   const size_t Qtot = (size_t)n.Lp / 4 + 1;
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-  const size_t o_ctr = take(4 * UPD_CTR_WORDS), o_prof = take(256 + 2 * 256 * 8), o_sq = take(2048 * 4), o_red = take(Qtot * 16),
+  const size_t o_ctr = take(4 * UPD_CTR_WORDS), o_prof = take(256 + 2 * 256 * 8), o_sq = take(2048 * 4), o_red = take(2 * Qtot * 16),
                o_part = take((size_t)G * Qtot * 16), o_img = take((size_t)3 * Qtot * 16),
                o_mv = take((size_t)4 * Qtot * 16),
                o_part2 = take((size_t)G * ((size_t)n.w1[0].lds / 4 + 1) * 16);
@@ -2689,12 +2708,16 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   }
   const bool split = upd_split_host(args.net, Gt, args.R, tp);
   if (!split) args.dp_push = 0;   // the push form is the head-split kernel's (ranks decide alike)
+  g_last_own = 0;
   if (split) {
     const int tw = upd_split_waves();
+    const bool own = !dp && tw == 4 && upd_split_own(args.net, 2 * Gt, 64 * tw);
     const void* k = tw == 8 ? (dp ? reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC8, 2, 4, true, 8>)
                                   : reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC8, 2, 4, false, 8>))
                             : (dp ? reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, true, 4>)
-                                  : reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, false, 4>));
+                                  : own ? reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, false, 4, true>)
+                                        : reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, false, 4>));
+    g_last_own = own ? 1 : 0;
     plan = UpdPlan{k, tw, 1};
   }
   // replicated tiles: the latency form on one GPU only; the split form: two roles per tile group
@@ -2712,7 +2735,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   g_last_plan[4] = (!upd_force_generic() && (upd_is_cartpole(args.net) ||
                                              (!args.net.discrete && args.net.A == 1 && args.net.D == 3))) ? 1 : 0;
   g_last_plan[5] = G / Gt;
-  g_last_plan[6] = split ? 1 : 0;
+  g_last_plan[6] = split ? (g_last_own ? 2 : 1) : 0;
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr + UPD_CTR_A, 0, 4 * (UPD_CTR_WORDS - UPD_CTR_A), st));

@@ -777,13 +777,14 @@ def ppo_update_last_plan() -> dict:
     "latency"), waves per workgroup, workgroups, 16-row tiles per workgroup and step, whether
     the kernel was a compile-time-layout specialisation, and the workgroups per tile group (the
     latency form's replicated tiles; the split form: its two head roles), and whether the
-    head-split latency form ran (csrc/prl_ppo_split.h)."""
+    head-split latency form ran (csrc/prl_ppo_split.h) and whether in its slice-owner variant
+    ("owner": AdamW by the slice owners, PRL_UPD_SPL_OWN)."""
     out = (ctypes.c_int32 * 7)()
     lib().prl_ppo_update_last_plan(out)
     tp, nw, G, tiles, spec, repl, split = list(out)
     return {"form": {1: "throughput", 0: "latency"}.get(tp), "waves": nw, "grid": G,
             "tiles": tiles, "specialised": bool(spec == 1), "replicas": repl,
-            "split": bool(split == 1)}
+            "split": bool(split >= 1), "owner": bool(split == 2)}
 
 
 XBUF_KINDS = {"auto": 0, "uncached": 1, "fine": 2}

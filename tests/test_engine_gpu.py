@@ -781,3 +781,60 @@ def test_split_form_matches_8wave_form(mb, N):
     assert torch.equal(outs[0][3], outs[1][3])
     assert abs(float(outs[0][4]) - float(outs[1][4])) <= 1e-4 * max(1.0, abs(float(outs[0][4])))
 
+
+
+@pytest.mark.parametrize("adv_scale", [1e-3, 1e3])
+def test_split_owner_form_matches_workgroup_adamw(monkeypatch, adv_scale):
+    """The split form's slice-owner variant (prl_ppo_split.h OWN, the default at mb 512: each
+    slice owner runs AdamW on its quads and publishes the new weights; the clip norm from
+    per-wave pieces) against its workgroup-AdamW variant (PRL_UPD_SPL_OWN=0) from the same
+    state on the same inputs.  adv x 1e-3: no step clips, so the same AdamW on the same gradient
+    values gives the same bits (weights, both moments, step count, loss).  adv x 1e3: EVERY step
+    clips (engine profile: clipped_steps_frac 1), so every step takes the owner variant's
+    redo + counter-C hand-off; the norm is summed in another order than the workgroup
+    variant's, so the two agree to float32 rounding of the clip coefficient (weights 3e-5)."""
+    import prl_native
+    from PPO import PPO
+    N, mb = 512 * 5 + 9, 512
+    data = _data(N, 4, False, seed=61)
+    torch.manual_seed(0)
+    p = PPO(False, 4, 2, k_epochs=2, batch_size=64, mini_batch_size=mb)
+    p.show_progress = False
+    eng = p._fused_engine()
+    init = [eng.flat.clone(), eng.m.clone(), eng.v.clone(), eng.step.clone()]
+    p.memory.push_device(*data)
+    p.learn()
+    torch.cuda.synchronize()
+    S, A, old, adv, ret = [x.clone() for x in p._last_update_inputs]
+    adv = adv * adv_scale
+    if adv_scale < 1:
+        # returns = the initial policy's own values (the policy's parameters are views of the
+        # engine's flat buffer): a near-zero value gradient, so no step clips
+        eng.flat.copy_(init[0])
+        _, V0 = eng.evaluate(p.policy, S, A)
+        ret = V0.clone()
+    outs = {}
+    monkeypatch.setenv("PRL_UPD_PROFILE", "1")
+    for own in ("1", "0"):
+        monkeypatch.setenv("PRL_UPD_SPL_OWN", own)
+        for dst, src in zip((eng.flat, eng.m, eng.v, eng.step), init):
+            dst.copy_(src)
+        eng.ws.fill_(0)
+        loss = eng.run(S, A, old, adv, ret, 3)
+        torch.cuda.synchronize()
+        plan = prl_native.ppo_update_last_plan()
+        assert plan["split"] and plan["owner"] == (own == "1"), plan
+        frac = eng.profile()["clipped_steps_frac"]
+        assert frac == (1.0 if adv_scale > 1 else 0.0), frac
+        outs[own] = [t.cpu().clone() for t in (eng.flat, eng.m, eng.v, eng.step, loss)]
+    assert not torch.equal(outs["1"][0], init[0].cpu())
+    if adv_scale < 1:
+        for a, b in zip(outs["1"], outs["0"]):
+            assert torch.equal(a, b)
+    else:
+        worst = float((outs["1"][0] - outs["0"][0]).abs().max())
+        assert worst <= ATOL, worst
+        for k in (1, 2):
+            a, b = outs["1"][k].double(), outs["0"][k].double()
+            assert float((a - b).abs().max()) <= 1e-3 * float(a.abs().max()) + 1e-12, k
+        assert torch.equal(outs["1"][3], outs["0"][3])
