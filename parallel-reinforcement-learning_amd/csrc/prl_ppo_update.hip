@@ -2462,13 +2462,16 @@ int upd_split_waves() {
   const char* e = getenv("PRL_UPD_SPL_WAVES");
   return (e && e[0] == '8') ? 8 : 4;
 }
-// The split form's slice-owner variant (prl_ppo_split.h, OWN): one rank, PRL_UPD_SPL_OWN != 0
-// (default on), and every slice narrow (2 nq <= NT: one owned quad per thread; mb >= 256 at the
-// CartPole shape), with the slices cut as spl_slice_start cuts them.
+// The split form's slice-owner variant (prl_ppo_split.h, OWN): one rank, PRL_UPD_SPL_OWN=1
+// (opt-in: it wins only where clip_grad_norm_ rarely scales a step — 11.84 vs 12.58 us per step
+// on the fixed synthetic 2^20 memory — while C2's training clips every step, where each clipped
+// step's redo + extra hand-off makes it 14.1 vs 12.8 us; tools/clip_stats.py), and every slice
+// narrow (2 nq <= NT: one owned quad per thread; mb >= 256 at the CartPole shape), with the
+// slices cut as spl_slice_start cuts them.
 int g_last_own = 0;
 bool upd_split_own(const UpdNet& n, int G, int NT) {
   const char* e = getenv("PRL_UPD_SPL_OWN");
-  if (e && e[0] == '0') return false;
+  if (!(e && e[0] == '1')) return false;
   const int Qp = n.Lp / 4, QT = n.w1[0].lds / 4;
   const int64_t U = (int64_t)Qp + QT + 2;
   auto start = [&](int g) {

@@ -785,7 +785,7 @@ def test_split_form_matches_8wave_form(mb, N):
 
 @pytest.mark.parametrize("adv_scale", [1e-3, 1e3])
 def test_split_owner_form_matches_workgroup_adamw(monkeypatch, adv_scale):
-    """The split form's slice-owner variant (prl_ppo_split.h OWN, the default at mb 512: each
+    """The split form's slice-owner variant (prl_ppo_split.h OWN, PRL_UPD_SPL_OWN=1: each
     slice owner runs AdamW on its quads and publishes the new weights; the clip norm from
     per-wave pieces) against its workgroup-AdamW variant (PRL_UPD_SPL_OWN=0) from the same
     state on the same inputs.  adv x 1e-3: no step clips, so the same AdamW on the same gradient
