@@ -183,6 +183,22 @@ def pmc_traffic(n):
     return round(per * n), src
 
 
+def update_pmc_traffic(kern, steps):
+    """HBM bytes per launch of the split update kernel from the committed PMC summary
+    (profiles/*update_pmc.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over
+    tools/engine_profile.py 262144 512, FETCH_SIZE doubled for gfx950), scaled per optimizer step
+    (5,632 steps per profiled launch: k_epochs 11 x 512 minibatches).  None for other kernels."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*update_pmc.json")))
+    if not files or kern != "ppo_update_split_kernel":
+        return None, None
+    recs = json.load(open(files[-1]))
+    rec = recs[0] if isinstance(recs, list) else recs
+    per_step = (rec["read_bytes_corrected"] + rec["write_bytes"]) / 5632.0
+    return round(per_step * steps), (os.path.relpath(files[-1], ROOT) +
+                                     f" ({per_step / 1e6:.2f} MB per optimizer step, scaled)")
+
+
 def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
     """K timed AsyncPPO iterations of one configuration (after `warmup` untimed ones) and the
     roofline re-timings of its kernels.  Returns the measured record (whole-job numbers are
@@ -281,10 +297,11 @@ def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
                                  "step gradient kernel -> RCCL all-reduce -> AdamW kernel; "
                                  "time = events around the loop",
                 }.get(kern, "stepped engine: one minibatch's gradient on this rank per launch")
+        upd_traffic, upd_src = update_pmc_traffic(kern, steps_per_launch)
         roofline = {"kernel": f"{kern} ({what})",
                     "bound": "mfma", "achieved": round(achieved, 3), "peak": F32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / F32_PEAK_TFLOPS, 5),
-                    "traffic": None,
+                    "traffic": upd_traffic, "traffic_source": upd_src,
                     "limiter": "latency: dependent optimizer steps (k_epochs x ceil(N/mb)), "
                                "each = forward+backward of mb rows + two grid-wide hand-offs",
                     "avg_launch_ms": round(avg_ms, 4), "launches": len(ms),
