@@ -389,9 +389,11 @@ int prl_colsum_f32(const float* x, int64_t rows, int32_t cols, float* out, float
  * defaults, capturable: the update uses step[0] + 1, and step[0] f32 on the device is advanced)
  * over FLAT f32 vectors of P entries in parameters() order: params, exp_avg, exp_avg_sq and grad
  * (left clipped, as torch leaves p.grad).  The norm is summed in float64 in a fixed order
- * (deterministic) and stored to total_norm[0] (f32, what clip_grad_norm_ returns).  Two launches
- * (update; clip of grad + step count), graph-capturable; the wide step's optimizer tail
- * (PPO/update.py).  16-B aligned buffers. */
+ * (deterministic) and stored to total_norm[0] (f32, what clip_grad_norm_ returns); total_norm[1]
+ * is a u32 arrival counter that must be zero before the first call (every call leaves it zero):
+ * the last workgroup to finish clips grad and advances the step.  One launch up to 262,144
+ * parameters (two above: update; clip of grad + step count), graph-capturable; the wide step's
+ * optimizer tail (PPO/update.py) and the RND predictor's AdamW.  16-B aligned buffers. */
 int prl_flat_adamw(float* params, float* exp_avg, float* exp_avg_sq, float* step, float* grad,
                    int64_t P, float lr, double beta1, double beta2, float eps, float weight_decay,
                    float max_norm, float* total_norm, void* stream);

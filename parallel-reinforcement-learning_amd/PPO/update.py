@@ -55,7 +55,8 @@ class FlatAdamState:
         self.m = torch.zeros(n, dtype=torch.float32, device=dev)
         self.v = torch.zeros(n, dtype=torch.float32, device=dev)
         self.step = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.total_norm = torch.zeros(1, dtype=torch.float32, device=dev)   # clip_grad_norm_'s value
+        # [0] clip_grad_norm_'s value, [1] prl_flat_adamw's arrival counter (kept at zero)
+        self.total_norm = torch.zeros(2, dtype=torch.float32, device=dev)
         self._bind()
 
     def _views(self, buf):
@@ -117,14 +118,21 @@ class FlatAdamState:
         opt = self.ppo.optimizer
         group = opt.param_groups[0]
         on_device = bool(group.get("capturable") or group.get("fused"))
+        host_step = None   # torch's default AdamW keeps host step counts: ONE device read for all
         for p, mv, vv in zip(self.params, self._views(self.m), self._views(self.v)):
             st = opt.state[p]
             st["exp_avg"], st["exp_avg_sq"] = mv, vv
-            if "step" in st and torch.is_tensor(st["step"]):
+            if "step" in st and torch.is_tensor(st["step"]) and st["step"].is_cuda:
                 st["step"].copy_(self.step.reshape(st["step"].shape))
+            elif on_device:
+                st["step"] = self.step.reshape(()).clone()
             else:
-                st["step"] = (self.step.reshape(()).clone() if on_device
-                              else torch.tensor(float(self.step.item())))
+                if host_step is None:
+                    host_step = float(self.step.item())
+                if "step" in st and torch.is_tensor(st["step"]):
+                    st["step"].fill_(host_step)
+                else:
+                    st["step"] = torch.tensor(host_step)
 
 
 def flat_adam_ok(optimizer) -> bool:

@@ -247,16 +247,19 @@ extern "C" int prl_colsum_f32(const float* x, int64_t rows, int32_t cols, float*
 // (torch defaults: decoupled weight decay, lerp for exp_avg, addcmul for exp_avg_sq, bias
 // corrections from the incremented step count).  Parameters, gradient and both moments are flat
 // vectors in parameters() order (the policy's Parameters and the optimizer's state are views of
-// them, PPO/update.py FlatAdamState).  Two launches: flat_adamw_kernel (below) forms the squared
-// norm in float64 in a fixed order in EVERY workgroup, the clip coefficient max_norm / (norm +
-// 1e-6) clamped to 1, and updates its own 1,024 quads of params / exp_avg / exp_avg_sq with the
-// persistent engine's arithmetic (prl_ppo_update.hip phase C); workgroup 0 stores the norm.
-// flat_adam_clip_kernel then leaves the gradient clipped (as torch leaves p.grad) and advances
-// the step count — the gradient cannot be rewritten in the first launch, whose workgroups are
-// still reading all of it for their norms.  One launch of torch's foreach-norm / stack / norm /
-// coefficient / foreach-mul / fused-AdamW chain each.
+// them, PPO/update.py FlatAdamState).  flat_adamw_kernel (below) forms the squared norm in float64
+// in a fixed order in EVERY workgroup, the clip coefficient max_norm / (norm + 1e-6) clamped to 1,
+// and updates its own 1,024 quads of params / exp_avg / exp_avg_sq with the persistent engine's
+// arithmetic (prl_ppo_update.hip phase C); workgroup 0 stores the norm.  The gradient must then be
+// left clipped (as torch leaves p.grad) and the step count advanced, which no workgroup may do
+// while another is still reading the gradient for its norm or the step for its bias corrections:
+// the LAST workgroup to finish (an arrival counter in the norm workspace, left at zero again) does
+// both, so one launch replaces torch's foreach-norm / stack / norm / coefficient / foreach-mul /
+// fused-AdamW chain.  Large P (> FA_FUSE_MAX_BLOCKS workgroups, where one workgroup's pass over
+// the whole gradient would be long) keeps a second launch for it (flat_adam_clip_kernel).
 constexpr int FA_THREADS = 1024;
 constexpr int FA_BATCH = 8;   // gradient quads per thread in flight during the norm pass
+constexpr int FA_FUSE_MAX_BLOCKS = 64;   // up to 262,144 parameters: clip + step in the last workgroup
 
 // Every workgroup forms the whole squared norm itself, in the same fixed order (thread t: quads
 // t, t + 1024, ... ascending, float64 fma; the 16 waves' sums in wave order), so all of them get
@@ -264,11 +267,13 @@ constexpr int FA_BATCH = 8;   // gradient quads per thread in flight during the 
 // last one the P % 4 tail).  (Until round 4 one 1024-thread workgroup did the norm AND the whole
 // update: ~19 us per C5 step, most of it one CU streaming ~600 KB in and out.)
 __global__ __launch_bounds__(FA_THREADS) void flat_adamw_kernel(
-    float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, const float* __restrict__ step,
-    const float* __restrict__ grad, int64_t P, float lr, double beta1, double beta2, float eps,
-    float wd, float max_norm, float* __restrict__ total_norm) {
+    float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, const float* step,
+    const float* grad, int64_t P, float lr, double beta1, double beta2, float eps,
+    float wd, float max_norm, float* __restrict__ total_norm, float* grad_out,
+    unsigned* arrive, float* step_out) {   // grad_out / step_out: grad / step (written last)
   __shared__ double s_part[FA_THREADS / 64];
   __shared__ float s_c[3];
+  __shared__ unsigned s_last;
   const int t = threadIdx.x;
   const int64_t Q = P / 4;
   const float4* g4p = reinterpret_cast<const float4*>(grad);
@@ -349,6 +354,31 @@ __global__ __launch_bounds__(FA_THREADS) void flat_adamw_kernel(
       v[k] = vw;
     }
   }
+  if (arrive == nullptr) return;   // the clip launch follows
+  // every read of grad and step in this workgroup is complete here (all consumed above)
+  __syncthreads();
+  if (t == 0) {
+    const unsigned old = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (old + 1 == gridDim.x) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (clipc != 1.0f) {   // x * 1 is x: an unclipped gradient is left as it is
+    float4* go4 = reinterpret_cast<float4*>(grad_out);
+    for (int64_t q = t; q < Q; q += FA_THREADS) {
+      float4 x = go4[q];
+      x.x *= clipc;
+      x.y *= clipc;
+      x.z *= clipc;
+      x.w *= clipc;
+      go4[q] = x;
+    }
+    for (int64_t k = 4 * Q + t; k < P; k += FA_THREADS) grad_out[k] *= clipc;
+  }
+  if (t == 0) {
+    step_out[0] = step0 + 1.0f;
+    __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 // grad *= the clip coefficient (from the stored norm, formed as flat_adamw_kernel formed it:
 // the same bits); thread 0 of workgroup 0 advances the step count
@@ -381,10 +411,14 @@ extern "C" int prl_flat_adamw(float* params, float* exp_avg, float* exp_avg_sq, 
   PRL_REQUIRE(aligned16(params) && aligned16(exp_avg) && aligned16(exp_avg_sq) && aligned16(grad),
               "prl_flat_adamw: buffers must be 16-B aligned");
   const unsigned nblk = (unsigned)std::max<int64_t>(1, cdiv(P / 4, FA_THREADS));
+  const bool fuse = nblk <= (unsigned)FA_FUSE_MAX_BLOCKS;
+  // total_norm[1]: the arrival counter (zero before the first call; every call leaves it zero)
+  unsigned* arrive = fuse ? reinterpret_cast<unsigned*>(total_norm + 1) : nullptr;
   hipLaunchKernelGGL(flat_adamw_kernel, dim3(nblk), dim3(FA_THREADS), 0, as_stream(stream), params,
                      exp_avg, exp_avg_sq, step, grad, P, lr, beta1, beta2, eps, weight_decay,
-                     max_norm, total_norm);
+                     max_norm, total_norm, grad, arrive, step);
   PRL_LAUNCH_CHECK("flat_adamw");
+  if (fuse) return PRL_OK;
   hipLaunchKernelGGL(flat_adam_clip_kernel, dim3((unsigned)std::max<int64_t>(1, cdiv(P / 4, 256))),
                      dim3(256), 0, as_stream(stream), grad, P, max_norm, total_norm, step);
   PRL_LAUNCH_CHECK("flat_adam_clip");

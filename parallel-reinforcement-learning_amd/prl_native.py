@@ -754,22 +754,25 @@ def ppo_update_set_split(mode: int) -> int:
 
 def flat_adamw(params, exp_avg, exp_avg_sq, step, grad, lr, beta1, beta2, eps, weight_decay,
                max_norm, total_norm=None):
-    """clip_grad_norm_(max_norm) + AdamW.step() over flat f32 vectors (two launches).  Returns
-    total_norm: a one-entry f32 device tensor holding the gradient's norm (clip_grad_norm_'s
-    return value; a new one unless passed)."""
+    """clip_grad_norm_(max_norm) + AdamW.step() over flat f32 vectors (one launch up to 262,144
+    parameters, two above).  total_norm: a two-entry f32 device workspace, zeroed before its
+    first use ([0] the gradient's norm, clip_grad_norm_'s return value; [1] the launch's arrival
+    counter, left at zero by every call; a new one unless passed).  Returns total_norm[:1]."""
     P = int(params.numel())
     for t, n in ((exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq"), (grad, "grad")):
         if t.numel() != P:
             raise ValueError(f"{n} has {t.numel()} entries, params {P}")
     if total_norm is None:
-        total_norm = torch.empty(1, dtype=torch.float32, device=params.device)
+        total_norm = torch.zeros(2, dtype=torch.float32, device=params.device)
+    if total_norm.numel() < 2:
+        raise ValueError("total_norm must hold 2 entries (the norm and an arrival counter)")
     _check(lib().prl_flat_adamw(
         _dev(params, torch.float32, "params"), _dev(exp_avg, torch.float32, "exp_avg"),
         _dev(exp_avg_sq, torch.float32, "exp_avg_sq"), _dev(step, torch.float32, "step"),
         _dev(grad, torch.float32, "grad"), P, float(lr), float(beta1), float(beta2), float(eps),
         float(weight_decay), float(max_norm), _dev(total_norm, torch.float32, "total_norm"),
         _stream()), "prl_flat_adamw")
-    return total_norm
+    return total_norm[:1]
 
 
 def ppo_update_last_plan() -> dict:

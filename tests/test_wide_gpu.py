@@ -384,8 +384,9 @@ def test_wide_graphed_rollout_equals_eager_rollout(monkeypatch):
 
 @pytest.mark.parametrize("scale", [1e-3, 1e2])
 def test_flat_adamw_matches_torch_clip_and_adamw(scale):
-    """prl_flat_adamw (the wide step's optimizer tail: clip_grad_norm_(2.0) + AdamW.step() in two
-    launches over flat buffers, PPO.py:248-250; ~37 K parameters = 10 workgroups of the first) against torch's own clip_grad_norm_ + AdamW
+    """prl_flat_adamw (the wide step's optimizer tail: clip_grad_norm_(2.0) + AdamW.step() in one
+    launch over flat buffers, PPO.py:248-250; ~37 K parameters = 10 workgroups, the last of which
+    clips the gradient and advances the step) against torch's own clip_grad_norm_ + AdamW
     (the reference's defaults: bias corrections from Python doubles) on C5's parameter shapes
     over four steps.  scale 1e-3: norm < 2, no clipping;
     1e2: clipping every step.  The two differ only in float32 rounding (norm summed in float64
@@ -426,6 +427,42 @@ def test_flat_adamw_matches_torch_clip_and_adamw(scale):
     assert float((m - wm).abs().max()) <= 1e-5 * float(wm.abs().max())
     assert float((v - wv).abs().max()) <= 1e-5 * float(wv.abs().max())
     assert float(step.item()) == 4.0
+
+
+@pytest.mark.parametrize("P", [262_144, 300_003])
+def test_flat_adamw_one_and_two_launch_forms(P):
+    """prl_flat_adamw at the fused form's largest size (64 workgroups: the last one clips and
+    advances the step) and above it (the separate clip launch; P % 4 = 3 exercises the tail)
+    against torch's clip_grad_norm_(2.0) + AdamW on one flat Parameter over three clipping steps:
+    the same bounds as test_flat_adamw_matches_torch_clip_and_adamw.  The arrival counter
+    (total_norm[1]) is back at zero after every call."""
+    import prl_native
+    g = torch.Generator(device="cuda").manual_seed(9)
+    p0 = (torch.rand(P, device="cuda", generator=g) - 0.5) * 0.6
+    ref = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.AdamW([ref], lr=1e-3)
+    flat = p0.clone()
+    m, v = torch.zeros_like(flat), torch.zeros_like(flat)
+    step = torch.zeros(1, device="cuda")
+    ws = torch.zeros(2, device="cuda")
+    for _ in range(3):
+        grad = torch.randn(P, device="cuda", generator=g) * 0.1
+        ref.grad = grad.clone()
+        tn = torch.nn.utils.clip_grad_norm_([ref], 2.0)
+        opt.step()
+        gbuf = grad.clone()
+        got_n = prl_native.flat_adamw(flat, m, v, step, gbuf, 1e-3, 0.9, 0.999, 1e-8, 1e-2, 2.0, ws)
+        torch.cuda.synchronize()
+        assert float(tn) > 2.0
+        assert float((gbuf - ref.grad).abs().max()) <= 1e-6 * float(ref.grad.abs().max())
+        assert abs(float(got_n) - float(tn)) <= 1e-6 * float(tn)
+        assert int(ws[1:].view(torch.int32).item()) == 0
+    ulp = float(torch.finfo(torch.float32).eps) * float(ref.detach().abs().max())
+    assert float((flat - ref.detach()).abs().max()) <= 16 * ulp
+    wm, wv = opt.state[ref]["exp_avg"], opt.state[ref]["exp_avg_sq"]
+    assert float((m - wm).abs().max()) <= 1e-5 * float(wm.abs().max())
+    assert float((v - wv).abs().max()) <= 1e-5 * float(wv.abs().max())
+    assert float(step.item()) == 3.0
 
 
 def test_wide_learn_native_adam_equals_torch_adam(monkeypatch):
