@@ -465,6 +465,48 @@ def test_flat_adamw_one_and_two_launch_forms(P):
     assert float(step.item()) == 3.0
 
 
+def test_flat_adamw_graph_replay_equals_eager():
+    """The one-launch flat AdamW captured in a HIP graph (the data-parallel wide step replays it
+    per minibatch): three replays give the same bits as three eager calls — parameters, moments,
+    the clipped gradient, the norm and the step — and the arrival counter is zero after each."""
+    import prl_native
+    P = 37_347   # C5's policy: 10 workgroups, a P % 4 tail of 3
+    g = torch.Generator(device="cuda").manual_seed(13)
+    p0 = (torch.rand(P, device="cuda", generator=g) - 0.5) * 0.6
+    grads = [torch.randn(P, device="cuda", generator=g) * 0.5 for _ in range(3)]
+
+    def fresh():
+        return [p0.clone(), torch.zeros(P, device="cuda"), torch.zeros(P, device="cuda"),
+                torch.zeros(1, device="cuda"), torch.zeros(2, device="cuda")]
+
+    e = fresh()
+    e_g = []
+    for gr in grads:
+        gb = gr.clone()
+        prl_native.flat_adamw(e[0], e[1], e[2], e[3], gb, 1e-3, 0.9, 0.999, 1e-8, 1e-2, 2.0, e[4])
+        e_g.append(gb)
+    c = fresh()
+    gbuf = torch.empty(P, device="cuda")
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            prl_native.flat_adamw(c[0], c[1], c[2], c[3], gbuf, 1e-3, 0.9, 0.999, 1e-8, 1e-2, 2.0,
+                                  c[4])
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    for i, gr in enumerate(grads):
+        gbuf.copy_(gr)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(gbuf, e_g[i])
+        assert int(c[4][1:].view(torch.int32).item()) == 0
+    for a, b in zip(c, e):
+        assert torch.equal(a[:1] if a.numel() == 2 else a, b[:1] if b.numel() == 2 else b)
+    assert float(c[3].item()) == 3.0
+
+
 def test_wide_learn_native_adam_equals_torch_adam(monkeypatch):
     """learn() on C5's net through the wide step with the native optimizer tail (default) and
     with torch's clip_grad_norm_ + fused AdamW (PRL_WIDE_ADAM=0): same data, two epochs with a
