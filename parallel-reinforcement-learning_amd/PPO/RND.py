@@ -123,7 +123,7 @@ class RND(nn.Module):
     # ------------------------------------------------------------------ graphed update (one GPU)
     def _flat_state(self):
         """The predictor's parameters, gradients and AdamW state as flat vectors (views, as the
-        policy's: update.FlatAdamState), so one native AdamW launch pair steps them."""
+        policy's: update.FlatAdamState), so one native AdamW launch steps them."""
         from .update import FlatAdamState
         params = list(self.pred_net.parameters())
         fa = getattr(self, "_fa", None)
@@ -203,7 +203,7 @@ class RND(nn.Module):
     def _update_native(self, values, all_reduce=None, counts=None) -> None:
         """update_pred with the fused gradient kernel: per minibatch ONE prl_rnd_pred_grad (both
         forwards, MSE, the predictor's backward, written into the flat gradient the parameters'
-        .grad view) and the native AdamW pair (max_norm = inf), plus, on data-parallel ranks, one
+        .grad view) and the native flat AdamW launch (max_norm = inf), plus, on data-parallel ranks, one
         all-reduce of the flat gradient (each rank's rows scaled by 2 / (union rows D): the
         union's mean).  Same steps in the same order as the loops below."""
         fa = self._flat_state()
@@ -316,7 +316,7 @@ class RND(nn.Module):
         if all_reduce is not None and self._flat_dp_ok():
             # data-parallel ranks on the GPU: the gradient is ONE flat buffer (the parameters'
             # .grad are views of it), so each step is one all-reduce instead of one per parameter
-            # tensor, and AdamW is the native flat launch pair (max_norm = inf: no clipping)
+            # tensor, and AdamW is the native flat launch (max_norm = inf: no clipping)
             fa = self._flat_state()
             group = self.optimizer.param_groups[0]
             beta1, beta2 = group["betas"]
