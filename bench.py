@@ -183,6 +183,37 @@ def pmc_traffic(n):
     return round(per * n), src
 
 
+def wide_pmc_traffic():
+    """HBM bytes of one C5 wide step (tile kernel + dW0 launch + dW0's fold) from the committed
+    PMC summary (profiles/*c5_wide_pmc.json: tools/gpu_c5_wide_pmc.sh, rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled for gfx950; per-dispatch means over a C5
+    bench run, ragged last minibatches included).  The tile kernel's evaluate instance is not a
+    step's."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*c5_wide_pmc.json")))
+    if not files:
+        return None, None
+    tot, seen = 0.0, set()
+    for rec in json.load(open(files[-1]))["kernels"]:
+        k = rec["kernel"]
+        if "ppo_wide_grad_kernel" in k:
+            targs = [x.strip() for x in k[k.index("<") + 1:k.rindex(">")].split(",")]
+            if len(targs) < 3 or targs[2] != "false":   # <KSM, SPLIT, EVAL, ...>: skip EVAL
+                continue
+            name = "grad"
+        elif "ppo_wide_dw0_kernel" in k:
+            name = "dw0"
+        elif "ppo_wide_reduce_kernel" in k:
+            name = "reduce"
+        else:
+            continue
+        tot += rec["read_bytes_corrected"] + rec["write_bytes"]
+        seen.add(name)
+    if seen != {"grad", "dw0", "reduce"}:
+        return None, None
+    return round(tot), os.path.relpath(files[-1], ROOT) + " (per-dispatch means, summed)"
+
+
 def update_pmc_traffic(kern, steps):
     """HBM bytes per launch of the split update kernel from the committed PMC summary
     (profiles/*update_pmc.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over
@@ -328,11 +359,13 @@ def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
         fpr = 2 * (trunk + heads + outs) * 2 + 2 * (heads + outs)
         rows = min(gu.mb, int(gu.sources[0].shape[0]))
         ach = fpr * rows / (cold_med * 1e-3) / 1e12
+        wide_traffic, wide_src = wide_pmc_traffic()
         roofline = {"kernel": "prl_ppo_wide_grad: ppo_wide_grad_kernel + ppo_wide_dw0_kernel (dW0 "
                               "beside the partials' fold) + ppo_wide_reduce_kernel (dW0's fold): one "
                               "optimizer step's forward + loss + backward, wide nets",
                     "bound": "mfma", "achieved": round(ach, 3), "peak": F32_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / F32_PEAK_TFLOPS, 5), "traffic": None,
+                    "unit": "TFLOP/s", "frac": round(ach / F32_PEAK_TFLOPS, 5),
+                    "traffic": wide_traffic, "traffic_source": wide_src,
                     "limiter": "one wave per SIMD (256 + 256 registers, no spills) and the LDS "
                                "holding the heads: dependent MFMA chains per 16-row tile",
                     "avg_launch_us": round(cold_med * 1e3, 2),
