@@ -214,20 +214,30 @@ def wide_pmc_traffic():
     return round(tot), os.path.relpath(files[-1], ROOT) + " (per-dispatch means, summed)"
 
 
-def update_pmc_traffic(kern, steps):
-    """HBM bytes per launch of the split update kernel from the committed PMC summary
-    (profiles/*update_pmc.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over
-    tools/engine_profile.py 262144 512, FETCH_SIZE doubled for gfx950), scaled per optimizer step
-    (5,632 steps per profiled launch: k_epochs 11 x 512 minibatches).  None for other kernels."""
+def update_pmc_traffic(kern, steps, mb):
+    """HBM bytes per launch of the split update kernel from the newest committed PMC summary
+    (profiles/*update_pmc.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE
+    doubled for gfx950), scaled per optimizer step from the profiled launch's own step count.
+    The summary records the minibatch size, optimizer steps per dispatch and commit it was
+    profiled at ("meta"); round 5's file predates that (mb 512, 5,632 steps).  None for other
+    kernels or when the bench's minibatch differs from the profiled one: the traffic is a
+    committed measurement of that kernel at that shape, not of this run."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*update_pmc.json")))
     if not files or kern != "ppo_update_split_kernel":
         return None, None
     recs = json.load(open(files[-1]))
-    rec = recs[0] if isinstance(recs, list) else recs
-    per_step = (rec["read_bytes_corrected"] + rec["write_bytes"]) / 5632.0
+    meta = recs.get("meta", {}) if isinstance(recs, dict) else {}
+    kerns = recs.get("kernels", []) if isinstance(recs, dict) else recs
+    rec = [r for r in kerns if "ppo_update_split_kernel" in r["kernel"]][0]
+    p_mb, p_steps = meta.get("mb", 512), meta.get("optimizer_steps_per_dispatch", 5632)
+    if p_mb != mb:
+        return None, None
+    per_step = (rec["read_bytes_corrected"] + rec["write_bytes"]) / float(p_steps)
+    at = f", profiled at commit {meta['commit']}" if "commit" in meta else ""
     return round(per_step * steps), (os.path.relpath(files[-1], ROOT) +
-                                     f" ({per_step / 1e6:.2f} MB per optimizer step, scaled)")
+                                     f" ({per_step / 1e6:.2f} MB per optimizer step at mb {p_mb}"
+                                     f"{at}; scaled to this launch's steps)")
 
 
 def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
@@ -328,7 +338,7 @@ def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
                                  "step gradient kernel -> RCCL all-reduce -> AdamW kernel; "
                                  "time = events around the loop",
                 }.get(kern, "stepped engine: one minibatch's gradient on this rank per launch")
-        upd_traffic, upd_src = update_pmc_traffic(kern, steps_per_launch)
+        upd_traffic, upd_src = update_pmc_traffic(kern, steps_per_launch, cfg["mb"])
         roofline = {"kernel": f"{kern} ({what})",
                     "bound": "mfma", "achieved": round(achieved, 3), "peak": F32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved / F32_PEAK_TFLOPS, 5),
@@ -533,7 +543,9 @@ def main():
                     help="skip learn() on the fixed synthetic 2^20 memory (learn_fixed_2p20)")
     ap.add_argument("--no-subconfigs", action="store_true",
                     help="skip the short c2_mb65536 / c3 / c5 sub-records after the headline")
-    ap.add_argument("--sub-steps", type=int, default=2, help="timed steps of each sub-record")
+    ap.add_argument("--sub-steps", type=int, default=5, help="timed steps of each sub-record")
+    ap.add_argument("--sub-warmup", type=int, default=2,
+                    help="untimed steps of each sub-record (the first rollouts capture graphs)")
     ap.add_argument("--cpu-envs", type=int, default=8192,
                     help="num_envs of the CPU baseline's sample iteration (~20 s of host work)")
     ap.add_argument("--no-env-scale", action="store_true",
@@ -582,7 +594,7 @@ def main():
             torch.cuda.empty_cache()
             scfg = dict(CONFIGS[base])
             scfg.update(over)
-            r, _ = run_config(args, scfg, args.sub_steps, 1, 1, 0, env_scale=False)
+            r, _ = run_config(args, scfg, args.sub_steps, args.sub_warmup, 1, 0, env_scale=False)
             r.pop("elapsed_s")
             r.pop("total_n")
             r["workload"] = workload(base, scfg)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PRL_ABI_VERSION 1
+#define PRL_ABI_VERSION 2
 
 enum prl_status {
   PRL_OK = 0,
@@ -444,6 +444,10 @@ int prl_ppo_update_dp(float* img_params, float* img_m, float* img_v, int32_t D, 
  * fallback): each workgroup then orders its slice stores before its flag with a system-scope
  * release fence and its slice loads after the poll with a system-scope acquire fence (the
  * uncached form relies on write-through system-scope stores and cache-missing loads instead).
+ * fine_grained is a bit field: bit 0 the above; bit 1 the push form of the exchange (the
+ * head-split kernel's); bit 2 forces the 8-wave kernel (no head split) — the ranks' kernel
+ * choice must be the same everywhere, so the caller votes with prl_ppo_update_dp_split and sets
+ * bit 2 unless every rank would run the split form.
  * No reference counterpart (the reference is single-process). */
 int prl_ppo_update_dpx(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step,
                        int32_t D, int32_t A, int32_t discrete, const float* S,
@@ -479,6 +483,11 @@ int32_t prl_ppo_update_set_repl(int32_t replicas);
  * the 8-wave kernel.  Per process; returns the previous value.  No reference counterpart
  * (performance knob / tests). */
 int32_t prl_ppo_update_set_split(int32_t mode);
+/* 1 when a prl_ppo_update_dpx launch of this shape and mini_batch would run the head-split kernel
+ * in this process (the split mode above, the shape, and 2 x tile groups <= the CUs), else 0: the
+ * data-parallel caller's vote (every rank must launch the same kernel form).  No reference
+ * counterpart. */
+int32_t prl_ppo_update_dp_split(int32_t D, int32_t A, int32_t discrete, int32_t mini_batch);
 /* Test utility: fill every CU's LDS with `value` (LDS is not cleared between launches; a kernel
  * that reads LDS it did not write in its own launch sees the previous launch's contents).  No
  * reference counterpart. */
@@ -489,9 +498,11 @@ int prl_debug_fill_lds(float value, void* stream);
  * out[4] = 1 for a compile-time-layout (CartPole / Pendulum) kernel, 0 for the runtime layout;
  * out[5] = workgroups per tile group (the latency form's replicated tiles, PRL_UPD_REPL; out[2]
  * counts them all; the split form: its two head roles); out[6] = 1 for the head-split latency
- * form, 2 for its slice-owner variant (AdamW by the slice owners, PRL_UPD_SPL_OWN).  All -1 before the first launch.  No reference counterpart (tests assert which kernel
- * ran). */
-void prl_ppo_update_last_plan(int32_t out[7]);
+ * form, 2 for its slice-owner variant (AdamW by the slice owners, PRL_UPD_SPL_OWN); out[7] = the
+ * split form's phase-B helper workgroups (launched beside out[2]; PRL_UPD_SPL_HELP).  All -1
+ * before the first launch.  No reference counterpart (tests assert which kernel ran).
+ * (ABI 2: out has 8 entries; ABI 1 had 7.) */
+void prl_ppo_update_last_plan(int32_t out[8]);
 /* A zeroed slice buffer of its own (shareable by IPC handle).  *kind in: 0 = uncached, falling
  * back to fine-grained memory, 1 = uncached only, 2 = fine-grained only; out: 1 = uncached,
  * 2 = fine-grained (what the buffer is; prl_ppo_update_dpx's fine_grained follows it). */

@@ -300,8 +300,11 @@ class FusedUpdate:
         self._xbuf_own, self._xbufs, self._dp_rank, self._dp_seq = own, ptrs, rank, 0
         # every rank runs the same collectives whatever its local outcome: ONE gather of
         # (ok, checksum) per rank, then the same decision everywhere
+        votes = [None] * world
+        tdist.all_gather_object(votes, prl_native.ppo_update_dp_split(self.D, self.A, self.discrete,
+                                                                      self.mini_batch))
         res = [None] * world
-        tdist.all_gather_object(res, self._dp_selftest(world))
+        tdist.all_gather_object(res, self._dp_selftest(world, all(votes)))
         sums = [c for _, c in res]
         if not (all(ok for ok, _ in res) and len(set(sums)) == 1 and sums[0] == sums[0]):
             warnings.warn("data-parallel persistent engine failed its self-test; using the "
@@ -314,7 +317,7 @@ class FusedUpdate:
     def _dp_checksum(self, flat) -> float:
         return float(flat.double().sum().item()) + float((flat.double() ** 2).sum().item())
 
-    def _dp_selftest(self, world):
+    def _dp_selftest(self, world, split=True):
         """One small prl_ppo_update_dpx launch (2 minibatches per rank, k 1) on scratch copies
         of the state.  Local only (no collective): returns (ok, parameter checksum); the caller
         gathers every rank's pair at once."""
@@ -339,7 +342,7 @@ class FusedUpdate:
                 inv, self.ppo.policy_clip, self.ppo.value_coef, self.ppo.entropy_coef,
                 group["lr"], group["betas"][0], group["betas"][1], group["eps"],
                 group["weight_decay"], 2.0, loss, world, self._dp_rank, self._xbufs,
-                self._dp_seq, self.ws, fine_grained=self._dp_fine, push=self._dp_push)
+                self._dp_seq, self.ws, fine_grained=self._dp_fine, push=self._dp_push, split=split)
             self._dp_seq += 2
             torch.cuda.synchronize()
             status = max(prl_native.ppo_update_status(self.ws).tolist())
@@ -376,9 +379,13 @@ class FusedUpdate:
         counts = [sum(min(mb, max(0, n - j * mb)) for n in n_ranks) for j in range(nb)]
         inv = torch.tensor([1.0 / c for c in counts], dtype=torch.float32, device=S.device)
         A2 = A if A.dim() == 2 else A.reshape(-1, 1)
-        # the ranks' launches must overlap: line them up (the cross-rank wait also absorbs skew)
+        # the ranks' launches must overlap: line them up (the cross-rank wait also absorbs skew).
+        # The gather doubles as the vote on the kernel form: the head-split kernel only when every
+        # rank's process would pick it (its split mode and CU count are per process)
         torch.cuda.synchronize()
-        tdist.barrier()
+        votes = [None] * world
+        tdist.all_gather_object(votes, prl_native.ppo_update_dp_split(self.D, self.A, self.discrete, mb))
+        split = all(votes)
         if self.before_dp_launch is not None:   # test injection point (a late rank)
             self.before_dp_launch(self._dp_rank)
         if self.events is not None:
@@ -391,7 +398,8 @@ class FusedUpdate:
                 ret.contiguous(), mb, k_epochs, nb, inv, self.ppo.policy_clip,
                 self.ppo.value_coef, self.ppo.entropy_coef, group["lr"], beta1, beta2,
                 group["eps"], group["weight_decay"], 2.0, self.loss, world, self._dp_rank, xb,
-                self._dp_seq, self.ws, fine_grained=self._dp_fine, push=self._dp_push)
+                self._dp_seq, self.ws, fine_grained=self._dp_fine, push=self._dp_push,
+                split=split)
             launch_error = None
         except (RuntimeError, ValueError) as e:
             # this rank did not launch (e.g. an argument check): it still joins the gather

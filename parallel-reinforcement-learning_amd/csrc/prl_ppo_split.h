@@ -346,7 +346,7 @@ __device__ inline void spl_sum_partials(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
 // tm[12 + 2 slot], tm[13 + 2 slot]; tm[16] counts the samples, tm[17] those whose last arrival
 // at A was a role-1 (critic) workgroup.
 __device__ inline void spl_prof_stamp(const UpdArgs& a, int slot, int g) {
-  __hip_atomic_store(a.prof + 32 + 256 * slot + g, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+  __hip_atomic_store(upd_g(a.prof + 32 + 256 * slot + g), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ inline void spl_prof_skew(const UpdArgs& a, int slot, int G, int Gt, unsigned long long* tm) {
@@ -355,7 +355,7 @@ __device__ inline void spl_prof_skew(const UpdArgs& a, int slot, int G, int Gt, 
   int arg = 0;
   for (int i0 = 0; i0 < G && i0 < 256; i0 += 64) {
     const int i = i0 + l;
-    const unsigned long long v = i < G ? __hip_atomic_load(a.prof + 32 + 256 * slot + i, __ATOMIC_RELAXED,
+    const unsigned long long v = i < G ? __hip_atomic_load(upd_g(a.prof + 32 + 256 * slot + i), __ATOMIC_RELAXED,
                                                            __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     unsigned long long vmx = i < G ? v : 0ull, vmn = i < G ? v : ~0ull;
     int vi = i;
@@ -475,6 +475,38 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
   sub.mark(1);   // slice combined, its stores issued
 }
 
+// Phase-B helpers: workgroups G .. Gs - 1 of a single-GPU split launch (PRL_UPD_SPL_HELP; by
+// default the CUs the 2 Gt tile workgroups leave idle).  They hold no parameters and run no tile:
+// each step they wait for counter A, reduce their slice, and arrive at counter B.  The slices are
+// cut over all Gs owners (spl_slice_start), so an owner loads ~1 / Gs of the partials' bytes
+// instead of ~1 / G: phase B's landing is the per-CU rate of latency-bound sc1 loads (~20 KB per
+// us), not the chip's.  Each quad is still summed over the same partials in the same order, and
+// the reduced gradient lands in the same place, so the tile workgroups see the same hand-off.
+template <int NT>
+__device__ __forceinline__ void spl_helper(const UpdArgs& args, int g, int Qtot, int Qp, int QT, float* scratch,
+                                        int* s_abort) {
+  const int t = threadIdx.x;
+  const SplSlice slc = spl_slice_plan<NT>(g, args.Gs, Qp, QT, args.Gt, args.spl_fill);
+  const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_part2 = upd_rsrc(args.part2),
+                               rs_red = upd_rsrc(args.red);
+  const UpdSub none{nullptr, nullptr};
+  for (int s = 0; s < args.total_steps; ++s) {
+    if (t < 64) {
+      const bool ok = upd_wait_sharded(args.ctr, UPD_CTR_A, (unsigned)args.G * (unsigned)(s + 1));
+      if (t == 0) *s_abort = ok ? 0 : 1;
+    }
+    __syncthreads();
+    if (*s_abort) return;
+    spl_slice_reduce<NT>(rs_part, rs_part2, rs_red, Qtot, Qp, QT, slc, args.Gt, scratch, false, none, args, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      if (args.profile && (s & 15) == 8) spl_prof_stamp(args, 1, g);
+      upd_arrive(args.ctr, UPD_CTR_B, g);
+    }
+  }
+}
+
 // NQC = ceil(Qp / 256): quads per thread of phase C's canonical sweep (the moment registers
 // cover the same slots; a slot holds moments only where this role owns the quad).
 // DP: data-parallel ranks (prl_ppo_update_dpx): union-minibatch row weights inv_count[j] and,
@@ -516,13 +548,18 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   const UpdScr sc = upd_scr(scratch, n.D, SPL_NW);
   int* s_abort = reinterpret_cast<int*>(hdr + 8);
   float* s_adam = hdr + 10;
+  const int Gs = args.Gs;   // slice owners: the G tile workgroups, then Gs - G phase-B helpers
+  if (g >= G) {
+    spl_helper<SPL_NT>(args, g, Qtot, Qp, QT, scratch, s_abort);
+    return;
+  }
 
   constexpr int NMR = OWN ? 1 : NQC;
   float4 mreg[NMR], vreg[NMR];
   for (int q = t; q < Qp; q += SPL_NT)
     *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(args.params + 4 * q);
   // OWN: this thread's slice quad (see slc below) and its moments
-  const SplSlice slc0 = spl_slice_plan<SPL_NT>(g, G, Qp, QT, Gt, args.spl_fill);
+  const SplSlice slc0 = spl_slice_plan<SPL_NT>(g, Gs, Qp, QT, Gt, args.spl_fill);
   const int oq = (OWN && t < slc0.nq && slc0.qlo + t < Qp) ? slc0.qlo + t : -1;
   if constexpr (OWN) {
     mreg[0] = oq >= 0 ? *reinterpret_cast<const float4*>(args.exp_avg + 4 * oq) : float4{0.f, 0.f, 0.f, 0.f};
@@ -739,15 +776,15 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     if (t < 64) {
       if (args.profile && (s & 15) == 8 && t == 0) spl_prof_stamp(args, 1, g);
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_B, g);
-      const bool ok = args.spl_poll ? upd_wait_sharded_pipe(args.ctr, UPD_CTR_B, (unsigned)G * (unsigned)(s + 1))
-                                    : upd_wait_sharded(args.ctr, UPD_CTR_B, (unsigned)G * (unsigned)(s + 1));
+      const bool ok = args.spl_poll ? upd_wait_sharded_pipe(args.ctr, UPD_CTR_B, (unsigned)Gs * (unsigned)(s + 1))
+                                    : upd_wait_sharded(args.ctr, UPD_CTR_B, (unsigned)Gs * (unsigned)(s + 1));
       if (t == 0) *s_abort = ok ? 0 : 1;
     }
     __syncthreads();
     if (*s_abort) return;
     mark(4);   // wait B
     if (args.profile && (s & 15) == 8 && g == 0) {   // (not A's sampled steps: its read-back delays g 0)
-      if (t < 64) spl_prof_skew(args, 1, G, Gt, tm);
+      if (t < 64) spl_prof_skew(args, 1, Gs, Gt, tm);
       __syncthreads();
       if (t == 0) pts[7] = __builtin_amdgcn_s_memrealtime();
     }

@@ -133,6 +133,7 @@ struct UpdArgs {
   int64_t N;
   int mb, nb, total_steps, G, R;
   int Gt;           // tile groups (= G, or G / replicas in the latency form's replicated tiles)
+  int Gs;           // head-split form: phase-B slice owners = the G tile workgroups + Gs - G helpers
   float clip, vf_coef, ent_coef, lr;
   double beta1, beta2;   // AdamW betas as the caller's doubles: 1 - beta2 from a float32 beta2 is 1.3e-5 off
   float eps, wd, max_norm;
@@ -2483,6 +2484,17 @@ bool upd_split_own(const UpdNet& n, int G, int NT) {
     if (2 * (start(g + 1) - start(g)) > NT) return false;
   return true;
 }
+// Phase-B helper workgroups of the single-GPU split form (spl_helper): PRL_UPD_SPL_HELP = their
+// number (0 = none), by default every CU the G tile workgroups leave free (capped at 256 owners).
+int upd_split_helpers(int G) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const int room = std::max(0, std::min(cus, 256) - G);
+  const char* e = getenv("PRL_UPD_SPL_HELP");
+  return e ? std::min(room, std::max(0, atoi(e))) : room;
+}
 bool upd_split_host(const UpdNet& n, int Gt, int R, bool tp) {
   if (tp || !g_split || upd_force_generic() || !upd_is_cartpole(n) || R != UPD_RT) return false;
   if (cdiv(n.Lp / 4, 64 * upd_split_waves()) > (upd_split_waves() == 8 ? SPL_NQC8 : SPL_NQC)) return false;
@@ -2604,7 +2616,7 @@ size_t upd_xbuf_bytes(const UpdNet& n, int mb) {
   return upd_xbuf_push_flags_off(n, mb) + (size_t)UPD_MAX_RANKS * 2 * upd_grid(mb) * 8;
 }
 unsigned g_dp_spin_limit = UPD_DP_SPIN_LIMIT;
-int32_t g_last_plan[7] = {-1, -1, -1, -1, -1, -1, -1};   // prl_ppo_update_last_plan
+int32_t g_last_plan[8] = {-1, -1, -1, -1, -1, -1, -1, -1};   // prl_ppo_update_last_plan
 
 int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, int32_t D,
             int32_t A, int32_t discrete, const float* S, const float* actions,
@@ -2709,7 +2721,9 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     if (p2.kern) plan = p2;
     else tp = false;
   }
-  const bool split = upd_split_host(args.net, Gt, args.R, tp);
+  // data-parallel ranks: fine_grained bit 2 = the ranks voted for the 8-wave kernel
+  // (prl_ppo_update_dp_split: the kernel form must not come from per-process state alone)
+  const bool split = upd_split_host(args.net, Gt, args.R, tp) && !(dp && (dp->fine & 4));
   if (!split) args.dp_push = 0;   // the push form is the head-split kernel's (ranks decide alike)
   g_last_own = 0;
   if (split) {
@@ -2726,6 +2740,8 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   // replicated tiles: the latency form on one GPU only; the split form: two roles per tile group
   const int G = split ? 2 * Gt : ((tp || dp) ? Gt : Gt * upd_repl(Gt));
   args.G = G;
+  // phase-B helpers of the single-GPU split form (prl_ppo_split.h, spl_helper)
+  args.Gs = (split && !dp && !g_last_own) ? G + upd_split_helpers(G) : G;
   const size_t lds = upd_lds_bytes_plan(args.net, plan.nw, tp, plan.tiles);
   PRL_REQUIRE(lds <= 160 * 1024, "prl_ppo_update: %zu B of LDS needed", lds);
   hipStream_t st = as_stream(stream);
@@ -2739,6 +2755,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
                                              (!args.net.discrete && args.net.A == 1 && args.net.D == 3))) ? 1 : 0;
   g_last_plan[5] = G / Gt;
   g_last_plan[6] = split ? (g_last_own ? 2 : 1) : 0;
+  g_last_plan[7] = args.Gs - G;
   PRL_HIP_TRY(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr, 0, 16, st));
   PRL_HIP_TRY(hipMemsetAsync(ws.ctr + UPD_CTR_A, 0, 4 * (UPD_CTR_WORDS - UPD_CTR_A), st));
@@ -2747,7 +2764,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
   hipLaunchKernelGGL(ppo_image_kernel, dim3(img_grid), dim3(UPD_THREADS), 0, st, args.net, params,
                      exp_avg, exp_avg_sq, img_p, img_m, img_v, 1);
   PRL_LAUNCH_CHECK("ppo_image");
-  PRL_HIP_TRY(upd_launch_resident(kern, G, 64 * plan.nw, lds, kargs, st));
+  PRL_HIP_TRY(upd_launch_resident(kern, args.Gs, 64 * plan.nw, lds, kargs, st));
   hipLaunchKernelGGL(ppo_image_kernel, dim3(img_grid), dim3(UPD_THREADS), 0, st, args.net, params,
                      exp_avg, exp_avg_sq, img_p, img_m, img_v, 0);
   PRL_LAUNCH_CHECK("ppo_image");
@@ -2804,8 +2821,16 @@ extern "C" int32_t prl_ppo_update_set_split(int32_t mode) {
   return prev;
 }
 
-extern "C" void prl_ppo_update_last_plan(int32_t out[7]) {
-  for (int i = 0; i < 7; ++i) out[i] = g_last_plan[i];
+extern "C" int32_t prl_ppo_update_dp_split(int32_t D, int32_t A, int32_t discrete, int32_t mini_batch) {
+  UpdNet n;
+  if (mini_batch <= 0 || !upd_layout(D, A, discrete, n)) return 0;
+  const int Gt = upd_grid(mini_batch);   // as upd_run: tile groups, rows per workgroup and step
+  const int R = (int)cdiv(cdiv((int64_t)mini_batch, (int64_t)Gt), (int64_t)UPD_RT) * UPD_RT;
+  return upd_split_host(n, Gt, R, false) ? 1 : 0;   // (data-parallel launches never take tp)
+}
+
+extern "C" void prl_ppo_update_last_plan(int32_t out[8]) {
+  for (int i = 0; i < 8; ++i) out[i] = g_last_plan[i];
 }
 
 extern "C" uint32_t prl_dp_set_spin_limit(uint32_t polls) {

@@ -90,6 +90,7 @@ SIGNATURES = {
     "prl_ppo_update_set_tp": [_I32],
     "prl_ppo_update_set_repl": [_I32],
     "prl_ppo_update_set_split": [_I32],
+    "prl_ppo_update_dp_split": [_I32, _I32, _I32, _I32],
     "prl_debug_fill_lds": [_F32, _P],
     "prl_ppo_update_last_plan": [_P],
     "prl_source_id": [],
@@ -117,10 +118,12 @@ _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_source_id": ctypes.c_char_p
              "prl_rnd_pred_grad_ws_floats": _I64, "prl_dp_xbuf_bytes": _I64,
              "prl_dp_set_spin_limit": ctypes.c_uint32, "prl_ppo_update_set_tp": _I32,
              "prl_ppo_update_set_repl": _I32, "prl_ppo_update_set_split": _I32,
+             "prl_ppo_update_dp_split": _I32,
              "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
 
 _lib = None
 _lock = threading.Lock()
+ABI_VERSION = 2   # include/prl_abi.h PRL_ABI_VERSION (2: prl_ppo_update_last_plan writes 8 entries)
 
 
 def _sources_id():
@@ -155,8 +158,9 @@ def lib():
                     fn = getattr(L, name)
                     fn.argtypes = args
                     fn.restype = _RESTYPES.get(name, ctypes.c_int)
-                if L.prl_abi_version() != 1:
-                    raise RuntimeError("libprl_hip.so ABI version mismatch")
+                if L.prl_abi_version() != ABI_VERSION:
+                    raise RuntimeError(f"libprl_hip.so ABI version {L.prl_abi_version()}, this "
+                                       f"package needs {ABI_VERSION}: rebuild it")
                 want = _sources_id()
                 got = L.prl_source_id().decode()
                 if want is not None and got != want:
@@ -781,13 +785,14 @@ def ppo_update_last_plan() -> dict:
     the kernel was a compile-time-layout specialisation, and the workgroups per tile group (the
     latency form's replicated tiles; the split form: its two head roles), and whether the
     head-split latency form ran (csrc/prl_ppo_split.h) and whether in its slice-owner variant
-    ("owner": AdamW by the slice owners, PRL_UPD_SPL_OWN)."""
-    out = (ctypes.c_int32 * 7)()
+    ("owner": AdamW by the slice owners, PRL_UPD_SPL_OWN), and the split form's phase-B helper
+    workgroups (launched beside "grid")."""
+    out = (ctypes.c_int32 * 8)()
     lib().prl_ppo_update_last_plan(out)
-    tp, nw, G, tiles, spec, repl, split = list(out)
+    tp, nw, G, tiles, spec, repl, split, helpers = list(out)
     return {"form": {1: "throughput", 0: "latency"}.get(tp), "waves": nw, "grid": G,
             "tiles": tiles, "specialised": bool(spec == 1), "replicas": repl,
-            "split": bool(split >= 1), "owner": bool(split == 2)}
+            "split": bool(split >= 1), "owner": bool(split == 2), "helpers": helpers}
 
 
 XBUF_KINDS = {"auto": 0, "uncached": 1, "fine": 2}
@@ -829,15 +834,22 @@ def dp_ipc_close(p):
         _check(lib().prl_dp_ipc_close(p), "prl_dp_ipc_close")
 
 
+def ppo_update_dp_split(D, A, discrete, mini_batch) -> bool:
+    """Would a data-parallel launch of this shape run the head-split kernel in this process?
+    (The ranks vote: the kernel form must be the same on every rank.)"""
+    return bool(lib().prl_ppo_update_dp_split(int(D), int(A), int(bool(discrete)), int(mini_batch)))
+
+
 def ppo_update_dpx(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, actions, old_logp,
                    adv, ret, mini_batch, k_epochs, nb_union, inv_count, clip, vf_coef, ent_coef,
                    lr, beta1, beta2, eps, weight_decay, max_norm, loss_out, world, rank, xbufs,
-                   seq0, workspace, fine_grained=False, push=False):
+                   seq0, workspace, fine_grained=False, push=False, split=True):
     """The persistent engine as one data-parallel rank: the cross-rank gradient sum runs inside
     the launch over the ranks' IPC-mapped slice buffers `xbufs` (rank order); fine_grained: any
     rank's buffer is fine-grained memory (the flags are then fenced); push: the push form of the
     exchange (every rank writes its slice and flag into every rank's buffer and polls its own;
-    the head-split kernel only, else the pull form runs) — every rank must pass the same."""
+    the head-split kernel only, else the pull form runs); split=False forces the 8-wave kernel
+    (the ranks' vote, ppo_update_dp_split) — every rank must pass the same."""
     N = int(S.shape[0])
     arr = (ctypes.c_void_p * len(xbufs))(*[ctypes.c_void_p(getattr(x, "value", x)) for x in xbufs])
     _check(lib().prl_ppo_update_dpx(
@@ -850,7 +862,8 @@ def ppo_update_dpx(params, exp_avg, exp_avg_sq, adam_step, D, A, discrete, S, ac
         float(vf_coef), float(ent_coef), float(lr), float(beta1), float(beta2), float(eps),
         float(weight_decay), float(max_norm), _dev(loss_out, torch.float32, "loss_out"),
         int(world), int(rank), ctypes.cast(arr, ctypes.c_void_p), int(seq0),
-        int(bool(fine_grained)) | (int(bool(push)) << 1), _dev(workspace, torch.uint8, "workspace"),
+        int(bool(fine_grained)) | (int(bool(push)) << 1) | (0 if split else 4),
+        _dev(workspace, torch.uint8, "workspace"),
         workspace.numel(),
         _stream()),
         "prl_ppo_update_dpx")

@@ -22,11 +22,11 @@ def test_abi_library_exports_every_declared_symbol():
     import prl_native
     L = prl_native.lib()
     syms = _declared_symbols()
-    assert len(syms) == len(prl_native.SIGNATURES) == 68
+    assert len(syms) == len(prl_native.SIGNATURES) == 69
     for s in syms:
         assert hasattr(L, s), s
         assert s in prl_native.SIGNATURES, f"{s} has no ctypes signature"
-    assert L.prl_abi_version() == 1
+    assert L.prl_abi_version() == prl_native.ABI_VERSION == 2
     # the library was built from the sources next to it (csrc/build.py stamps them)
     assert L.prl_source_id().decode() == prl_native._sources_id()
 

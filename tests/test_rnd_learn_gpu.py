@@ -46,8 +46,12 @@ WEIGHT_ATOL = {"learn_rnd": (2e-6, 2e-6), "learn_rnd_c5": (1e-5, 5e-6), "learn_r
 # learn_rnd_c5 needs it through the fused update_pred gradient (prl_rnd_pred_grad): 1.04e-5 from
 # the PyTorch-CPU float32 fixture, whose own distance from the float64 update is of that order
 # (AdamW's m / sqrt(v) turns last-bit gradient differences on near-zero entries into up to ~1 %
-# of an lr = 1e-3 step, in either float32 run).
+# of an lr = 1e-3 step, in either float32 run).  Measured (round 5, MI355X): learn_rnd_c5 ours
+# 1.04e-5 from the fixture (2.08 x its 5e-6 bound); vs float64 ours 2.08e-5, reference 1.04e-5.
+# The other tags stay inside their absolute bounds.  Past the bound the guard applies, but never
+# past RND_CEIL_FACTOR x the bound (a hard ceiling, so the relational guard cannot hide drift).
 F64_FACTOR = 3.0
+RND_CEIL_FACTOR = 3.0
 
 
 def _rnd_update_f64(g, S, mb):
@@ -169,6 +173,7 @@ def test_learn_with_rnd_matches_reference_learn(golden, tag, path):
     pol_atol, rnd_atol = WEIGHT_ATOL[tag]
     sd, ref = p.rnd.state_dict(), _sub(g, "rnd_final/")
     worst_rnd = max(_max_abs(sd[k].cpu(), ref[k]) for k in ref)
+    assert worst_rnd <= RND_CEIL_FACTOR * rnd_atol, (tag, worst_rnd, rnd_atol)   # hard ceiling
     if worst_rnd > rnd_atol:   # the relational guard (WEIGHT_ATOL note)
         S_in, _ = _inputs(g)
         w64 = _rnd_update_f64(g, S_in, int(g["mb"]))

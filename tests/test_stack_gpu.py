@@ -139,8 +139,10 @@ def test_cartpole_persistent_rollout_matches_oracle_given_its_probs(E):
     """The whole CartPole rollout as one launch (prl_cartpole_rollout: one thread per env runs
     the actor's forward, Categorical sampling, the float64 step and the trajectory push to the end
     of its episode), through AsyncPPO.worker() with the real policy.  Its forward sums in another
-    order than the per-step path's PyTorch GEMMs, so the check is: (1) its probabilities at t = 0
-    against a float64 forward of policy_old (1e-5), and (2) given the probabilities it sampled
+    order than the per-step path's PyTorch GEMMs, so the check is: (1) its probabilities at EVERY
+    step of every env (the row of probs_out it sampled from) against a float64 forward of
+    policy_old on the state the env was in (the memory's env-major rows: 1e-5), and (2) given the
+    probabilities it sampled
     from at every step (probs_out), the oracle worker (AsyncPPO.py:117-146 with the oracle's
     Philox sampling and gymnasium 1.1.1 physics) reproduces the memory bit for bit — states,
     actions, rewards, done flags, lengths and the score counters."""
@@ -175,11 +177,8 @@ def test_cartpole_persistent_rollout_matches_oracle_given_its_probs(E):
     orc = O.CartPoleOracle(E)
     orc.seed(np.arange(E) + seed)
     ss = a.sample_seed
-    first = {}
 
     def act(states, idx, t):
-        if t == 0:
-            first["S"] = states.copy()
         return O.sample_categorical(P[t], ss, np.full(E, t, np.int32))[idx]
 
     ref = O.worker_oracle(orc, act)
@@ -189,11 +188,16 @@ def test_cartpole_persistent_rollout_matches_oracle_given_its_probs(E):
     np.testing.assert_array_equal(R, ref["R"])
     np.testing.assert_array_equal(Dn, ref["D"])
     assert float(a.reward_score) == float(ref["reward_score"])
-    # (1) the probabilities at t = 0 against a float64 forward of policy_old
+    # (1) every step's probabilities against a float64 forward of policy_old: memory row k of
+    # env e (env-major) is env e's state at step t = k - (its first row), sampled from P[t, e]
+    lens = ref["lengths"]
+    env_of = np.repeat(np.arange(E), lens)
+    t_of = np.arange(n) - np.repeat(np.cumsum(lens) - lens, lens)
     pol = copy.deepcopy(ppo.policy_old).cpu().double()
     with torch.no_grad():
-        p64 = pol.actor(pol.model(torch.from_numpy(first["S"]).double())).numpy()
-    np.testing.assert_allclose(P[0].astype(np.float64), p64, rtol=0, atol=1e-5)
+        p64 = pol.actor(pol.model(torch.from_numpy(S).double())).numpy()
+    assert t_of.max() > 8     # the check reaches well past the reset neighbourhood
+    np.testing.assert_allclose(P[t_of, env_of].astype(np.float64), p64, rtol=0, atol=1e-5)
 
 
 def test_evaluate_matches_oracle_episodes():
@@ -333,7 +337,9 @@ def test_rnd_module_matches_reference(golden):
         x = torch.from_numpy(g[f"D{D}_x"]).cuda()
         out = r.compute_intrinsic_reward(list(x.split(64)))
         np.testing.assert_allclose(out.cpu().numpy(), g[f"D{D}_r"], rtol=2e-5, atol=1e-8)
-        r.update_pred(list(x.split(64)))   # stays PyTorch; must run
+        # must run: the native prl_rnd_pred_grad + prl_flat_adamw step (its numbers are checked
+        # in test_rnd_learn_gpu.py)
+        r.update_pred(list(x.split(64)))
 
 
 def test_gae_graph_capture_replay():
