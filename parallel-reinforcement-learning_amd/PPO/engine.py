@@ -300,11 +300,28 @@ class FusedUpdate:
         self._xbuf_own, self._xbufs, self._dp_rank, self._dp_seq = own, ptrs, rank, 0
         # every rank runs the same collectives whatever its local outcome: ONE gather of
         # (ok, checksum) per rank, then the same decision everywhere
+        # co-residency: every rank's workgroups of one launch must be resident together, so ranks
+        # that share a GPU (the one-GPU rehearsals) must fit its CUs between them — the split
+        # kernel's 2 x tile groups per rank, else the 8-wave kernel's tile groups, else no
+        # persistent launch at all (the stepped loop runs)
         votes = [None] * world
-        tdist.all_gather_object(votes, prl_native.ppo_update_dp_split(self.D, self.A, self.discrete,
-                                                                      self.mini_batch))
+        tdist.all_gather_object(votes, (self._device_key(),
+                                        prl_native.ppo_update_dp_split(self.D, self.A, self.discrete,
+                                                                       self.mini_batch)))
+        share = sum(1 for k, _ in votes if k == self._device_key())
+        cus = torch.cuda.get_device_properties(self.flat.device).multi_processor_count
+        fits = [None] * world
+        tdist.all_gather_object(fits, (share * 2 * self.grid <= cus, share * self.grid <= cus))
+        self._dp_split_fits = all(f for f, _ in fits)
+        if not all(f for _, f in fits):
+            warnings.warn("data-parallel persistent engine: the ranks sharing a GPU do not fit its "
+                          "CUs together; using the stepped loop")
+            self.close()
+            self._xb_tried = True
+            return None
         res = [None] * world
-        tdist.all_gather_object(res, self._dp_selftest(world, all(votes)))
+        tdist.all_gather_object(res, self._dp_selftest(
+            world, all(s for _, s in votes) and self._dp_split_fits))
         sums = [c for _, c in res]
         if not (all(ok for ok, _ in res) and len(set(sums)) == 1 and sums[0] == sums[0]):
             warnings.warn("data-parallel persistent engine failed its self-test; using the "
@@ -313,6 +330,13 @@ class FusedUpdate:
             self._xb_tried = True
             return None
         return ptrs
+
+    def _device_key(self):
+        """Which physical GPU this rank's engine runs on (host + device UUID, or PCI location)."""
+        import socket
+        pr = torch.cuda.get_device_properties(self.flat.device)
+        uid = str(getattr(pr, "uuid", "") or "")
+        return (socket.gethostname(), uid or (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id))
 
     def _dp_checksum(self, flat) -> float:
         return float(flat.double().sum().item()) + float((flat.double() ** 2).sum().item())
@@ -385,7 +409,7 @@ class FusedUpdate:
         torch.cuda.synchronize()
         votes = [None] * world
         tdist.all_gather_object(votes, prl_native.ppo_update_dp_split(self.D, self.A, self.discrete, mb))
-        split = all(votes)
+        split = all(votes) and getattr(self, "_dp_split_fits", True)
         if self.before_dp_launch is not None:   # test injection point (a late rank)
             self.before_dp_launch(self._dp_rank)
         if self.events is not None:

@@ -35,6 +35,7 @@
 // 8, waves 4-7 only join the tile's barriers and add their threads to the publish, phase B's
 // loads and phase C (PRL_UPD_SPL_WAVES; A/B)
 constexpr int SPL_NW = 4;
+constexpr int SPL_CQ = 4;   // quads per norm piece (spl_piece)
 
 // one 16-row tile of role r = head h (h = r): forward (trunk + head h), the head's loss, its
 // backward through the trunk; the gradient into the LDS image Ga (first tile of the step: every
@@ -286,13 +287,25 @@ __device__ __forceinline__ void spl_tile(const UpdNet& n, const UpdArgs& args, i
 // equal-quad slices left the trunk's owners loading twice the others' bytes, 3.7 vs 2.0 us).
 // So quad q weighs 2 for q < QT and q == Qp, else 1: weighted position w(q) = q + min(q, QT),
 // U = Qp + QT + 2 units, and slice g starts at the first quad with w(q) >= U g / G.
+// Starts are rounded down to a multiple of SPL_CQ (a norm piece's chunk, below: no chunk straddles
+// two slices; upd_split_own on the host cuts the same way).
 __device__ inline int spl_slice_start(int g, int G, int Qp, int QT) {
   const int Qtot = Qp + 1;
   const int64_t U = (int64_t)Qp + QT + 2;
   const int64_t u = U * g / G;
   const int64_t q = u <= 2 * (int64_t)QT ? (u + 1) / 2 : u - QT;
-  return (int)(q < Qtot ? q : Qtot);
+  return q < Qtot ? (int)(q / SPL_CQ) * SPL_CQ : Qtot;
 }
+
+// Norm pieces (PRL_UPD_SPL_PIECES, default on): clip_grad_norm_'s squared norm as a sum of
+// per-chunk pieces, chunk c = reduced-gradient quads [SPL_CQ c, SPL_CQ c + SPL_CQ) below the loss
+// quad, piece = ((q0^2 + q1^2) + (q2^2 + q3^2)) of the quads' ((x^2 + y^2) + (z^2 + w^2)).  Each
+// piece is a function of its chunk's reduced values only, formed by whichever workgroup owns the
+// chunk (slice owner, helper, or the data-parallel union of the slice), so every launch form
+// gives the same pieces; phase C sums them in one canonical order (the same bits on every
+// workgroup) and loads only the gradient quads its role owns (trunk + its head: ~half the
+// gradient) instead of all of them.
+// (upd_sq4 / upd_piece, prl_ppo_update.hip: shared with the data-parallel union slices; SPL_CQ = 4)
 
 // Sum of quad q over partials first, first + stride, ... of part (< Gt) and, for a dual quad
 // (nv = 2 Gt: the trunk / loss quads), over the same positions of part2 (quad qd there): the
@@ -416,15 +429,15 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
                                         __amdgpu_buffer_rsrc_t rs_red, int Qtot, int Qp, int QT,
                                         const SplSlice& pl, int Gt, float* scratch, bool sys,
                                         UpdSub sub, const UpdArgs& args, int par,
-                                        float4* gout = nullptr) {
+                                        float4* gout = nullptr, float* pieces = nullptr) {
   // gout (the slice-owner form, narrow slices only): thread t < nq keeps its quad's reduced
-  // gradient in *gout instead of storing it (the loss quad Qp is stored as always)
+  // gradient in *gout instead of storing it (the loss quad Qp is stored as always); pieces: the
+  // norm pieces of the slice's chunks (not with sys: the data-parallel union forms them)
   const int t = threadIdx.x;
   const int qlo = pl.qlo, qhi = pl.qhi, nq = pl.nq;
   if (nq <= 0) return;
   const int P2 = QT + 1;
-  auto fin = [&](int q, double ax, double ay, double az, double aw) {
-    const float4 r = float4{(float)ax, (float)ay, (float)az, (float)aw};
+  auto fin = [&](int q, const float4 r) {
     if (sys && args.dp_push) {
       // push form: straight into every rank's receive slot [par][this rank] (upd_dp_union_slice_push)
 #pragma unroll
@@ -440,13 +453,21 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
     }
   };
   if (2 * nq > NT) {
-    // wide slices (few workgroups, small minibatches): each thread owns whole quads
-    for (int q = qlo + t; q < qhi; q += NT) {
-      double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
-      const bool dual = q < QT || q == Qp;
-      spl_sum_partials(rs_part, rs_part2, Qtot, P2, q, q < QT ? q : QT, 0, 1, Gt, dual ? 2 * Gt : Gt,
-                       ax, ay, az, aw);
-      fin(q, ax, ay, az, aw);
+    // wide slices (few workgroups, small minibatches): each thread owns whole quads (uniform
+    // trip count: the pieces' DPP sums need every lane)
+    for (int q0 = qlo; q0 < qhi; q0 += NT) {
+      const int q = q0 + t;
+      float sqv = 0.f;
+      if (q < qhi) {
+        double ax = 0.0, ay = 0.0, az = 0.0, aw = 0.0;
+        const bool dual = q < QT || q == Qp;
+        spl_sum_partials(rs_part, rs_part2, Qtot, P2, q, q < QT ? q : QT, 0, 1, Gt, dual ? 2 * Gt : Gt,
+                         ax, ay, az, aw);
+        const float4 r = float4{(float)ax, (float)ay, (float)az, (float)aw};
+        fin(q, r);
+        sqv = q < Qp ? upd_sq4(r) : 0.f;
+      }
+      if (pieces) upd_piece(pieces, sqv, q, q < qhi && q < Qp);
     }
     return;
   }
@@ -463,15 +484,19 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
   }
   sub.mark(0);   // thread 0's partial loads landed and summed
   __syncthreads();
+  float sqv = 0.f;
   if (t < nq) {
     double ax = red[4 * t], ay = red[4 * t + 1], az = red[4 * t + 2], aw = red[4 * t + 3];
     for (int k = 1; k < spl; ++k) {
       const double* o = red + 4 * (k * nq + t);
       ax += o[0]; ay += o[1]; az += o[2]; aw += o[3];
     }
-    if (gout && qlo + t != Qp) *gout = float4{(float)ax, (float)ay, (float)az, (float)aw};
-    else fin(qlo + t, ax, ay, az, aw);
+    const float4 r = float4{(float)ax, (float)ay, (float)az, (float)aw};
+    if (gout && qlo + t != Qp) *gout = r;
+    else fin(qlo + t, r);
+    sqv = qlo + t < Qp ? upd_sq4(r) : 0.f;
   }
+  if (pieces) upd_piece(pieces, sqv, qlo + t, t < nq && qlo + t < Qp);
   sub.mark(1);   // slice combined, its stores issued
 }
 
@@ -497,7 +522,8 @@ __device__ __forceinline__ void spl_helper(const UpdArgs& args, int g, int Qtot,
     }
     __syncthreads();
     if (*s_abort) return;
-    spl_slice_reduce<NT>(rs_part, rs_part2, rs_red, Qtot, Qp, QT, slc, args.Gt, scratch, false, none, args, 0);
+    spl_slice_reduce<NT>(rs_part, rs_part2, rs_red, Qtot, Qp, QT, slc, args.Gt, scratch, false, none, args, 0,
+                         nullptr, args.spl_pieces ? args.sq : nullptr);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
@@ -747,7 +773,8 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       const unsigned long long gstep = args.dp_seq0 + (unsigned long long)s;
       const int par = (int)(gstep & 1ull);
       spl_slice_reduce<SPL_NT>(rs_part, rs_part2, DP ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
-                               Qtot, Qp, QT, slc, Gt, scratch, DP, subm, args, par, OWN ? &og : nullptr);
+                               Qtot, Qp, QT, slc, Gt, scratch, DP, subm, args, par, OWN ? &og : nullptr,
+                               (!DP && !OWN && args.spl_pieces) ? args.sq : nullptr);
       if constexpr (OWN) {
         // the owner's speculative AdamW (clip coefficient 1) on its quad; the new weights go out
         // in place of the gradient, with this wave's piece of the squared norm
@@ -767,8 +794,9 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       __syncthreads();
       if (DP) {
         const int qlo = slc.qlo, qhi = slc.qhi;
-        if (!(args.dp_push ? upd_dp_union_slice_push(args, rs_red, Qtot, g, gstep, par, s_abort, qlo, qhi)
-                           : upd_dp_union_slice(args, rs_red, Qtot, g, G, gstep, par, s_abort, qlo, qhi)))
+        float* const pcs = args.spl_pieces ? args.sq : nullptr;
+        if (!(args.dp_push ? upd_dp_union_slice_push(args, rs_red, Qtot, g, gstep, par, s_abort, qlo, qhi, pcs)
+                           : upd_dp_union_slice(args, rs_red, Qtot, g, G, gstep, par, s_abort, qlo, qhi, pcs)))
           return;
       }
     }
@@ -792,11 +820,42 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     float4 gq[NQC];
     float clipc;
     {
-#pragma unroll
-      for (int i = 0; i < NQC; ++i)
-        if (i * SPL_NT < Qp) gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
+      const bool pcs = !OWN && args.spl_pieces;
       float tot = 0.f;
-      if constexpr (OWN) {
+      if (pcs) {
+        // the norm from the pieces, loaded FIRST: every wave sums all of them itself (lane l:
+        // pieces 4 l .. 4 l + 3 of each 256-piece chunk, chunk by chunk, then the DPP tree; the
+        // same order and bits in every wave of every workgroup), so no workgroup barrier holds
+        // AdamW until the whole gradient has landed: slot i's update waits for slot i's loads only
+        const int nch = (Qp + SPL_CQ - 1) / SPL_CQ;   // <= 1,024 (NQC <= 10 at 4 waves)
+        const __amdgpu_buffer_rsrc_t rs_sq = upd_rsrc(args.sq);
+        const int l = t & 63;
+        float4 pc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (256 * c < nch) pc[c] = ld4_sc1_so(rs_sq, 16u * (unsigned)l, 1024u * (unsigned)c);
+        // this role's slots (uniform per workgroup: a slot any of its quads is owned in)
+#pragma unroll
+        for (int i = 0; i < NQC; ++i)
+          if (i * SPL_NT < Qp && (role == 0 ? i * SPL_NT < QH : (i * SPL_NT < QT || (i + 1) * SPL_NT > QH)))
+            gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
+        float acc = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int k = 256 * c + 4 * l;
+          if (256 * c < nch && k < nch)
+            acc += ((pc[c].x + (k + 1 < nch ? pc[c].y : 0.f)) + ((k + 2 < nch ? pc[c].z : 0.f) + (k + 3 < nch ? pc[c].w : 0.f)));
+        }
+        acc = wave_sum_f32_to63(acc);
+        tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), 63));
+        subm.mark(2);   // thread 0's pieces landed
+      } else {
+#pragma unroll
+        for (int i = 0; i < NQC; ++i)
+          if (i * SPL_NT < Qp) gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
+      }
+      if (pcs) {
+      } else if constexpr (OWN) {
         // gq: the NEW weights; the norm from the G x TW pieces, in one fixed order everywhere
         // (lane l: pieces 4 l .. 4 l + 3 of each 256-piece chunk, every chunk's load issued first)
         const int l = t & 63, npc = G * TW;
@@ -881,31 +940,9 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
           float4 pw = *reinterpret_cast<float4*>(W + 4 * q);
           float4 m4 = mreg[i], v4 = vreg[i];
           const float4 g4 = gq[i];
-          // the engine's AdamW arithmetic (ppo_update_body): the 4-wave scalar form, or two
-          // elements per packed-f32 instruction (the same operations per element, so the same bits)
-          if (args.spl_pk) {
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-              const upd_f2 gr = upd_f2{f4get(g4, 2 * hh), f4get(g4, 2 * hh + 1)} * clipc;
-              upd_f2 m = upd_f2{f4get(m4, 2 * hh), f4get(m4, 2 * hh + 1)};
-              upd_f2 v = upd_f2{f4get(v4, 2 * hh), f4get(v4, 2 * hh + 1)};
-              upd_f2 p = upd_f2{f4get(pw, 2 * hh), f4get(pw, 2 * hh + 1)};
-              p = p * decay;
-              m = upd_pkfma(upd_f2{omb1, omb1}, gr - m, m);
-              v = upd_pkfma((upd_f2)(omb2 * gr), gr, v * b2);
-              const upd_f2 sq{__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
-              const upd_f2 denom = upd_pkfma(sq, upd_f2{inv_bc2_sqrt, inv_bc2_sqrt}, upd_f2{args.eps, args.eps});
-              upd_f2 rq{__builtin_amdgcn_rcpf(denom.x), __builtin_amdgcn_rcpf(denom.y)};
-              rq = upd_pkfma(rq, upd_pkfma(-denom, rq, upd_f2{1.0f, 1.0f}), rq);
-              p = upd_pkfma(upd_f2{-step_size, -step_size}, m * rq, p);
-              f4set(m4, 2 * hh, m.x);
-              f4set(m4, 2 * hh + 1, m.y);
-              f4set(v4, 2 * hh, v.x);
-              f4set(v4, 2 * hh + 1, v.y);
-              f4set(pw, 2 * hh, p.x);
-              f4set(pw, 2 * hh + 1, p.y);
-            }
-          } else {
+          // the engine's AdamW arithmetic (ppo_update_body, the 4-wave scalar form; hipcc pairs
+          // the elements into packed-f32 instructions itself)
+          {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float gr = f4get(g4, e) * clipc;

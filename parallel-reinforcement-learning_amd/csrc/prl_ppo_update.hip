@@ -148,6 +148,7 @@ struct UpdArgs {
   int spl_direct;   // head-split form: dW1 stored from registers into the partial (PRL_UPD_SPL_DIRECT)
   int spl_poll;     // head-split form: counter waits with four polls in flight (PRL_UPD_SPL_POLL)
   int spl_pk;       // head-split form: AdamW two elements per packed-f32 instruction (PRL_UPD_SPL_PK)
+  int spl_pieces;   // head-split form: the clip norm from per-chunk pieces (PRL_UPD_SPL_PIECES)
   float* red;       // [Qtot * 4]
   float* sq;        // [NW G] per-wave squared-norm pieces of the slices
   unsigned* ctr;    // [0] arrivals A, [1] arrivals B, [2] abort, [3] status (zeroed per launch),
@@ -1527,9 +1528,19 @@ __device__ inline float upd_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgp
 // args.dp_fine) the flag store follows a system-scope release and the slice loads a system-scope
 // acquire.
 
+// The head-split form's clip-norm pieces (prl_ppo_split.h, spl_piece): chunks of 4 reduced-gradient
+// quads, piece = ((q0^2 + q1^2) + (q2^2 + q3^2)) of ((x^2 + y^2) + (z^2 + w^2)), formed here for the
+// data-parallel union slices exactly as the single-GPU slice owners form them.
+__device__ inline float upd_sq4(float4 r) { return (r.x * r.x + r.y * r.y) + (r.z * r.z + r.w * r.w); }
+__device__ inline void upd_piece(float* pieces, float sqv, int q, bool valid) {
+  sqv += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sqv), 0xB1, 0xF, 0xF, false));
+  sqv += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sqv), 0x4E, 0xF, 0xF, false));
+  if (valid && (q & 3) == 0) st_sc1f(pieces + q / 4, sqv);
+}
+
 __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t rs_red, int Qtot,
                                    int g, int G, unsigned long long gstep, int par, int* s_abort,
-                                   int qlo_in = -1, int qhi_in = -1) {
+                                   int qlo_in = -1, int qhi_in = -1, float* pieces = nullptr) {
   const int t = threadIdx.x, NT = blockDim.x;
   const unsigned long long want = gstep + 1ull;
   if (t == 0) {
@@ -1580,19 +1591,26 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
   const int qlo = qlo_in >= 0 ? qlo_in : (int)((int64_t)Qtot * g / G);
   const int qhi = qhi_in >= 0 ? qhi_in : (int)((int64_t)Qtot * (g + 1) / G);
   const size_t base = (size_t)par * Qtot * 4;
-  for (int q = qlo + t; q < qhi; q += NT) {
-    float4 acc = ld4_aux<UPD_AUX_SYS>(upd_rsrc(args.xbuf[0] + base), (size_t)q * 4);
+  // (uniform trip count: the split form's norm pieces, spl_piece, need every lane)
+  for (int q0 = qlo; q0 < qhi; q0 += NT) {
+    const int q = q0 + t;
+    float sqv = 0.f;
+    if (q < qhi) {
+      float4 acc = ld4_aux<UPD_AUX_SYS>(upd_rsrc(args.xbuf[0] + base), (size_t)q * 4);
 #pragma unroll
-    for (int r = 1; r < UPD_MAX_RANKS; ++r) {
-      if (r < args.world) {
-        const float4 x = ld4_aux<UPD_AUX_SYS>(upd_rsrc(args.xbuf[r] + base), (size_t)q * 4);
-        acc.x += x.x;
-        acc.y += x.y;
-        acc.z += x.z;
-        acc.w += x.w;
+      for (int r = 1; r < UPD_MAX_RANKS; ++r) {
+        if (r < args.world) {
+          const float4 x = ld4_aux<UPD_AUX_SYS>(upd_rsrc(args.xbuf[r] + base), (size_t)q * 4);
+          acc.x += x.x;
+          acc.y += x.y;
+          acc.z += x.z;
+          acc.w += x.w;
+        }
       }
+      st4_sc1(rs_red, (size_t)q * 4, acc);
+      sqv = q < Qtot - 1 ? upd_sq4(acc) : 0.f;
     }
-    st4_sc1(rs_red, (size_t)q * 4, acc);
+    if (pieces) upd_piece(pieces, sqv, q, q < qhi && q < Qtot - 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1612,7 +1630,7 @@ __device__ bool upd_dp_union_slice(const UpdArgs& args, __amdgpu_buffer_rsrc_t r
 // i.e. finished reading this one.
 __device__ bool upd_dp_union_slice_push(const UpdArgs& args, __amdgpu_buffer_rsrc_t rs_red, int Qtot,
                                         int g, unsigned long long gstep, int par, int* s_abort,
-                                        int qlo, int qhi) {
+                                        int qlo, int qhi, float* pieces = nullptr) {
   const int t = threadIdx.x, NT = blockDim.x;
   const unsigned long long want = gstep + 1ull;
   if (t == 0) {
@@ -1660,19 +1678,25 @@ __device__ bool upd_dp_union_slice_push(const UpdArgs& args, __amdgpu_buffer_rsr
   if (*s_abort) return false;
   const __amdgpu_buffer_rsrc_t rs_rx = upd_rsrc(args.xbuf_self + args.xpush_off +
                                                 (size_t)par * UPD_MAX_RANKS * Qtot * 4);
-  for (int q = qlo + t; q < qhi; q += NT) {
-    float4 acc = ld4_aux<UPD_AUX_SYS>(rs_rx, (size_t)q * 4);
+  for (int q0 = qlo; q0 < qhi; q0 += NT) {
+    const int q = q0 + t;
+    float sqv = 0.f;
+    if (q < qhi) {
+      float4 acc = ld4_aux<UPD_AUX_SYS>(rs_rx, (size_t)q * 4);
 #pragma unroll
-    for (int r = 1; r < UPD_MAX_RANKS; ++r) {
-      if (r < args.world) {
-        const float4 x = ld4_aux<UPD_AUX_SYS>(rs_rx, ((size_t)r * Qtot + q) * 4);
-        acc.x += x.x;
-        acc.y += x.y;
-        acc.z += x.z;
-        acc.w += x.w;
+      for (int r = 1; r < UPD_MAX_RANKS; ++r) {
+        if (r < args.world) {
+          const float4 x = ld4_aux<UPD_AUX_SYS>(rs_rx, ((size_t)r * Qtot + q) * 4);
+          acc.x += x.x;
+          acc.y += x.y;
+          acc.z += x.z;
+          acc.w += x.w;
+        }
       }
+      st4_sc1(rs_red, (size_t)q * 4, acc);
+      sqv = q < Qtot - 1 ? upd_sq4(acc) : 0.f;
     }
-    st4_sc1(rs_red, (size_t)q * 4, acc);
+    if (pieces) upd_piece(pieces, sqv, q, q < qhi && q < Qtot - 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -2478,14 +2502,18 @@ bool upd_split_own(const UpdNet& n, int G, int NT) {
   auto start = [&](int g) {
     const int64_t u = U * g / G;
     const int64_t q = u <= 2 * (int64_t)QT ? (u + 1) / 2 : u - QT;
-    return (int)(q < Qp + 1 ? q : Qp + 1);
+    return q < Qp + 1 ? (int)(q / 4) * 4 : Qp + 1;   // spl_slice_start: SPL_CQ-aligned starts
   };
   for (int g = 0; g < G; ++g)
     if (2 * (start(g + 1) - start(g)) > NT) return false;
   return true;
 }
 // Phase-B helper workgroups of the single-GPU split form (spl_helper): PRL_UPD_SPL_HELP = their
-// number (0 = none), by default every CU the G tile workgroups leave free (capped at 256 owners).
+// number, at most the CUs the G tile workgroups leave free (capped at 256 owners).  Default 0:
+// measured slower (mb 512, same box: 12.74 us per step without helpers, 13.77 with 64, 14.88
+// with 192) — their polls of counter A during the tiles and of B during the slice loads slow
+// both hand-offs (wait A 1.40 -> 2.31 us, slice reduce 2.08 -> 2.71) more than the smaller
+// slices save.
 int upd_split_helpers(int G) {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -2493,7 +2521,7 @@ int upd_split_helpers(int G) {
     return 0;
   const int room = std::max(0, std::min(cus, 256) - G);
   const char* e = getenv("PRL_UPD_SPL_HELP");
-  return e ? std::min(room, std::max(0, atoi(e))) : room;
+  return e ? std::min(room, std::max(0, atoi(e))) : 0;
 }
 bool upd_split_host(const UpdNet& n, int Gt, int R, bool tp) {
   if (tp || !g_split || upd_force_generic() || !upd_is_cartpole(n) || R != UPD_RT) return false;
@@ -2709,6 +2737,8 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     args.spl_poll = (pp && pp[0] == '1') ? 1 : 0;
     const char* pk = getenv("PRL_UPD_SPL_PK");
     args.spl_pk = (pk && pk[0] == '1') ? 1 : 0;
+    const char* pc = getenv("PRL_UPD_SPL_PIECES");
+    args.spl_pieces = (pc && pc[0] == '0') ? 0 : 1;
   }
   args.tp_m0 = ws.mv;
   args.tp_v0 = ws.mv + L4;

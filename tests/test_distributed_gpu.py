@@ -316,9 +316,14 @@ def _config_worker(rank, world, port, cfg, out_dir):
         sd = {kk: v.cpu().numpy() for kk, v in p.policy.state_dict().items()}
         if cfg["rnd"]:
             sd.update({"rnd." + kk: v.cpu().numpy() for kk, v in p.rnd.state_dict().items()})
+        import prl_native
+        plan = prl_native.ppo_update_last_plan()
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **sd, _n=np.int64(n), _head=head,
                  _key=np.uint64(a.sample_seed), _loss=np.float32(p.last_loss.item()),
-                 _path=np.array(p.last_update_path))
+                 _path=np.array(p.last_update_path), _split=np.int32(plan["split"]),
+                 _grid=np.int32(plan["grid"]))
+        if getattr(p, "_engine", None) is not None:
+            p._engine.close()
     finally:
         torch.distributed.destroy_process_group()
 
@@ -347,6 +352,65 @@ def test_two_ranks_at_config_per_rank_shape(tmp_path, name, cfg):
         if not key.startswith("_"):
             np.testing.assert_array_equal(outs[0][key], outs[1][key], err_msg=key)
     assert all(np.isfinite(o["_loss"]) for o in outs)   # each rank reports its own rows
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name,cfg", [("c4", C4), ("c5", C5)])
+def test_eight_ranks_at_config_per_rank_shape(tmp_path, name, cfg):
+    """The WHOLE C4 (8 x 65,536 CartPole envs) and C5 (8 x 16,384 synthetic envs + RND)
+    workloads as 8 data-parallel ranks sharing cuda:0 (the 8-GPU node's rank layout rehearsed on
+    one GPU; gloo for the host exchange): independent rollouts, one learn() each, the assertions
+    of test_two_ranks_at_config_per_rank_shape.  C4 runs the data-parallel persistent engine;
+    8 ranks x 64 split workgroups exceed one GPU's CUs, so the ranks' co-residency vote
+    (PPO/engine.py dp_slices) picks the 8-wave kernel (8 x 32 workgroups) — on a node each rank
+    has a GPU of its own and the split kernel runs.  C5: the wide step + the RND predictor's
+    all-reduced update.  All 8 ranks end bit-identical."""
+    import random
+    port = 28800 + random.randint(0, 150)
+    world = 8
+    mp.spawn(_config_worker, args=(world, port, cfg, str(tmp_path)), nprocs=world, join=True)
+    outs = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(world)]
+    assert len({int(o["_key"]) for o in outs}) == world                # rank-mixed sampling keys
+    for r in range(1, world):
+        assert not np.array_equal(outs[0]["_head"], outs[r]["_head"])  # different rollouts
+    assert min(int(o["_n"]) for o in outs) >= cfg["E"]                 # >= one step per env
+    if name == "c4":
+        assert all(str(o["_path"]) == "fused-dp-persistent" for o in outs)
+        assert all(int(o["_split"]) == 0 and int(o["_grid"]) == 32 for o in outs)   # 8 x 32 CUs
+    else:
+        assert all(str(o["_path"]) == "graph" for o in outs)
+    for key in outs[0].files:
+        if not key.startswith("_"):
+            for r in range(1, world):
+                np.testing.assert_array_equal(outs[0][key], outs[r][key], err_msg=f"{key} rank {r}")
+    assert all(np.isfinite(o["_loss"]) for o in outs)
+
+
+@pytest.mark.timeout(300)
+def test_eight_ranks_persistent_dp_engine_push_equals_pull(tmp_path):
+    """8 data-parallel ranks sharing cuda:0 at mb 64 (8 x 8 split workgroups: the head-split
+    kernel fits, so this is the DEFAULT push form of the exchange at the node's rank count):
+    unequal shards (rank 1 one minibatch short), two learn() calls; the push form gives exactly
+    the pull form's bits and all 8 ranks end bit-identical."""
+    import random
+    mb, nb, k, world = 64, 5, 3, 8
+    port = 28500 + random.randint(0, 30)
+    mp.spawn(_dpx_worker, args=(world, port, mb, nb, k, str(tmp_path), "auto", False), nprocs=world,
+             join=True)
+    mp.spawn(_dpx_worker, args=(world, port + 40, mb, nb, k, str(tmp_path), "auto", True),
+             nprocs=world, join=True)
+    pull = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(world)]
+    push = [np.load(os.path.join(tmp_path, f"pushrank{r}.npz")) for r in range(world)]
+    assert int(push[0]["_push"]) == 1 and int(pull[0]["_push"]) == 0
+    assert all(int(o["_split"]) == 1 for o in push + pull)
+    assert all(str(o["_path"]) == "fused-dp-persistent" for o in push + pull)
+    for key in pull[0].files:
+        if key.startswith("_"):
+            continue
+        for r in range(world):
+            np.testing.assert_array_equal(pull[r][key], pull[0][key], err_msg=key)
+            np.testing.assert_array_equal(push[r][key], pull[0][key], err_msg=key)
+    assert float(push[0]["_loss"]) == float(pull[0]["_loss"])
 
 
 def _wide_shard(rank, mb, nb, D=348, A=17):
