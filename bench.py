@@ -240,6 +240,26 @@ def update_pmc_traffic(kern, steps, mb):
                                      f"{at}; scaled to this launch's steps)")
 
 
+def unit_pmc_traffic(pattern, match, unit_key):
+    """HBM bytes per unit (env-step) of a kernel from the newest committed PMC summary matching
+    profiles/<pattern> ({"meta": {unit_key: units per dispatch, ...}, "kernels": [...]}: written
+    by tools/gpu_traffic_pmc.sh + tools/pmc_meta.py, FETCH_SIZE doubled for gfx950).  Returns
+    (bytes per unit, source) or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    if not files:
+        return None, None
+    rec = json.load(open(files[-1]))
+    if not isinstance(rec, dict) or unit_key not in rec.get("meta", {}):
+        return None, None
+    ks = [k for k in rec["kernels"] if match in k["kernel"]]
+    if not ks:
+        return None, None
+    per = (ks[0]["read_bytes_corrected"] + ks[0]["write_bytes"]) / float(rec["meta"][unit_key])
+    at = f", profiled at commit {rec['meta']['commit']}" if rec["meta"].get("commit") else ""
+    return per, f"{os.path.relpath(files[-1], ROOT)} ({per:.1f} B per {unit_key.split('_per_')[0]}{at})"
+
+
 def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
     """K timed AsyncPPO iterations of one configuration (after `warmup` untimed ones) and the
     roofline re-timings of its kernels.  Returns the measured record (whole-job numbers are
@@ -440,10 +460,15 @@ def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
         env_warm, _ = time_kernel(env_launch, cold=False, prep=lambda: env.reset_device(tr.obs[0]))
         bpe = ENV_STEP_BYTES[cfg["env"]]
         ach = bpe * E / (env_cold * 1e-3) / 1e9
+        per_es, env_src = (unit_pmc_traffic("*rollout_step_pmc.json", "rollout_step_kernel",
+                                            "env_steps_per_dispatch")
+                           if cfg["env"] == "CartPole-v1" else (None, None))
         roofline_env = {"kernel": "prl_rollout_step: rollout_step_kernel (fused env step + "
                                   "action sampling + trajectory append, thread per env)",
                         "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                        "traffic": None if per_es is None else round(per_es * E),
+                        "traffic_source": env_src,
                         "avg_launch_us": round(env_cold * 1e3, 2),
                         "cache": "cold (512 MiB read-only flush)",
                         "warm_launch_us": round(env_warm * 1e3, 2),
@@ -474,11 +499,15 @@ def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
             n_es = int(tr.ep_len.sum().item())
             ms_r = r0.elapsed_time(r1)
             ach = 8960.0 * n_es / (ms_r * 1e-3) / 1e12
+            per_es, cpr_src = unit_pmc_traffic("*cp_rollout_pmc.json", "cp_rollout_kernel",
+                                               "env_steps_per_dispatch")
             roofline_rollout = {"kernel": "prl_cartpole_rollout: cp_rollout_kernel (the whole "
                                           "rollout in one launch, thread per env)",
                                 "bound": "valu", "achieved": round(ach, 2),
                                 "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                "frac": round(ach / F32_PEAK_TFLOPS, 4), "traffic": None,
+                                "frac": round(ach / F32_PEAK_TFLOPS, 4),
+                                "traffic": None if per_es is None else round(per_es * n_es),
+                                "traffic_source": cpr_src,
                                 "launch_ms": round(ms_r, 3), "env_steps": n_es,
                                 "vector_steps": k_last + 1,
                                 "env_steps_per_s": round(n_es / (ms_r * 1e-3), 1),
