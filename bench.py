@@ -257,7 +257,7 @@ def unit_pmc_traffic(pattern, match, unit_key):
         return None, None
     per = (ks[0]["read_bytes_corrected"] + ks[0]["write_bytes"]) / float(rec["meta"][unit_key])
     at = f", profiled at commit {rec['meta']['commit']}" if rec["meta"].get("commit") else ""
-    return per, f"{os.path.relpath(files[-1], ROOT)} ({per:.1f} B per {unit_key.split('_per_')[0]}{at})"
+    return per, f"{os.path.relpath(files[-1], ROOT)} ({per:.1f} B per {unit_key.split('_per_')[0].rstrip('s').replace('_', '-')}{at})"
 
 
 def run_config(args, cfg, steps, warmup, world, rank, env_scale, dump_gae=None):
