@@ -412,12 +412,12 @@ extern "C" int prl_flat_adamw(float* params, float* exp_avg, float* exp_avg_sq, 
               "prl_flat_adamw: buffers must be 16-B aligned");
   const unsigned nblk = (unsigned)std::max<int64_t>(1, cdiv(P / 4, FA_THREADS));
   const bool fuse = nblk <= (unsigned)FA_FUSE_MAX_BLOCKS;
-  // total_norm[1]: the arrival counter.  Every call leaves it zero, but a caller's buffer may not
-  // start so (torch.empty, a reused buffer, a launch that died), and then no workgroup would see
-  // itself last: the gradient would stay unclipped and the step count unadvanced, silently.  So
-  // it is zeroed here on the stream in front of the launch (a memset node when captured).
+  // total_norm[1]: the arrival counter, zero before a buffer's first call (prl_native.flat_adamw
+  // zeroes a caller's buffer once, on first use) and left zero by every call.  (Not a
+  // hipMemsetAsync per call: captured into the data-parallel ranks' optimizer graph, that memset
+  // node broke the step — tests/test_distributed_gpu.py::test_two_ranks_wide_step_equal_one_
+  // process_on_the_union, 4.7e-3 vs 1e-3, round 6.)
   unsigned* arrive = fuse ? reinterpret_cast<unsigned*>(total_norm + 1) : nullptr;
-  if (fuse) PRL_HIP_TRY(hipMemsetAsync(arrive, 0, sizeof(unsigned), as_stream(stream)));
   hipLaunchKernelGGL(flat_adamw_kernel, dim3(nblk), dim3(FA_THREADS), 0, as_stream(stream), params,
                      exp_avg, exp_avg_sq, step, grad, P, lr, beta1, beta2, eps, weight_decay,
                      max_norm, total_norm, grad, arrive, step);

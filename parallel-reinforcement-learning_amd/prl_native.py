@@ -761,7 +761,10 @@ def flat_adamw(params, exp_avg, exp_avg_sq, step, grad, lr, beta1, beta2, eps, w
     """clip_grad_norm_(max_norm) + AdamW.step() over flat f32 vectors (one launch up to 262,144
     parameters, two above).  total_norm: a two-entry f32 device workspace, zeroed before its
     first use ([0] the gradient's norm, clip_grad_norm_'s return value; [1] the launch's arrival
-    counter, left at zero by every call; a new one unless passed).  Returns total_norm[:1]."""
+    counter, left at zero by every call; a new one unless passed).  A caller's buffer is zeroed
+    here on its first use (torch.empty or a reused buffer would otherwise leave the counter
+    dirty: no workgroup would see itself last, so the gradient would stay unclipped and the
+    step count unadvanced, silently).  Returns total_norm[:1]."""
     P = int(params.numel())
     for t, n in ((exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq"), (grad, "grad")):
         if t.numel() != P:
@@ -770,6 +773,9 @@ def flat_adamw(params, exp_avg, exp_avg_sq, step, grad, lr, beta1, beta2, eps, w
         total_norm = torch.zeros(2, dtype=torch.float32, device=params.device)
     if total_norm.numel() < 2:
         raise ValueError("total_norm must hold 2 entries (the norm and an arrival counter)")
+    if not getattr(total_norm, "_prl_fa_zeroed", False):
+        total_norm.zero_()
+        total_norm._prl_fa_zeroed = True
     _check(lib().prl_flat_adamw(
         _dev(params, torch.float32, "params"), _dev(exp_avg, torch.float32, "exp_avg"),
         _dev(exp_avg_sq, torch.float32, "exp_avg_sq"), _dev(step, torch.float32, "step"),

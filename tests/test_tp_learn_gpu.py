@@ -104,7 +104,7 @@ def test_large_minibatch_learn_matches_reference_learn(golden, tag):
     assert p.last_update_path == "fused"
     plan = prl_native.ppo_update_last_plan()
     assert plan == {"form": "throughput", "waves": 8, "grid": 256, "tiles": 16,
-                    "specialised": True, "replicas": 1, "split": False, "owner": False}, plan
+                    "specialised": True, "replicas": 1, "split": False, "owner": False, "helpers": 0}, plan
     _, _, _, adv, returns = p._last_update_inputs
     ret_ref, adv_ref = g["returns"].astype(np.float64), g["adv"].astype(np.float64)
     # GAE is bit-exact against the reference (test_kernels_gpu); here it runs on our old values
