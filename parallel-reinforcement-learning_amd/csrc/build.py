@@ -52,7 +52,8 @@ def _compile(src, force, sid):
         extra = [f'-DPRL_SOURCE_ID="{sid}"']
     if not force and _mtime(obj) >= max(_mtime(d) for d in deps):
         return obj, None
-    cmd = [HIPCC, *CFLAGS, *extra, "-c", os.path.join(HERE, src), "-o", obj]
+    cmd = [HIPCC, *CFLAGS, *extra, *os.environ.get("PRL_EXTRA_CFLAGS", "").split(), "-c",
+           os.path.join(HERE, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"{' '.join(cmd)}\n{r.stdout}\n{r.stderr}"

@@ -500,6 +500,19 @@ __device__ inline void spl_slice_reduce(__amdgpu_buffer_rsrc_t rs_part, __amdgpu
   sub.mark(1);   // slice combined, its stores issued
 }
 
+// The split form's counter waits (PRL_UPD_SPL_POLL, A/B): 0 = one poll in flight, s_sleep 1
+// between polls (default); 1 = four polls in flight; 2 / 3 / 4 = one in flight, s_sleep 2 / 4 / 8
+// (fewer polls against the counter lines while the other workgroups' arrivals land there)
+__device__ inline bool spl_wait(const UpdArgs& args, int base, unsigned target) {
+  switch (args.spl_poll) {
+    case 1: return upd_wait_sharded_pipe(args.ctr, base, target);
+    case 2: return upd_wait_sharded<2>(args.ctr, base, target);
+    case 3: return upd_wait_sharded<4>(args.ctr, base, target);
+    case 4: return upd_wait_sharded<8>(args.ctr, base, target);
+    default: return upd_wait_sharded<1>(args.ctr, base, target);
+  }
+}
+
 // Phase-B helpers: workgroups G .. Gs - 1 of a single-GPU split launch (PRL_UPD_SPL_HELP; by
 // default the CUs the 2 Gt tile workgroups leave idle).  They hold no parameters and run no tile:
 // each step they wait for counter A, reduce their slice, and arrive at counter B.  The slices are
@@ -750,8 +763,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     if (t < 64) {
       if (skew && t == 0) spl_prof_stamp(args, 0, g);
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_A, g);
-      const bool ok = args.spl_poll ? upd_wait_sharded_pipe(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1))
-                                    : upd_wait_sharded(args.ctr, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));
+      const bool ok = spl_wait(args, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));
       if (t == 0) *s_abort = ok ? 0 : 1;
     } else if (t == 64) {
       const double tstep = (double)step0 + (double)(s + 1);
@@ -804,8 +816,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     if (t < 64) {
       if (args.profile && (s & 15) == 8 && t == 0) spl_prof_stamp(args, 1, g);
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_B, g);
-      const bool ok = args.spl_poll ? upd_wait_sharded_pipe(args.ctr, UPD_CTR_B, (unsigned)Gs * (unsigned)(s + 1))
-                                    : upd_wait_sharded(args.ctr, UPD_CTR_B, (unsigned)Gs * (unsigned)(s + 1));
+      const bool ok = spl_wait(args, UPD_CTR_B, (unsigned)Gs * (unsigned)(s + 1));
       if (t == 0) *s_abort = ok ? 0 : 1;
     }
     __syncthreads();

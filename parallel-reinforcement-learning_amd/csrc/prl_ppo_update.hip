@@ -237,7 +237,11 @@ __device__ inline unsigned ld_sc1u(const unsigned* p) {
 // 8-way sharded arrival counters (shard k at word 32 (1 + k) of its block, one 128-B line each):
 // an arrival adds to shard g & 7, so at most G / 8 atomics meet on one line; a whole wave polls,
 // lanes 0..7 one shard each, and the DPP sum over the 8 lanes is the arrival count.
-constexpr int UPD_SHARDS = 8;
+#ifndef PRL_UPD_SHARDS
+#define PRL_UPD_SHARDS 8   // (8 or 16; -DPRL_UPD_SHARDS=16 builds the 16-line form for A/Bs)
+#endif
+constexpr int UPD_SHARDS = PRL_UPD_SHARDS;
+static_assert(UPD_SHARDS == 8 || UPD_SHARDS == 16, "8 or 16 counter shards");
 constexpr int UPD_CTR_A = 32;                              // first shard word of counter A
 constexpr int UPD_CTR_B = UPD_CTR_A + 32 * UPD_SHARDS;     // ... of counter B
 constexpr int UPD_CTR_C = UPD_CTR_B + 32 * UPD_SHARDS;     // ... of counter C (split form, OWN)
@@ -246,15 +250,17 @@ __device__ inline void upd_arrive(unsigned* ctr, int base, int g) {
   __hip_atomic_fetch_add(upd_g(ctr + base + 32 * (g & (UPD_SHARDS - 1))), 1u, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ inline unsigned upd_isum8(unsigned v) {
+__device__ inline unsigned upd_isum8(unsigned v) {   // (lanes 0 .. UPD_SHARDS - 1 into lane 0)
   v += (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
   v += (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
   v += (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+  if constexpr (UPD_SHARDS == 16) v += (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);
   return v;
 }
 // one whole wave: wait until the shards of counter `base` sum to >= target; false on timeout /
 // abort (same abort / status / sticky words as upd_wait).  Lane 8 loads the abort word in the
 // same round as lanes 0-7 load the shards: one memory round trip per poll, not two in series.
+template <int SL = 1>   // s_sleep between polls (64 x SL cycles)
 __device__ inline bool upd_wait_sharded(unsigned* ctr, int base, unsigned target) {
   const int l = threadIdx.x & 63;
   for (unsigned spins = 0;; ++spins) {
@@ -271,7 +277,7 @@ __device__ inline bool upd_wait_sharded(unsigned* ctr, int base, unsigned target
       }
       return false;
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(SL);
   }
 }
 
@@ -2734,7 +2740,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     const char* d = getenv("PRL_UPD_SPL_DIRECT");
     args.spl_direct = (d && d[0] == '1') ? 1 : 0;
     const char* pp = getenv("PRL_UPD_SPL_POLL");
-    args.spl_poll = (pp && pp[0] == '1') ? 1 : 0;
+    args.spl_poll = pp ? std::max(0, std::min(4, atoi(pp))) : 0;
     const char* pk = getenv("PRL_UPD_SPL_PK");
     args.spl_pk = (pk && pk[0] == '1') ? 1 : 0;
     const char* pc = getenv("PRL_UPD_SPL_PIECES");
