@@ -285,15 +285,16 @@ __device__ __forceinline__ void spl_tile(const UpdNet& n, const UpdArgs& args, i
 // Phase B's slices, balanced by loads: a trunk or loss quad sums 2 Gt partials, a head quad Gt,
 // and phase B's time per workgroup follows the bytes it loads (~20 KB per us per CU, measured:
 // equal-quad slices left the trunk's owners loading twice the others' bytes, 3.7 vs 2.0 us).
-// So quad q weighs 2 for q < QT and q == Qp, else 1: weighted position w(q) = q + min(q, QT),
-// U = Qp + QT + 2 units, and slice g starts at the first quad with w(q) >= U g / G.
-// Starts are rounded down to a multiple of SPL_CQ (a norm piece's chunk, below: no chunk straddles
-// two slices; upd_split_own on the host cuts the same way).
-__device__ inline int spl_slice_start(int g, int G, int Qp, int QT) {
+// So a head quad weighs 4 units and a trunk / loss quad tw4 (8 = twice: the default;
+// PRL_UPD_SPL_TW4 for A/Bs): weighted position w(q) = 4 q + (tw4 - 4) min(q, QT), U = 4 (Qp - QT)
+// + tw4 (QT + 1) units, and slice g starts at the first quad with w(q) >= U g / G, rounded down
+// to a multiple of SPL_CQ (a norm piece's chunk, below: no chunk straddles two slices).  The
+// host's slice-owner check (upd_split_own) cuts the same way.
+__host__ __device__ inline int spl_slice_start(int g, int G, int Qp, int QT, int tw4 = 8) {
   const int Qtot = Qp + 1;
-  const int64_t U = (int64_t)Qp + QT + 2;
-  const int64_t u = U * g / G;
-  const int64_t q = u <= 2 * (int64_t)QT ? (u + 1) / 2 : u - QT;
+  const int64_t U = 4 * (int64_t)(Qp - QT) + (int64_t)tw4 * (QT + 1);
+  const int64_t u = U * g / G, ut = (int64_t)tw4 * QT;
+  const int64_t q = u <= ut ? (u + tw4 - 1) / tw4 : QT + (u - ut + 3) / 4;
   return q < Qtot ? (int)(q / SPL_CQ) * SPL_CQ : Qtot;
 }
 
@@ -401,10 +402,10 @@ struct SplSlice {
   int qi, sb;   // this thread's quad (qlo + qi) and its first partial
 };
 template <int NT>
-__device__ inline SplSlice spl_slice_plan(int g, int G, int Qp, int QT, int Gt, int fill) {
+__device__ inline SplSlice spl_slice_plan(int g, int G, int Qp, int QT, int Gt, int fill, int tw4 = 8) {
   SplSlice p;
-  p.qlo = spl_slice_start(g, G, Qp, QT);
-  p.qhi = spl_slice_start(g + 1, G, Qp, QT);
+  p.qlo = spl_slice_start(g, G, Qp, QT, tw4);
+  p.qhi = spl_slice_start(g + 1, G, Qp, QT, tw4);
   p.nq = p.qhi - p.qlo;
   // spl threads per quad, each summing every spl-th partial: a power of two (fill 0), or as
   // many as the NT threads allow (fill 1: more loads in flight; the slice loads are latency-bound)
@@ -524,7 +525,7 @@ template <int NT>
 __device__ __forceinline__ void spl_helper(const UpdArgs& args, int g, int Qtot, int Qp, int QT, float* scratch,
                                         int* s_abort) {
   const int t = threadIdx.x;
-  const SplSlice slc = spl_slice_plan<NT>(g, args.Gs, Qp, QT, args.Gt, args.spl_fill);
+  const SplSlice slc = spl_slice_plan<NT>(g, args.Gs, Qp, QT, args.Gt, args.spl_fill, args.spl_tw4);
   const __amdgpu_buffer_rsrc_t rs_part = upd_rsrc(args.part), rs_part2 = upd_rsrc(args.part2),
                                rs_red = upd_rsrc(args.red);
   const UpdSub none{nullptr, nullptr};
@@ -598,7 +599,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   for (int q = t; q < Qp; q += SPL_NT)
     *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(args.params + 4 * q);
   // OWN: this thread's slice quad (see slc below) and its moments
-  const SplSlice slc0 = spl_slice_plan<SPL_NT>(g, Gs, Qp, QT, Gt, args.spl_fill);
+  const SplSlice slc0 = spl_slice_plan<SPL_NT>(g, Gs, Qp, QT, Gt, args.spl_fill, args.spl_tw4);
   const int oq = (OWN && t < slc0.nq && slc0.qlo + t < Qp) ? slc0.qlo + t : -1;
   if constexpr (OWN) {
     mreg[0] = oq >= 0 ? *reinterpret_cast<const float4*>(args.exp_avg + 4 * oq) : float4{0.f, 0.f, 0.f, 0.f};
@@ -614,6 +615,11 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   }
   const float step0 = args.adam_step[0];
   if (t < 24) reinterpret_cast<unsigned long long*>(hdr + 16)[t] = 0ull;
+  if (t == 0) {   // 1 / B of a full and of the last minibatch (read per step from LDS, below)
+    const int64_t blast = std::min<int64_t>(args.mb, args.N - (int64_t)(args.nb - 1) * args.mb);
+    hdr[117] = 1.0f / (float)args.mb;
+    hdr[118] = 1.0f / (float)std::max<int64_t>(blast, 1);
+  }
   for (int k = t; k < Lp + 4; k += SPL_NT) Ga[k] = 0.0f;   // entries no tile writes stay 0 for good
   __syncthreads();
 
@@ -723,9 +729,14 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   for (int s = 0; s < args.total_steps; ++s) {
     const int jn = j == nb - 1 ? 0 : j + 1;
     const int Bn = B_of(jn);
-    const float invB = DP ? args.inv_count[j] : (Bj == args.mb ? invB_full : invB_last);
+    // (1 / B from LDS: as a loop-invariant register value the compiler re-derived the division
+    // in the loop top, on every step's critical path)
+    const float invB = DP ? args.inv_count[j] : hdr[Bj == args.mb ? 117 : 118];
     const int myrows = rows_of(Bj);
     // ---- phase A: this role's share of tile group gt's gradient ------------------------------
+    // (the next step's prefetch stays here: issued during wait A instead, by the waves idle
+    // while wave 0 polls, it made the tile 0.13 us shorter and wait A 0.35 us longer —
+    // profiles/r06_prefetch_in_waitA_ab.txt)
     if (myrows > 0) {
       const UpdIn<KSM> cur = upd_in_real(nin);
       // prefetch the next step's tile under this one and the hand-offs
@@ -765,12 +776,14 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       if (t == 0) upd_arrive(args.ctr, UPD_CTR_A, g);
       const bool ok = spl_wait(args, UPD_CTR_A, (unsigned)G * (unsigned)(s + 1));
       if (t == 0) *s_abort = ok ? 0 : 1;
-    } else if (t == 64) {
-      const double tstep = (double)step0 + (double)(s + 1);
-      const double bc1 = 1.0 - pow((double)args.beta1, tstep);
-      const double bc2 = 1.0 - pow((double)args.beta2, tstep);
-      s_adam[0] = (float)((double)args.lr / bc1);
-      s_adam[1] = (float)(1.0 / sqrt(bc2));
+    } else {
+      if (t == 64) {
+        const double tstep = (double)step0 + (double)(s + 1);
+        const double bc1 = 1.0 - pow((double)args.beta1, tstep);
+        const double bc2 = 1.0 - pow((double)args.beta2, tstep);
+        s_adam[0] = (float)((double)args.lr / bc1);
+        s_adam[1] = (float)(1.0 / sqrt(bc2));
+      }
     }
     __syncthreads();
     if (*s_abort) return;

@@ -149,6 +149,7 @@ struct UpdArgs {
   int spl_poll;     // head-split form: counter waits with four polls in flight (PRL_UPD_SPL_POLL)
   int spl_pk;       // head-split form: AdamW two elements per packed-f32 instruction (PRL_UPD_SPL_PK)
   int spl_pieces;   // head-split form: the clip norm from per-chunk pieces (PRL_UPD_SPL_PIECES)
+  int spl_tw4;      // head-split form: 4 x a trunk / loss quad's weight in phase B's slicing (PRL_UPD_SPL_TW4)
   float* red;       // [Qtot * 4]
   float* sq;        // [NW G] per-wave squared-norm pieces of the slices
   unsigned* ctr;    // [0] arrivals A, [1] arrivals B, [2] abort, [3] status (zeroed per launch),
@@ -2504,14 +2505,8 @@ bool upd_split_own(const UpdNet& n, int G, int NT) {
   const char* e = getenv("PRL_UPD_SPL_OWN");
   if (!(e && e[0] == '1')) return false;
   const int Qp = n.Lp / 4, QT = n.w1[0].lds / 4;
-  const int64_t U = (int64_t)Qp + QT + 2;
-  auto start = [&](int g) {
-    const int64_t u = U * g / G;
-    const int64_t q = u <= 2 * (int64_t)QT ? (u + 1) / 2 : u - QT;
-    return q < Qp + 1 ? (int)(q / 4) * 4 : Qp + 1;   // spl_slice_start: SPL_CQ-aligned starts
-  };
-  for (int g = 0; g < G; ++g)
-    if (2 * (start(g + 1) - start(g)) > NT) return false;
+  for (int g = 0; g < G; ++g)   // (the default trunk weight: the owner form ignores PRL_UPD_SPL_TW4)
+    if (2 * (spl_slice_start(g + 1, G, Qp, QT) - spl_slice_start(g, G, Qp, QT)) > NT) return false;
   return true;
 }
 // Phase-B helper workgroups of the single-GPU split form (spl_helper): PRL_UPD_SPL_HELP = their
@@ -2743,6 +2738,8 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
     args.spl_poll = pp ? std::max(0, std::min(4, atoi(pp))) : 0;
     const char* pk = getenv("PRL_UPD_SPL_PK");
     args.spl_pk = (pk && pk[0] == '1') ? 1 : 0;
+    const char* tw = getenv("PRL_UPD_SPL_TW4");
+    args.spl_tw4 = tw ? std::max(4, std::min(16, atoi(tw))) : 8;
     const char* pc = getenv("PRL_UPD_SPL_PIECES");
     args.spl_pieces = (pc && pc[0] == '0') ? 0 : 1;
   }
@@ -2771,6 +2768,7 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
                                   : own ? reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, false, 4, true>)
                                         : reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, false, 4>));
     g_last_own = own ? 1 : 0;
+    if (own) args.spl_tw4 = 8;   // upd_split_own checked the default slicing
     plan = UpdPlan{k, tw, 1};
   }
   // replicated tiles: the latency form on one GPU only; the split form: two roles per tile group

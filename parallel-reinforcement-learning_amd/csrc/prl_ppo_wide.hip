@@ -1178,6 +1178,7 @@ struct WrArgs {
   const float* scales;
   int64_t N, mb;
   float vf_coef, ent_coef;
+  int q0;   // first quad folded (the split form: past W0's block, which dW0's own fold writes)
 };
 template <int S>
 __device__ __forceinline__ void ppo_wide_reduce_body(const WrArgs& r, int blk) {
@@ -1187,7 +1188,7 @@ __device__ __forceinline__ void ppo_wide_reduce_body(const WrArgs& r, int blk) {
   float* __restrict__ grad = r.grad;
   __shared__ double4 acc_s[S][QU];
   const int t = threadIdx.x, slot = t / QU, qi = t % QU;
-  const int quad = blk * QU + qi;
+  const int quad = r.q0 + blk * QU + qi;
   const int stride = Pq + 4;
   const int nq = stride / 4;
   double4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -1516,9 +1517,13 @@ extern "C" int prl_ppo_wide_grad_prof(const float* params, int32_t D, int32_t A,
 #undef WD_LAUNCH
   PRL_LAUNCH_CHECK("ppo_wide_grad");
   const int nq = (n.Pq + 4) / 4;
-  const WrArgs fold{part, G, n.P, n.Pq, grad, loss_out, cursor, scales, N, mini_batch, vf_coef, ent_coef};
+  WrArgs fold{part, G, n.P, n.Pq, grad, loss_out, cursor, scales, N, mini_batch, vf_coef, ent_coef, 0};
   if (split) {   // dW0 = dH0^T X beside the partials' fold, then dW0's fold into grad's W0 block
-    const dim3 grid2((unsigned)(G2 + wr_blocks<4>(nq)));
+    // The tile kernel leaves its partials' W0 block unwritten in the split form (dW0 comes from
+    // part2): the fold starts past it instead of reading 256 x 64 D unwritten floats and writing
+    // grad's W0 block twice (C5: 22.8 of the fold's 38 MB per step)
+    if (n.w0 == 0) fold.q0 = (WD_H * n.D) / 4;
+    const dim3 grid2((unsigned)(G2 + wr_blocks<4>(nq - fold.q0)));
     if (KSM == 32)
       hipLaunchKernelGGL(ppo_wide_dw0_kernel<32>, grid2, dim3(WD_THREADS), 0, st, a, part2, G2, fold);
     else if (wd_spec(n))
