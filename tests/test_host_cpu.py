@@ -221,6 +221,31 @@ def test_kernel_bench_tool_imports():
     assert mod.CARTPOLE_STEP_BYTES == 111 and mod.GAE_BYTES_PER_TRANSITION == 20
 
 
+def test_bench_traffic_comes_from_recorded_workloads():
+    """bench.py's roofline `traffic` fields read committed PMC summaries (profiles/*_pmc.json):
+    scaled per unit from the workload the summary records, the update engine's only at the
+    minibatch size it was profiled at (None otherwise), and labelled with where it came from."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    per, src = bench.update_pmc_traffic("ppo_update_split_kernel", 1000, 512)
+    assert per is not None and 2e9 < per < 5e9 and "per optimizer step at mb 512" in src
+    assert bench.update_pmc_traffic("ppo_update_split_kernel", 1000, 65536) == (None, None)
+    assert bench.update_pmc_traffic("ppo_update_kernel", 1000, 512) == (None, None)
+    env, src = bench.unit_pmc_traffic("*rollout_step_pmc.json", "rollout_step_kernel",
+                                      "env_steps_per_dispatch")
+    assert 100 < env < 130 and "B per env-step" in src      # 111 B algorithmic
+    cpr, _ = bench.unit_pmc_traffic("*cp_rollout_pmc.json", "cp_rollout_kernel", "env_steps_per_dispatch")
+    assert 20 < cpr < 111                                   # the one-launch rollout keeps state in registers
+    assert bench.unit_pmc_traffic("*no_such_pmc.json", "x", "y") == (None, None)
+    wide, _ = bench.wide_pmc_traffic()
+    assert 2e8 < wide < 4e8
+    gae, _ = bench.pmc_traffic(1 << 20)
+    assert 20 * (1 << 20) <= gae < 24 * (1 << 20)           # 20 B per transition algorithmic
+
+
 @pytest.mark.parametrize("n", [3 * 64, 3 * 64 + 5])
 def test_split_k_linear_function_vs_autograd(monkeypatch, n):
     """PPO.layers._SplitKLinear (the large-batch Linear's split-K weight / bias gradient) is plain
