@@ -547,6 +547,71 @@ __device__ __forceinline__ void spl_helper(const UpdArgs& args, int g, int Qtot,
   }
 }
 
+// Wave-block AdamW (WB: the 4-wave workgroup-AdamW form).  Before barrier #0 a tile's wave b
+// reads only the parameters of its own channel block — W0 rows 16b .. 16b + 15, γ0 / β0 block b,
+// the head's W1 rows 16b .. 16b + 15, γ1 / β1 block b, W2 columns 16b .. 16b + 15 — and every
+// other parameter read comes after barrier #0.  So when wave b's AdamW updates exactly those
+// quads (wave 0 also the head's output biases, read after barrier #1), no workgroup barrier is
+// needed between AdamW and the next step's tile: a wave goes from its last AdamW slot straight
+// into its forward.  List k of (role h, wave b) -> parameter quad (-1 past its end); lane l
+// holds entries l + 64 i (SPL_WBQ slots; the host checks the length).  W1 / W2 padding columns
+// (zero gradient, zero moments: they stay 0) are not listed.
+constexpr int SPL_WBQ = 5;
+__host__ __device__ constexpr int spl_wb_len(const UpdNet& n, int h, int b) {
+  return 4 * n.w0.stride + 8 + 16 * UPD_H / 4 + 8 + 4 * n.out[h] + (b == 0 ? (n.out[h] + 3) / 4 : 0);
+}
+__host__ __device__ __forceinline__ int spl_wb_quad(const UpdNet& n, int h, int b, int k) {
+  const int s0 = 4 * n.w0.stride;   // W0 rows 16b .. 16b + 15: 16 stride floats, contiguous
+  if (k < s0) return (n.w0.lds + 16 * b * n.w0.stride) / 4 + k;
+  k -= s0;
+  if (k < 4) return (n.g0.lds + 16 * b) / 4 + k;
+  k -= 4;
+  if (k < 4) return (n.b0.lds + 16 * b) / 4 + k;
+  k -= 4;
+  const int w1 = h == 0 ? n.w1[0].lds : n.w1[1].lds;   // (two-head nets: h is 0 or 1)
+  if (k < 256) return (w1 + (16 * b + (k >> 4)) * UPD_HS) / 4 + (k & 15);
+  k -= 256;
+  if (k < 4) return ((h == 0 ? n.g1[0].lds : n.g1[1].lds) + 16 * b) / 4 + k;
+  k -= 4;
+  if (k < 4) return ((h == 0 ? n.b1[0].lds : n.b1[1].lds) + 16 * b) / 4 + k;
+  k -= 4;
+  const int no = h == 0 ? n.out[0] : n.out[1];
+  if (k < 4 * no) return ((h == 0 ? n.w2[0].lds : n.w2[1].lds) + (k >> 2) * UPD_HS + 16 * b) / 4 + (k & 3);
+  k -= 4 * no;
+  if (b == 0 && k < (no + 3) / 4) return (h == 0 ? n.b2[0].lds : n.b2[1].lds) / 4 + k;
+  return -1;
+}
+// Host check (once per net shape, prl_ppo_update): role h's four lists cover every quad the
+// role owns (trunk + head h) exactly once, W1 / W2 padding quads aside, within SPL_WBQ slots.
+inline bool spl_wb_check(const UpdNet& n) {
+  if (n.nh != 2) return false;
+  const int Qp = n.Lp / 4, QT = n.w1[0].lds / 4, QH = n.w1[1].lds / 4;
+  for (int h = 0; h < 2; ++h) {
+    std::vector<int> seen(Qp, 0);
+    for (int b = 0; b < 4; ++b) {
+      if (spl_wb_len(n, h, b) > 64 * SPL_WBQ) return false;
+      for (int k = 0; k < 64 * SPL_WBQ; ++k) {
+        const int q = spl_wb_quad(n, h, b, k);
+        if ((q >= 0) != (k < spl_wb_len(n, h, b))) return false;
+        if (q < 0) continue;
+        if (q >= Qp || seen[q]++) return false;
+      }
+    }
+    for (int q = 0; q < Qp; ++q) {
+      const bool owned = h == 0 ? q < QH : (q < QT || q >= QH);
+      // a padding quad: columns 64 .. 67 of a W1 / W2 row (stride UPD_HS = 68)
+      bool pad = false;
+      for (int hh = 0; hh < 2; ++hh) {
+        const int lo = (4 * q - n.w1[hh].lds), lo2 = (4 * q - n.w2[hh].lds);
+        if (lo >= 0 && lo < UPD_H * UPD_HS && lo % UPD_HS == UPD_H) pad = true;
+        if (lo2 >= 0 && lo2 < n.out[hh] * UPD_HS && lo2 % UPD_HS == UPD_H) pad = true;
+      }
+      if (seen[q] != ((owned && !pad) ? 1 : 0)) return false;
+    }
+  }
+  return true;
+}
+
 // NQC = ceil(Qp / 256): quads per thread of phase C's canonical sweep (the moment registers
 // cover the same slots; a slot holds moments only where this role owns the quad).
 // DP: data-parallel ranks (prl_ppo_update_dpx): union-minibatch row weights inv_count[j] and,
@@ -576,7 +641,15 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   auto owned = [&](int q) { return role == 0 ? q < QH : (q < QT || q >= QH); };
   // slot i of this thread: the quad of the canonical sweep (t + NT i) its moments / AdamW cover,
   // where this role owns it (-1: none)
+  // WB: the wave-block lists (spl_wb_quad) instead of the canonical sweep
+  constexpr bool WB = TW == SPL_NW && !OWN;
+  int wq[SPL_WBQ];
+  if constexpr (WB) {
+#pragma unroll
+    for (int i = 0; i < SPL_WBQ; ++i) wq[i] = spl_wb_quad(n, role, t >> 6, (t & 63) + 64 * i);
+  }
   auto slotq = [&](int i) {
+    if constexpr (WB) return wq[i];
     const int o = t + i * SPL_NT;
     return (o < Qp && owned(o)) ? o : -1;
   };
@@ -594,7 +667,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     return;
   }
 
-  constexpr int NMR = OWN ? 1 : NQC;
+  constexpr int NMR = OWN ? 1 : (WB ? SPL_WBQ : NQC);   // moment slots per thread
   float4 mreg[NMR], vreg[NMR];
   for (int q = t; q < Qp; q += SPL_NT)
     *reinterpret_cast<float4*>(W + 4 * q) = *reinterpret_cast<const float4*>(args.params + 4 * q);
@@ -606,7 +679,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     vreg[0] = oq >= 0 ? *reinterpret_cast<const float4*>(args.exp_avg_sq + 4 * oq) : float4{0.f, 0.f, 0.f, 0.f};
   } else {
 #pragma unroll
-    for (int i = 0; i < NQC; ++i) {
+    for (int i = 0; i < NMR; ++i) {
       const int q = slotq(i);
       const bool own = q >= 0;
       mreg[i] = own ? *reinterpret_cast<const float4*>(args.exp_avg + 4 * q) : float4{0.f, 0.f, 0.f, 0.f};
@@ -799,7 +872,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       const int par = (int)(gstep & 1ull);
       spl_slice_reduce<SPL_NT>(rs_part, rs_part2, DP ? upd_rsrc(args.xbuf_self + (size_t)par * Qtot * 4) : rs_red,
                                Qtot, Qp, QT, slc, Gt, scratch, DP, subm, args, par, OWN ? &og : nullptr,
-                               (!DP && !OWN && args.spl_pieces) ? args.sq : nullptr);
+                               (!DP && !OWN && (WB || args.spl_pieces)) ? args.sq : nullptr);
       if constexpr (OWN) {
         // the owner's speculative AdamW (clip coefficient 1) on its quad; the new weights go out
         // in place of the gradient, with this wave's piece of the squared norm
@@ -819,7 +892,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       __syncthreads();
       if (DP) {
         const int qlo = slc.qlo, qhi = slc.qhi;
-        float* const pcs = args.spl_pieces ? args.sq : nullptr;
+        float* const pcs = (WB || args.spl_pieces) ? args.sq : nullptr;
         if (!(args.dp_push ? upd_dp_union_slice_push(args, rs_red, Qtot, g, gstep, par, s_abort, qlo, qhi, pcs)
                            : upd_dp_union_slice(args, rs_red, Qtot, g, G, gstep, par, s_abort, qlo, qhi, pcs)))
           return;
@@ -841,10 +914,10 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       if (t == 0) pts[7] = __builtin_amdgcn_s_memrealtime();
     }
     // ---- phase C: the norm in the canonical order, then AdamW on the owned quads -------------
-    float4 gq[NQC];
+    float4 gq[WB ? SPL_WBQ : NQC];
     float clipc;
     {
-      const bool pcs = !OWN && args.spl_pieces;
+      const bool pcs = WB || (!OWN && args.spl_pieces);   // (WB: always the pieces)
       float tot = 0.f;
       if (pcs) {
         // the norm from the pieces, loaded FIRST: every wave sums all of them itself (lane l:
@@ -858,11 +931,18 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
 #pragma unroll
         for (int c = 0; c < 4; ++c)
           if (256 * c < nch) pc[c] = ld4_sc1_so(rs_sq, 16u * (unsigned)l, 1024u * (unsigned)c);
-        // this role's slots (uniform per workgroup: a slot any of its quads is owned in)
+        if constexpr (WB) {
+          // this wave's block list (past its end: quad 0, unused)
 #pragma unroll
-        for (int i = 0; i < NQC; ++i)
-          if (i * SPL_NT < Qp && (role == 0 ? i * SPL_NT < QH : (i * SPL_NT < QT || (i + 1) * SPL_NT > QH)))
-            gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
+          for (int i = 0; i < SPL_WBQ; ++i)
+            gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)(wq[i] >= 0 ? wq[i] : 0), 0u);
+        } else {
+          // this role's slots (uniform per workgroup: a slot any of its quads is owned in)
+#pragma unroll
+          for (int i = 0; i < NQC; ++i)
+            if (i * SPL_NT < Qp && (role == 0 ? i * SPL_NT < QH : (i * SPL_NT < QT || (i + 1) * SPL_NT > QH)))
+              gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
+        }
         float acc = 0.f;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -873,7 +953,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
         acc = wave_sum_f32_to63(acc);
         tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), 63));
         subm.mark(2);   // thread 0's pieces landed
-      } else {
+      } else if constexpr (!WB) {
 #pragma unroll
         for (int i = 0; i < NQC; ++i)
           if (i * SPL_NT < Qp) gq[i] = ld4_sc1_so(rs_red, 16u * (unsigned)t, 16u * (unsigned)(i * SPL_NT));
@@ -895,7 +975,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
         v = wave_sum_f32_to63(v);
         tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
         subm.mark(2);   // thread 0's weight quads and the pieces landed
-      } else {
+      } else if constexpr (!WB) {
         float acc = 0.f;
 #pragma unroll
         for (int i = 0; i < NQC; ++i)
@@ -958,7 +1038,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       const float b2 = (float)args.beta2;
       const float omb1 = (float)(1.0 - (double)args.beta1), omb2 = (float)(1.0 - (double)args.beta2);
 #pragma unroll
-      for (int i = 0; i < NQC; ++i) {
+      for (int i = 0; i < NMR; ++i) {
         const int q = slotq(i);
         if (q >= 0) {
           float4 pw = *reinterpret_cast<float4*>(W + 4 * q);
@@ -989,7 +1069,9 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
         }
       }
     }
-    __syncthreads();
+    // (WB: no barrier — each wave updated exactly the parameters its next forward reads before
+    // the tile's barrier #0, spl_wb_quad)
+    if constexpr (!WB) __syncthreads();
     mark(6);   // AdamW (OWN: the new weights into LDS)
   }
   // ---- write back: role 0's first workgroup the trunk + head 0, role 1's the critic head (OWN:
@@ -1003,7 +1085,7 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
   }
   if (gt == 0) {
     if constexpr (!OWN) {
-      for (int i = 0; i < NQC; ++i) {
+      for (int i = 0; i < NMR; ++i) {
         const int q = slotq(i);
         if (q >= 0 && (role == 0 ? q < QH : q >= QH)) {
           *reinterpret_cast<float4*>(args.params + 4 * q) = *reinterpret_cast<const float4*>(W + 4 * q);

@@ -38,6 +38,7 @@
 #include <float.h>
 
 #include <algorithm>
+#include <vector>
 
 #include <dlfcn.h>
 #include <string.h>
@@ -2769,6 +2770,12 @@ int upd_run(float* params, float* exp_avg, float* exp_avg_sq, float* adam_step, 
                                         : reinterpret_cast<const void*>(ppo_update_split_kernel<SPL_NQC, 2, 4, false, 4>));
     g_last_own = own ? 1 : 0;
     if (own) args.spl_tw4 = 8;   // upd_split_own checked the default slicing
+    // the 4-wave workgroup-AdamW form updates by wave-block lists (prl_ppo_split.h, WB): its clip
+    // norm always comes from the pieces (PRL_UPD_SPL_PIECES=0 applies to the other forms only)
+    if (tw == 4 && !own) {
+      args.spl_pieces = 1;
+      PRL_REQUIRE(spl_wb_check(args.net), "prl_ppo_update: the wave-block AdamW lists do not cover the net");
+    }
     plan = UpdPlan{k, tw, 1};
   }
   // replicated tiles: the latency form on one GPU only; the split form: two roles per tile group

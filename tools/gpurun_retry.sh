@@ -5,7 +5,7 @@ out=$1; lim=$2; cmd=$3
 for i in $(seq 1 20); do
   /usr/local/graft/bin/gpurun --timeout "$lim" -- "$cmd" > "$out" 2>&1
   rc=$?
-  if [ $rc -ne 3 ] && ! grep -q "no free box right now" "$out"; then break; fi
+  if [ $rc -ne 3 ] && ! grep -q -e "no free box right now" -e "slot(s) on this pod are busy" -e "status=transient" "$out"; then break; fi
   sleep 120
 done
 echo "gpurun rc=$rc after $i tries" >> "$out"
