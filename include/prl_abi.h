@@ -488,6 +488,12 @@ int32_t prl_ppo_update_set_split(int32_t mode);
  * data-parallel caller's vote (every rank must launch the same kernel form).  No reference
  * counterpart. */
 int32_t prl_ppo_update_dp_split(int32_t D, int32_t A, int32_t discrete, int32_t mini_batch);
+/* Host-only check (no GPU): 1 when the head-split kernel's wave-block AdamW lists
+ * (csrc/prl_ppo_split.h spl_wb_quad: wave b of role h updates, and publishes, the parameter quads
+ * its own next forward reads before the tile's first barrier) cover every quad role h owns
+ * exactly once for this shape, else 0.  The launch refuses a shape that fails it.  No reference
+ * counterpart (tests). */
+int32_t prl_ppo_update_wb_check(int32_t D, int32_t A, int32_t discrete);
 /* Test utility: fill every CU's LDS with `value` (LDS is not cleared between launches; a kernel
  * that reads LDS it did not write in its own launch sees the previous launch's contents).  No
  * reference counterpart. */

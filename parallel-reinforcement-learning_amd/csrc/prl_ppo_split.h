@@ -37,15 +37,38 @@
 constexpr int SPL_NW = 4;
 constexpr int SPL_CQ = 4;   // quads per norm piece (spl_piece)
 
+// The trunk's forward of channel block b (H0^T = W0 X^T, GroupNorm + SiLU) for one tile's
+// inputs: F block b into the LDS tile Fs, the normalised values and 1 / std kept for the backward.
+template <int KSM>
+__device__ __forceinline__ void spl_trunk_fwd(const UpdNet& n, const float* W, const UpdScr& sc,
+                                              const float (&xin)[KSM], upd_v4& xh0, float& r0) {
+  const int l = threadIdx.x & 63, x = l & 15, q = l >> 4, b = threadIdx.x >> 6;
+  const int D = n.D, KS = (D + 3) >> 2;
+  upd_v4 acc = {0.f, 0.f, 0.f, 0.f}, Fw;
+  const float* wr = W + n.w0.lds + (16 * b + x) * n.w0.stride;
+#pragma unroll
+  for (int s = 0; s < KSM; ++s) {
+    if (s < KS) {
+      const int d = 4 * s + q;
+      acc = upd_mma(d < D ? wr[d] : 0.0f, xin[s], acc);
+    }
+  }
+  upd_gn_fwd_frag(acc, upd_ld4(W + n.g0.lds + 16 * b + 4 * q), upd_ld4(W + n.b0.lds + 16 * b + 4 * q), xh0, r0,
+                  Fw);
+  upd_st4(sc.Fs + x * UPD_ZS + 16 * b + 4 * q, Fw);
+}
+
 // one 16-row tile of role r = head h (h = r): forward (trunk + head h), the head's loss, its
 // backward through the trunk; the gradient into the LDS image Ga (first tile of the step: every
 // entry the role publishes is stored, never accumulated, since a split workgroup runs ONE tile
-// per step).  Three workgroup barriers.
-template <int KA, int TW>
+// per step).  Three workgroup barriers.  PRE: the trunk's forward ran already (spl_trunk_fwd at
+// the end of the previous step's AdamW, WB form): its Fs block is in LDS, xh0 / r0 are given.
+template <int KA, int TW, bool PRE = false>
 __device__ __forceinline__ void spl_tile(const UpdNet& n, const UpdArgs& args, int h, const float* W,
                                          float* Ga, const UpdScr& sc, const UpdIn<upd_ksm<KA>()>& in,
                                          int rc, float invB, unsigned long long* tm, bool direct,
-                                         __amdgpu_buffer_rsrc_t rs_mypart) {
+                                         __amdgpu_buffer_rsrc_t rs_mypart, upd_v4 pxh0 = upd_v4{},
+                                         float pr0 = 0.f) {
   constexpr int KSM = upd_ksm<KA>();
   const int t = threadIdx.x, l = t & 63, x = l & 15, q = l >> 4, w = t >> 6;
   if (TW > SPL_NW && w >= SPL_NW) {   // the tile's three barriers, nothing else
@@ -69,21 +92,13 @@ __device__ __forceinline__ void spl_tile(const UpdNet& n, const UpdArgs& args, i
   const UpdHead hi = upd_head_info(n, h);
   const int oc = hi.oc, no = hi.no;
   // ---- forward: trunk block b (H0^T = W0 X^T, GroupNorm + SiLU), every wave its own block
-  upd_v4 Fw, xh0, xh, G;
+  upd_v4 xh0, xh, G;
   float r0, rh;
-  {
-    upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* wr = W + n.w0.lds + (16 * b + x) * n.w0.stride;
-#pragma unroll
-    for (int s = 0; s < KSM; ++s) {
-      if (s < KS) {
-        const int d = 4 * s + q;
-        acc = upd_mma(d < D ? wr[d] : 0.0f, in.xin[s], acc);
-      }
-    }
-    upd_gn_fwd_frag(acc, upd_ld4(W + n.g0.lds + 16 * b + 4 * q), upd_ld4(W + n.b0.lds + 16 * b + 4 * q),
-                    xh0, r0, Fw);
-    upd_st4(sc.Fs + x * UPD_ZS + 16 * b + 4 * q, Fw);
+  if constexpr (PRE) {
+    xh0 = pxh0;
+    r0 = pr0;
+  } else {
+    spl_trunk_fwd<KSM>(n, W, sc, in.xin, xh0, r0);
   }
   __syncthreads();   // #0: Fs
   {
@@ -551,14 +566,17 @@ __device__ __forceinline__ void spl_helper(const UpdArgs& args, int g, int Qtot,
 // reads only the parameters of its own channel block — W0 rows 16b .. 16b + 15, γ0 / β0 block b,
 // the head's W1 rows 16b .. 16b + 15, γ1 / β1 block b, W2 columns 16b .. 16b + 15 — and every
 // other parameter read comes after barrier #0.  So when wave b's AdamW updates exactly those
-// quads (wave 0 also the head's output biases, read after barrier #1), no workgroup barrier is
+// quads (wave 1 also the head's output biases, read after barrier #1), no workgroup barrier is
 // needed between AdamW and the next step's tile: a wave goes from its last AdamW slot straight
-// into its forward.  List k of (role h, wave b) -> parameter quad (-1 past its end); lane l
+// into its forward.  The same lists are what each wave WRITES into the tile's gradient image
+// (spl_tile: dW2 / γ1 β1 / dW1 / γ0 β0 / dW0 of its block; wave 1 the output biases), so each
+// wave also publishes its own list straight after its tile, without a workgroup barrier in front
+// (the loss partials' words go out from the waves that form them: 2 and 3).  List k of (role h, wave b) -> parameter quad (-1 past its end); lane l
 // holds entries l + 64 i (SPL_WBQ slots; the host checks the length).  W1 / W2 padding columns
 // (zero gradient, zero moments: they stay 0) are not listed.
 constexpr int SPL_WBQ = 5;
 __host__ __device__ constexpr int spl_wb_len(const UpdNet& n, int h, int b) {
-  return 4 * n.w0.stride + 8 + 16 * UPD_H / 4 + 8 + 4 * n.out[h] + (b == 0 ? (n.out[h] + 3) / 4 : 0);
+  return 4 * n.w0.stride + 8 + 16 * UPD_H / 4 + 8 + 4 * n.out[h] + (b == 1 ? (n.out[h] + 3) / 4 : 0);
 }
 __host__ __device__ __forceinline__ int spl_wb_quad(const UpdNet& n, int h, int b, int k) {
   const int s0 = 4 * n.w0.stride;   // W0 rows 16b .. 16b + 15: 16 stride floats, contiguous
@@ -578,7 +596,7 @@ __host__ __device__ __forceinline__ int spl_wb_quad(const UpdNet& n, int h, int 
   const int no = h == 0 ? n.out[0] : n.out[1];
   if (k < 4 * no) return ((h == 0 ? n.w2[0].lds : n.w2[1].lds) + (k >> 2) * UPD_HS + 16 * b) / 4 + (k & 3);
   k -= 4 * no;
-  if (b == 0 && k < (no + 3) / 4) return (h == 0 ? n.b2[0].lds : n.b2[1].lds) / 4 + k;
+  if (b == 1 && k < (no + 3) / 4) return (h == 0 ? n.b2[0].lds : n.b2[1].lds) / 4 + k;
   return -1;
 }
 // Host check (once per net shape, prl_ppo_update): role h's four lists cover every quad the
@@ -770,8 +788,29 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
     for (int q = W1lo + t; q < W1hi; q += SPL_NT) st4_sc1(rs_mypart, (size_t)q * 4, float4{0.f, 0.f, 0.f, 0.f});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  if constexpr (WB) {
+    // the per-wave publish never writes the W1 / W2 padding quads nor the loss quad's other
+    // words: this workgroup's partial regions start at zero (drained before any publish)
+    const float4 z = {0.f, 0.f, 0.f, 0.f};
+    if (role == 0) {
+      for (int q = t; q < QH; q += SPL_NT) st4_sc1(rs_part, ((size_t)gt * Qtot + q) * 4, z);
+      if (t == 0) st4_sc1(rs_part, ((size_t)gt * Qtot + Qp) * 4, z);
+    } else {
+      for (int q = QH + t; q < Qp; q += SPL_NT) st4_sc1(rs_part, ((size_t)gt * Qtot + q) * 4, z);
+      for (int q = t; q <= QT; q += SPL_NT) st4_sc1(rs_part2, ((size_t)gt * (QT + 1) + q) * 4, z);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   float loss_last = 0.f;
   const SplSlice& slc = slc0;
+  // WB: the trunk's forward of the NEXT step's tile runs inside this step's AdamW (right after
+  // slot 0, which holds the wave's W0 block and γ0 / β0: spl_wb_quad), beside the other slots'
+  // updates; the first step's here.  (Fs is free: its last reader, dW1, is behind the tile's
+  // barriers; the next tile reads it after its barrier #0.)
+  upd_v4 nxh0 = {0.f, 0.f, 0.f, 0.f};
+  float nr0 = 0.f;
+  if constexpr (WB) spl_trunk_fwd<KSM>(n, W, sc, upd_in_real(nin).xin, nxh0, nr0);
   // the AdamW arithmetic of one quad (the engine's 4-wave scalar form): clipped gradient g4 * c
   auto adamw_quad = [&](const float4 g4, float4& m4, float4& v4, float4& pw, float clipc) {
     const float step_size = s_adam[0];
@@ -814,15 +853,13 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       const UpdIn<KSM> cur = upd_in_real(nin);
       // prefetch the next step's tile under this one and the hand-offs
       tile_load(jn, rows_of(Bn), nin);
-      spl_tile<KA, TW>(n, args, role, W, Ga, sc, cur, myrows, invB, tm, direct, rs_mypart);
+      spl_tile<KA, TW, WB>(n, args, role, W, Ga, sc, cur, myrows, invB, tm, direct, rs_mypart, nxh0, nr0);
     } else {
       for (int k = t; k < Lp + 4; k += SPL_NT) Ga[k] = 0.0f;
       tile_load(jn, rows_of(Bn), nin);
     }
     j = jn;
     Bj = Bn;
-    __syncthreads();
-    mark(0);   // phase A compute
     // (direct and rows this step: the dW1 quads are in the partial already; with no rows they
     // are published from the zeroed image like the rest)
     const bool skip = direct && myrows > 0;
@@ -830,11 +867,35 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
       if (!(skip && q >= W1lo && q < W1hi))
         st4_sc1(rs_part, ((size_t)gt * Qtot + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
     };
-    if (role == 0) {
+    if (WB && myrows > 0) {
+      // WB: each wave publishes its own list from the image entries it wrote itself (no
+      // workgroup barrier in front); the loss words from waves 2 (k = role) and 3 (k = 2, actor)
+      upd_wave_sync();
+      mark(0);   // phase A compute (wave 0)
+#pragma unroll
+      for (int i = 0; i < SPL_WBQ; ++i) {
+        const int q = wq[i];
+        if (q >= 0 && !(skip && q >= W1lo && q < W1hi)) {
+          const float4 v = *reinterpret_cast<const float4*>(Ga + 4 * q);
+          if (role == 1 && q < QT) st4_sc1(rs_part2, ((size_t)gt * (QT + 1) + q) * 4, v);
+          else st4_sc1(rs_part, ((size_t)gt * Qtot + q) * 4, v);
+        }
+      }
+      const int w = t >> 6;
+      if ((t & 63) == 0 && (w == 2 || (w == 3 && role == 0))) {
+        const int k = w == 3 ? 2 : role;
+        if (role == 0) st1_sc1(rs_part, (int)(((size_t)gt * Qtot + Qp) * 4) + k, Ga[Lp + k]);
+        else st1_sc1(rs_part2, (int)(((size_t)gt * (QT + 1) + QT) * 4) + k, Ga[Lp + k]);
+      }
+    } else if (role == 0) {
+      __syncthreads();
+      mark(0);   // phase A compute
       const int qe = QH;   // trunk + head 0
       for (int q = t; q < qe; q += SPL_NT) pub(q);
       if (t == 0) st4_sc1(rs_part, ((size_t)gt * Qtot + Qp) * 4, *reinterpret_cast<const float4*>(Ga + Lp));
     } else {
+      __syncthreads();
+      mark(0);   // phase A compute
       for (int q = QH + t; q < Qp; q += SPL_NT) pub(q);
       for (int q = t; q < QT; q += SPL_NT)
         st4_sc1(rs_part2, ((size_t)gt * (QT + 1) + q) * 4, *reinterpret_cast<const float4*>(Ga + 4 * q));
@@ -1066,6 +1127,12 @@ __device__ __forceinline__ void ppo_split_body(const UpdNet& n, const UpdArgs& a
           mreg[i] = m4;
           vreg[i] = v4;
           *reinterpret_cast<float4*>(W + 4 * q) = pw;
+        }
+        if constexpr (WB) {
+          if (i == 0) {   // slot 0 holds the trunk forward's parameters (this wave's own writes)
+            upd_wave_sync();
+            spl_trunk_fwd<KSM>(n, W, sc, upd_in_real(nin).xin, nxh0, nr0);
+          }
         }
       }
     }

@@ -2870,6 +2870,12 @@ extern "C" int32_t prl_ppo_update_dp_split(int32_t D, int32_t A, int32_t discret
   return upd_split_host(n, Gt, R, false) ? 1 : 0;   // (data-parallel launches never take tp)
 }
 
+extern "C" int32_t prl_ppo_update_wb_check(int32_t D, int32_t A, int32_t discrete) {
+  UpdNet n;
+  if (!upd_layout(D, A, discrete, n)) return 0;
+  return spl_wb_check(n) ? 1 : 0;
+}
+
 extern "C" void prl_ppo_update_last_plan(int32_t out[8]) {
   for (int i = 0; i < 8; ++i) out[i] = g_last_plan[i];
 }

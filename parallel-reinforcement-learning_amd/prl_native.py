@@ -90,6 +90,7 @@ SIGNATURES = {
     "prl_ppo_update_set_tp": [_I32],
     "prl_ppo_update_set_repl": [_I32],
     "prl_ppo_update_set_split": [_I32],
+    "prl_ppo_update_wb_check": [_I32, _I32, _I32],
     "prl_ppo_update_dp_split": [_I32, _I32, _I32, _I32],
     "prl_debug_fill_lds": [_F32, _P],
     "prl_ppo_update_last_plan": [_P],
@@ -118,6 +119,7 @@ _RESTYPES = {"prl_last_error": ctypes.c_char_p, "prl_source_id": ctypes.c_char_p
              "prl_rnd_pred_grad_ws_floats": _I64, "prl_dp_xbuf_bytes": _I64,
              "prl_dp_set_spin_limit": ctypes.c_uint32, "prl_ppo_update_set_tp": _I32,
              "prl_ppo_update_set_repl": _I32, "prl_ppo_update_set_split": _I32,
+             "prl_ppo_update_wb_check": _I32,
              "prl_ppo_update_dp_split": _I32,
              "prl_ppo_image_floats": _I64, "prl_colsum_partial_floats": _I64}
 
@@ -155,7 +157,14 @@ def lib():
                                        "parallel-reinforcement-learning_amd/csrc/build.py")
                 L = ctypes.CDLL(LIB_PATH)
                 for name, args in SIGNATURES.items():
-                    fn = getattr(L, name)
+                    try:
+                        fn = getattr(L, name)
+                    except AttributeError:
+                        # an explicit PRL_HIP_LIB (an older build for a same-box A/B) may lack
+                        # symbols added since; the in-tree library must export every one
+                        if "PRL_HIP_LIB" in os.environ:
+                            continue
+                        raise
                     fn.argtypes = args
                     fn.restype = _RESTYPES.get(name, ctypes.c_int)
                 if L.prl_abi_version() != ABI_VERSION:

@@ -22,7 +22,7 @@ def test_abi_library_exports_every_declared_symbol():
     import prl_native
     L = prl_native.lib()
     syms = _declared_symbols()
-    assert len(syms) == len(prl_native.SIGNATURES) == 69
+    assert len(syms) == len(prl_native.SIGNATURES) == 70
     for s in syms:
         assert hasattr(L, s), s
         assert s in prl_native.SIGNATURES, f"{s} has no ctypes signature"
@@ -42,6 +42,18 @@ def test_abi_host_calls_without_gpu():
     assert prl_native.lib().prl_workspace_bytes(99, 10) == -1
     with pytest.raises(RuntimeError, match="unknown env kind"):
         prl_native.env_dims(7)
+
+
+def test_split_wave_block_lists_cover_the_net():
+    """The head-split kernel's wave-block AdamW / publish lists (csrc/prl_ppo_split.h
+    spl_wb_quad) partition each role's parameter quads (trunk + its head, padding aside) among
+    its four waves, within the moment slots a lane holds: checked on the host for the CartPole
+    shape the kernel runs (D 4, A 2, discrete), and refused for a shape it does not."""
+    import prl_native
+    L = prl_native.lib()
+    assert L.prl_ppo_update_wb_check(4, 2, 1) == 1
+    assert L.prl_ppo_update_wb_check(64, 8, 1) == 0      # W0 blocks past the 5 slots per lane
+    assert L.prl_ppo_update_wb_check(3, 1, 0) == 0       # three heads: not a split-form shape
 
 
 def test_product_refuses_cpu_tensors():
