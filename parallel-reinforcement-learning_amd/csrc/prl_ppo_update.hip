@@ -352,6 +352,10 @@ __device__ inline bool upd_wait(unsigned* ctr, int which, unsigned target) {
 // first minibatch's ratio is still exactly 1.
 __device__ inline float upd_exp(float x) { return __expf(x); }
 __device__ inline float upd_log(float x) { return __logf(x); }
+// log of a clamped probability (x in [FLT_EPSILON, 1 - FLT_EPSILON], or NaN): no denormal / inf
+// cases, so v_log_f32 (log2) times ln 2 alone — __logf's lowering adds a denormal rescale and an
+// extra-precision ln 2 split around it, ~9 dependent instructions on the actor's loss chain
+__device__ inline float upd_log_unit(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
 __device__ inline float upd_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ inline float upd_sigmoid(float y) { return upd_rcp(1.0f + upd_exp(-y)); }
 
@@ -473,9 +477,11 @@ __device__ inline void upd_row_dist(const UpdNet& n, const OT& O, const float* a
     for (int k = 0; k < UPD_MAXA; ++k) {
       d.q[k] = d.p[k] * rS2;
       if (k < A) {
-        const float c = d.q[k] < FLT_EPSILON ? FLT_EPSILON
-                                             : (d.q[k] > 1.0f - FLT_EPSILON ? 1.0f - FLT_EPSILON : d.q[k]);
-        const float l = upd_log(c);
+        // torch's clamp(probs, eps, 1 - eps), NaN propagated; branch-free (a select per bound, the
+        // log always evaluated: no per-branch constant folding into divergent code)
+        const float qk = d.q[k];
+        const float c = qk != qk ? qk : fminf(fmaxf(qk, FLT_EPSILON), 1.0f - FLT_EPSILON);
+        const float l = upd_log_unit(c);
         d.H += l * d.q[k];
         if (k == d.ai) { la = l; d.qa = d.q[k]; }
       }
@@ -902,17 +908,27 @@ __device__ inline void upd_tile_outputs_reg(const UpdNet& n, const float* W, con
 #pragma unroll
     for (int j4 = 0; j4 < 4; ++j4) {
       if (4 * j4 < n.nout) {
-        upd_v4 v = upd_ld4(sc.Op + (0 * 16 + x) * 16 + 4 * j4);
+        // every wave's partial and the biases read first, all in flight together (one LDS round
+        // trip on the loss's critical path: the scheduler otherwise chained them one by one under
+        // the kernel's register pressure), then summed in wave order
+        upd_v4 pv[NW];
+        float bz[4];
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) pv[ww] = upd_ld4(sc.Op + (ww * 16 + x) * 16 + 4 * j4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bz[e] = 4 * j4 + e < n.nout ? W[upd_bias_of(n, 4 * j4 + e)] : 0.f;
+        __builtin_amdgcn_sched_barrier(0);
+        upd_v4 v = pv[0];
 #pragma unroll
         for (int ww = 1; ww < NW; ++ww) {
-          const upd_v4 p = upd_ld4(sc.Op + (ww * 16 + x) * 16 + 4 * j4);
+          const upd_v4 p = pv[ww];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += p[e];
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int j = 4 * j4 + e;
-          O[j] = j < n.nout ? v[e] + W[upd_bias_of(n, j)] : 0.f;
+          O[j] = j < n.nout ? v[e] + bz[e] : 0.f;
         }
       }
     }
