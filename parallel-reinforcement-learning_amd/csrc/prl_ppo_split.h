@@ -161,30 +161,35 @@ __device__ __forceinline__ void spl_tile(const UpdNet& n, const UpdArgs& args, i
   upd_wave_sync();
   SPL_CMARK(2)
   {
-    // dW2_h[j][16b + x] = sum_rows dO[row][oc + j] G[row][16b + x]
-    upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
+    // dW2_h[j][16b + x] = sum_rows dO[row][oc + j] G[row][16b + x]; dG^T block b = W2_h^T dO_h^T
+    // (K = the head's outputs) — every operand (and γ1 / β1) read first, in flight together
+    float oa[4], tb[4], ga[UPD_MAXA / 4], gb[UPD_MAXA / 4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const float a = x < no ? dOw[(4 * s + q) * 16 + oc + x] : 0.0f;
-      acc = upd_mma(a, Tw[(4 * s + q) * 16 + x], acc);
+      oa[s] = x < no ? dOw[(4 * s + q) * 16 + oc + x] : 0.0f;
+      tb[s] = Tw[(4 * s + q) * 16 + x];
     }
+#pragma unroll
+    for (int s = 0; s < UPD_MAXA / 4; ++s) {
+      const int j = 4 * s + q;
+      ga[s] = j < no ? W[hi.w2 + j * UPD_HS + 16 * b + x] : 0.0f;
+      gb[s] = j < no ? dOw[x * 16 + oc + j] : 0.0f;
+    }
+    const upd_v4 g1w = upd_ld4(W + hi.g1 + 16 * b + 4 * q), b1w = upd_ld4(W + hi.b1 + 16 * b + 4 * q);
+    __builtin_amdgcn_sched_barrier(0);
+    upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = upd_mma(oa[s], tb[s], acc);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (4 * q + i < no) Ga[hi.w2 + (4 * q + i) * UPD_HS + 16 * b + x] = acc[i];
-    // dG^T block b = W2_h^T dO_h^T (K = the head's outputs), GroupNorm + SiLU backward -> dZ
+    // GroupNorm + SiLU backward -> dZ
     upd_v4 dg = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < UPD_MAXA / 4; ++s) {
-      if (4 * s < no) {
-        const int j = 4 * s + q;
-        const float a = j < no ? W[hi.w2 + j * UPD_HS + 16 * b + x] : 0.0f;
-        const float bb = j < no ? dOw[x * 16 + oc + j] : 0.0f;
-        dg = upd_mma(a, bb, dg);
-      }
-    }
+    for (int s = 0; s < UPD_MAXA / 4; ++s)
+      if (4 * s < no) dg = upd_mma(ga[s], gb[s], dg);
     upd_v4 dy;
-    const upd_v4 dz = upd_gn_bwd_frag(dg, xh, upd_ld4(W + hi.g1 + 16 * b + 4 * q),
-                                      upd_ld4(W + hi.b1 + 16 * b + 4 * q), rh, dy);
+    const upd_v4 dz = upd_gn_bwd_frag(dg, xh, g1w, b1w, rh, dy);
     upd_st4(sc.Zs + x * UPD_ZS + 16 * b + 4 * q, dz);
     upd_v4 dyx;
 #pragma unroll
@@ -208,22 +213,34 @@ __device__ __forceinline__ void spl_tile(const UpdNet& n, const UpdArgs& args, i
 #pragma unroll
     for (int sg = 0; sg < 4; ++sg) zb[sg] = upd_ld4(Zh + 16 * sg + 4 * q);
     upd_v4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+    float wa[16];   // (the A operands read first, in flight together with zb: see dW1 below)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) wa[s] = Wh[(16 * (s & 3) + 4 * q + (s >> 2)) * UPD_HS];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const int o = 16 * (s & 3) + 4 * q + (s >> 2);
-      if (s & 1) d1 = upd_mma(Wh[o * UPD_HS], zb[s & 3][s >> 2], d1);
-      else d0 = upd_mma(Wh[o * UPD_HS], zb[s & 3][s >> 2], d0);
+      if (s & 1) d1 = upd_mma(wa[s], zb[s & 3][s >> 2], d1);
+      else d0 = upd_mma(wa[s], zb[s & 3][s >> 2], d0);
     }
     // ---- dW1_h[16b + 4q + i][16bb + x] = sum_rows dZ[row][16b + 4q + i] F[row][16bb + x]:
     //      independent of dF, issued behind it
     upd_v4 acc[4];
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) acc[bb] = upd_v4{0.f, 0.f, 0.f, 0.f};
+    // every operand read first, in flight together (the scheduler otherwise issued them two by two
+    // between the MFMAs, one LDS round trip per pair under the kernel's register pressure)
+    float za[4], fb[4][4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const float a = sc.Zs[(4 * s + q) * UPD_ZS + 16 * b + x];
+      za[s] = sc.Zs[(4 * s + q) * UPD_ZS + 16 * b + x];
 #pragma unroll
-      for (int bb = 0; bb < 4; ++bb) acc[bb] = upd_mma(a, sc.Fs[(4 * s + q) * UPD_ZS + 16 * bb + x], acc[bb]);
+      for (int bb = 0; bb < 4; ++bb) fb[s][bb] = sc.Fs[(4 * s + q) * UPD_ZS + 16 * bb + x];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) acc[bb] = upd_mma(za[s], fb[s][bb], acc[bb]);
     }
     upd_v4 dF;
 #pragma unroll
@@ -263,9 +280,15 @@ __device__ __forceinline__ void spl_tile(const UpdNet& n, const UpdArgs& args, i
       if (16 * e < D) {
         upd_v4 a0 = {0.f, 0.f, 0.f, 0.f};
         const int d = 16 * e + x;
+        float ta[4], xb[4];   // (operands read first, in flight together)
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-          a0 = upd_mma(Tw[(4 * s + q) * 16 + x], d < D ? sc.Xs[(4 * s + q) * sc.XS + d] : 0.0f, a0);
+        for (int s = 0; s < 4; ++s) {
+          ta[s] = Tw[(4 * s + q) * 16 + x];
+          xb[s] = d < D ? sc.Xs[(4 * s + q) * sc.XS + d] : 0.0f;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) a0 = upd_mma(ta[s], xb[s], a0);
         if (d < D) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) Ga[n.w0.lds + (16 * b + 4 * q + i) * n.w0.stride + d] = a0[i];
