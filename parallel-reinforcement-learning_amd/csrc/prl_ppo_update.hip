@@ -1124,11 +1124,15 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
       const float* Th = Tw + slot * UPD_RT * 16;
       // dW2_h[j][16b + x] += sum_rows dO[row][oc + j] G_h[row][ch]  (G_h transposed via Th)
       upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
+      float oa[4], tb[4];   // (every operand read first, in flight together)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const float a = x < no ? dOw[(4 * s + q) * 16 + oc + x] : 0.0f;
-        acc = upd_mma(a, Th[(4 * s + q) * 16 + x], acc);
+        oa[s] = x < no ? dOw[(4 * s + q) * 16 + oc + x] : 0.0f;
+        tb[s] = Th[(4 * s + q) * 16 + x];
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = upd_mma(oa[s], tb[s], acc);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if constexpr (RG) {
@@ -1184,12 +1188,18 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
         upd_v4 acc[4];
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) acc[bb] = CHAIN ? gr.w1(h, bb) : upd_v4{0.f, 0.f, 0.f, 0.f};
+        float za[4], fb[4][4];   // (every operand read first, in flight together)
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const float a = Zh[(4 * s + q) * UPD_ZS + 16 * b + x];
+          za[s] = Zh[(4 * s + q) * UPD_ZS + 16 * b + x];
 #pragma unroll
-          for (int bb = 0; bb < 4; ++bb)
-            acc[bb] = upd_mma(a, sc.Fs[(4 * s + q) * UPD_ZS + 16 * bb + x], acc[bb]);
+          for (int bb = 0; bb < 4; ++bb) fb[s][bb] = sc.Fs[(4 * s + q) * UPD_ZS + 16 * bb + x];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb) acc[bb] = upd_mma(za[s], fb[s][bb], acc[bb]);
         }
         if constexpr (CHAIN) {
 #pragma unroll
@@ -1226,11 +1236,14 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
           upd_v4 zb[4];
 #pragma unroll
           for (int sg = 0; sg < 4; ++sg) zb[sg] = upd_ld4(Zh + 16 * sg + 4 * q);
+          float wa[16];   // (the A operands read first, in flight together with zb)
+#pragma unroll
+          for (int s = 0; s < 16; ++s) wa[s] = Wh[(16 * (s & 3) + 4 * q + (s >> 2)) * UPD_HS];
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int s = 0; s < 16; ++s) {
-            const int o = 16 * (s & 3) + 4 * q + (s >> 2);
-            if (s & 1) d1 = upd_mma(Wh[o * UPD_HS], zb[s & 3][s >> 2], d1);
-            else d0 = upd_mma(Wh[o * UPD_HS], zb[s & 3][s >> 2], d0);
+            if (s & 1) d1 = upd_mma(wa[s], zb[s & 3][s >> 2], d1);
+            else d0 = upd_mma(wa[s], zb[s & 3][s >> 2], d0);
           }
         }
       }
@@ -1262,9 +1275,15 @@ __device__ void upd_tile(const UpdNet& n, const UpdArgs& args, const float* W, f
       if (16 * e < D) {
         upd_v4 acc = {0.f, 0.f, 0.f, 0.f};
         const int d = 16 * e + x;
+        float ta[4], xb[4];   // (operands read first, in flight together)
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-          acc = upd_mma(Tw[(4 * s + q) * 16 + x], d < D ? sc.Xs[(4 * s + q) * sc.XS + d] : 0.0f, acc);
+        for (int s = 0; s < 4; ++s) {
+          ta[s] = Tw[(4 * s + q) * 16 + x];
+          xb[s] = d < D ? sc.Xs[(4 * s + q) * sc.XS + d] : 0.0f;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = upd_mma(ta[s], xb[s], acc);
         if constexpr (RG) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) gr.w0(e)[i] += acc[i];
